@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric on MI355X:
+   "MLUPS (Jacobi smoother) + V-cycle wall-time, 512^3 fp64; achieved HBM GB/s %peak".
+
+A step = one fused damped-Jacobi sweep (residual + update, 7-point stencil, fp64, LINEAR mode) over
+level 0 of the 512^3 grid of BASELINE config #3, i.e. one pass of the hot path over 512^3 lattice
+updates; value = lattice updates of all ranks / max-over-ranks wall time (MLUPS). Inputs are
+resident in HBM before the timed region. The V-cycle wall time (512^3, 2+2, including the 8-byte
+norm readback) is measured after the timed region and reported under "vcycle".
+
+Multi-GPU (torchrun, one process per GPU): weak scaling, every rank owns 512^3 lattice points.
+
+Roofline: the smoother is HBM-bound (0.5 flop/B); algorithmic bytes = 24 B per lattice update
+(read v, read f, write v_new) x 512^3 per launch / average launch duration measured
+with HIP events on the solver's stream; peak = 8000 GB/s (MI355X HBM3E, MI355X_MICROARCH.md).
+cpu_baseline: the reference's own CpuSolver::jacobi (oracle/_ref/ref_probe, compiled from
+/root/reference/src/cpu) on this host's cores, a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "gpu-solve_amd"))
+
+import gpusolve as gsv  # noqa: E402
+
+PEAK_GBPS = 8000.0
+BYTES_PER_LUP = 24.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=512, help="per-rank cube edge (BASELINE config #3: 512)")
+    ap.add_argument("--vcycles", type=int, default=5, help="timed V-cycles after one warm-up cycle (0: skip)")
+    ap.add_argument("--cpu-sweeps", type=int, default=6, help="cpu_baseline sample size (0: skip)")
+    ap.add_argument("--cpu-vcycles", type=int, default=1, help="cpu_baseline V-cycles (0: skip)")
+    return ap.parse_args()
+
+
+def pmc_traffic(n):
+    """HBM bytes per launch of the smoother from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(REPO, "profiles", "pmc_smoother.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if int(d.get("n", -1)) == n:
+            return float(d["hbm_bytes_per_launch"]), d
+    except (OSError, ValueError, KeyError):
+        pass
+    return None, None
+
+
+def cpu_baseline(n, sweeps, vcycles):
+    """Reference CPU smoother on this host (kind "reference"); falls back to the oracle port."""
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_probe")
+    port = os.path.join(REPO, "oracle", "build", "gso_cli")
+    exe, kind = (ref, "reference") if os.path.exists(ref) else (port, "port")
+    if not os.path.exists(exe):
+        return None
+    env = dict(os.environ)
+    threads = int(env.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    env["OMP_NUM_THREADS"] = str(threads)
+    env.setdefault("OMP_PROC_BIND", "close")
+    out = {"unit": "MLUPS", "cores": threads, "kind": kind}
+    r = subprocess.run([exe, "time_jacobi", str(n), str(n), str(n), "0", str(sweeps)], capture_output=True,
+                       text=True, env=env, timeout=600)
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    out["value"] = round(float(j["mlups"]), 3)
+    out["sample"] = (f"{sweeps} level-0 Jacobi sweeps (CpuSolver::jacobi, residual+update) of the {n}^3 linear "
+                     f"grid after 1 warm-up sweep, {threads} OpenMP threads")
+    if vcycles > 0:
+        r = subprocess.run([exe, "time_vcycle", str(n), str(n), str(n), "0", str(vcycles)], capture_output=True,
+                           text=True, env=env, timeout=900)
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+        out["vcycle_ms"] = round(float(j["ms_per_cycle"]), 1)
+        out["sample"] += f"; {vcycles} 2+2 V-cycle(s) after 1 warm-up cycle"
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+        out["cpu_model"] = model
+    except (OSError, IndexError):
+        pass
+    return out
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    n = a.n
+    params = gsv.GridParams(maxiter=1, tol=0.0, gridDim=(n, n, n), mode=gsv.GS_LINEAR, preSmoothing=2,
+                            postSmoothing=2)
+    grid = gsv.HipGridData(params)
+    drv = gsv.driver()
+    stream = torch.cuda.ExternalStream(grid.stream())
+
+    def sweep():
+        rc = drv.gs_grid_jacobi(grid.handle, 0, 1)
+        if rc:
+            raise gsv.GpuSolveError(drv.gs_last_error().decode())
+
+    for _ in range(a.warmup):
+        sweep()
+    grid.sync()
+    barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        sweep()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / a.steps  # average launch duration on the solver's stream
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+
+    lups_per_rank = float(n) ** 3
+    total_lups = lups_per_rank * a.steps * world
+    value = total_lups / elapsed / 1e6
+    achieved = BYTES_PER_LUP * lups_per_rank / (kernel_ms * 1e-3) / 1e9
+    traffic, pmc = pmc_traffic(n)
+
+    vc = None
+    if a.vcycles > 0:
+        res = gsv.HipSolver.vcycle(grid)  # warm-up (first touch of every level)
+        barrier()
+        import ctypes as C
+        ms, last = C.c_double(), C.c_double()
+        rc = drv.gs_grid_time_vcycles(grid.handle, a.vcycles, C.byref(ms), C.byref(last))
+        if rc:
+            raise gsv.GpuSolveError(drv.gs_last_error().decode())
+        vt = torch.tensor([ms.value / a.vcycles], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(vt, op=dist.ReduceOp.MAX)
+        vc = {"ms": round(vt.item(), 3), "cycles": a.vcycles, "config": f"{n}^3 linear 2+2, norm readback included",
+              "first_residual": res}
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_sweeps > 0:
+        try:
+            cpu = cpu_baseline(n, a.cpu_sweeps, a.cpu_vcycles)
+        except Exception as e:  # the baseline is reported, never required
+            cpu = {"error": str(e)}
+
+    if rank == 0:
+        line = {
+            "metric": "MLUPS (Jacobi smoother) + V-cycle wall-time, 512³ fp64; achieved HBM GB/s %peak",
+            "value": round(value, 1),
+            "unit": "MLUPS",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (analytic RHS of the reference, v0 = 0)",
+            "config": {"workload": f"{n}^3 linear 7-point fused Jacobi sweep (level 0), BASELINE config #3",
+                       "grid_per_rank": [n, n, n], "mode": "linear", "omega": 0.8,
+                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_GBPS, 4),
+                         "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
+                         "algorithmic_bytes_per_launch": BYTES_PER_LUP * lups_per_rank},
+            "vcycle": vc,
+            "cpu_baseline": cpu,
+            "kernel_build": gsv.build_info(),
+        }
+        if pmc:
+            line["roofline"]["traffic_source"] = pmc.get("source")
+        print(json.dumps(line), flush=True)
+    grid.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

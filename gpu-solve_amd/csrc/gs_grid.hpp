@@ -1,0 +1,114 @@
+// gs_grid.hpp — device-resident level hierarchy (HipGridData) and the V-cycle / Newton drivers.
+//
+// Mirrors the reference backend contract:
+//   CpuGridData  (src/cpu/CpuGridData.{h,cpp})  -> gs::HipGridData
+//   CpuSolver    (src/cpu/CpuSolver.{h,cpp})     -> gs::HipSolver   (solve, restrict public)
+//   NewtonSolver (src/cpu/NewtonSolver.{h,cpp})  -> gs::NewtonSolver
+// All fields live in HBM for the whole solve; the only device->host traffic per V-cycle is the
+// 8-byte residual norm.
+#pragma once
+#include <array>
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "gpusolve_hip.h"
+#include "gs_params.hpp"
+
+namespace gs {
+
+void check(int code, const char* what); // throws gs::Error with gs_strerror(code)
+
+// One padded fp64 field in the pitched x-fastest layout of include/gpusolve_hip.h.
+class DeviceField {
+public:
+    DeviceField() = default;
+    DeviceField(int64_t nx, int64_t ny, int64_t nz, hipStream_t s); // zero-filled
+    ~DeviceField();
+    DeviceField(const DeviceField&) = delete;
+    DeviceField& operator=(const DeviceField&) = delete;
+    DeviceField(DeviceField&& o) noexcept { *this = std::move(o); }
+    DeviceField& operator=(DeviceField&& o) noexcept;
+
+    double* data() const { return origin_; }
+    int64_t ldy() const { return ldy_; }
+    int64_t ldz() const { return ldz_; }
+    int64_t span() const { return span_; } // elements from origin covering every padded point
+    explicit operator bool() const { return base_ != nullptr; }
+    void zero(hipStream_t s);
+    void swap(DeviceField& o) noexcept;
+
+private:
+    double* base_ = nullptr;
+    double* origin_ = nullptr;
+    int64_t ldy_ = 0, ldz_ = 0, span_ = 0, alloc_ = 0;
+};
+
+struct StreamGuard {
+    hipStream_t s = nullptr;
+    StreamGuard();
+    ~StreamGuard();
+};
+
+class HipGridData final : public GridParams {
+public:
+    struct LevelData {
+        DeviceField v;       // current iterate
+        DeviceField vAlt;    // Jacobi ping-pong partner (the fused sweep reads v, writes vAlt)
+        DeviceField restV;   // restricted v (FAS)
+        DeviceField newtonV; // Newton linearisation point
+        DeviceField f;       // right-hand side
+        DeviceField r;       // residual (restriction source)
+        std::array<std::size_t, 3> levelDim{};
+        double h = 0.0;
+        gs_level geom{};     // kernel-side geometry
+    };
+
+    explicit HipGridData(const GridParams& grid);
+    ~HipGridData();
+
+    LevelData& getLevel(std::size_t l) { return levels_[l]; }
+    const LevelData& getLevel(std::size_t l) const { return levels_[l]; }
+    std::size_t numLevels() const { return levels_.size(); }
+
+    DeviceField newtonF;  // Newton: the original right-hand side (src/cpu/CpuGridData.h:36)
+    gs_stencil stencilAbi{};
+    hipStream_t stream() const { return stream_.s; }
+
+    // residual-norm plumbing: per-block partials, device scalar, pinned host scalar
+    double* partials() const { return partials_; }
+    double* dNorm() const { return dNorm_; }
+    double readNorm(); // async D2H of dNorm + stream sync: the one host sync per V-cycle
+
+private:
+    std::vector<LevelData> levels_;
+    StreamGuard stream_;
+    double* partials_ = nullptr;
+    double* dNorm_ = nullptr;
+    double* hNorm_ = nullptr;
+};
+
+class HipSolver {
+public:
+    static void solve(HipGridData& grid);
+    static void restrict(HipGridData& grid, const DeviceField& src, std::size_t srcLevel, DeviceField& dst);
+
+    // exposed for benchmarks / the C ABI
+    static double compResidual(HipGridData& grid, std::size_t level, bool storeR, bool norm);
+    static double vcycle(HipGridData& grid);
+    static void jacobi(HipGridData& grid, std::size_t level, std::size_t sweeps);
+
+    // solve() records its residual history here when non-null (initial, then one per V-cycle)
+    static thread_local std::vector<double>* history;
+};
+
+class NewtonSolver {
+public:
+    static void solve(HipGridData& grid);
+    static double compF(HipGridData& grid);
+    static void findError(HipGridData& grid);
+    static thread_local std::vector<double>* history;
+};
+
+} // namespace gs

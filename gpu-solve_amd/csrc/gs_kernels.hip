@@ -1,0 +1,599 @@
+// gs_kernels.hip — CDNA4 (gfx950) HIP kernels of the GMG V-cycle + the extern "C" launchers
+// declared in include/gpusolve_hip.h.
+//
+// Numerics follow the reference CPU backend operator by operator (src/cpu/CpuSolver.cpp,
+// src/cpu/NewtonSolver.cpp, src/cpu/CpuGridData.cpp of Bricktricker/gpu-solve): every expression
+// keeps the reference's evaluation order and the library is built with -ffp-contract=off, so in
+// LINEAR mode every field is bit-identical to the CPU path; only the l2-norm summation order
+// (deterministic here: fixed per-block partials + fixed-order finish) and, in the non-linear
+// modes, ocml's exp vs glibc's exp (<= 1 ulp) differ.
+//
+// Layout: x unit-stride, z slowest (include/gpusolve_hip.h), so Z-slabs are contiguous planes and
+// a wave64 row load along x is one coalesced 1 KiB (dwordx4 per lane) access.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "gpusolve_hip.h"
+
+namespace {
+
+constexpr int WAVE = 64;
+
+// ---------------------------------------------------------------------------------------------
+// Stencil coefficients by value (they land in SGPRs).
+struct Coef {
+    double s[7];
+    double hh;     // h*h
+    double omega;
+    double gamma;
+    double alpha;  // h*h / s0          (CpuSolver.cpp:145)
+    double preFac; // s0 / (h*h)        (CpuSolver.cpp:144)
+    int64_t off[7]; // generic kernel: linear element offsets of the 7 entries
+};
+
+bool canonical_order(const gs_stencil* S)
+{
+    static const int cx[7] = {0, 1, -1, 0, 0, 0, 0};
+    static const int cy[7] = {0, 0, 0, 1, -1, 0, 0};
+    static const int cz[7] = {0, 0, 0, 0, 0, 1, -1};
+    for (int i = 0; i < 7; i++)
+        if (S->ox[i] != cx[i] || S->oy[i] != cy[i] || S->oz[i] != cz[i]) return false;
+    return true;
+}
+
+bool valid_stencil(const gs_stencil* S)
+{
+    for (int i = 0; i < 7; i++)
+        if (S->ox[i] < -1 || S->ox[i] > 1 || S->oy[i] < -1 || S->oy[i] > 1 || S->oz[i] < -1 || S->oz[i] > 1)
+            return false;
+    return true;
+}
+
+Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamma)
+{
+    Coef k;
+    for (int i = 0; i < 7; i++) {
+        k.s[i] = S->s[i];
+        k.off[i] = S->ox[i] + S->oy[i] * L->ldy + S->oz[i] * L->ldz;
+    }
+    k.hh = L->h * L->h;
+    k.omega = omega;
+    k.gamma = gamma;
+    k.alpha = k.hh / S->s[0];
+    k.preFac = S->s[0] / k.hh;
+    return k;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Point formulas (reference evaluation order; built with -ffp-contract=off).
+
+// stencil sum in config order, then /h^2 and the non-linear term  — CpuSolver.cpp:56-76
+template <int MODE>
+__device__ __forceinline__ double op_value(const Coef& k, double c, double xp, double xm, double yp, double ym,
+                                           double zp, double zm, double w)
+{
+    double s = 0.0;
+    s += k.s[0] * c;
+    s += k.s[1] * xp;
+    s += k.s[2] * xm;
+    s += k.s[3] * yp;
+    s += k.s[4] * ym;
+    s += k.s[5] * zp;
+    s += k.s[6] * zm;
+    s /= k.hh;
+    if (MODE == GS_NEWTON) {
+        const double ew = exp(w);
+        s += k.gamma * (1 + w) * c * ew;
+    } else if (MODE == GS_NONLINEAR) {
+        const double ev = exp(c);
+        const double nl = k.gamma * c * ev;
+        s += nl;
+    }
+    return s;
+}
+
+// Jacobi point update from the old value and its residual — CpuSolver.cpp:157-171
+template <int MODE>
+__device__ __forceinline__ double jacobi_update(const Coef& k, double v, double r, double w)
+{
+    if (MODE == GS_LINEAR) return v + k.omega * (k.alpha * r);
+    const double u = (MODE == GS_NONLINEAR) ? v : w;
+    const double eu = exp(u);
+    const double den = k.preFac + k.gamma * (1 + u) * eu;
+    return v + k.omega * (r / den);
+}
+
+__device__ __forceinline__ double wave_sum(double x)
+{
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) x += __shfl_down(x, o, WAVE);
+    return x;
+}
+
+// Block-wide fixed-order sum; result valid in thread 0. nwaves <= 16.
+template <int NWAVES>
+__device__ __forceinline__ double block_sum(double x, double* lds)
+{
+    const int tid = threadIdx.x + threadIdx.y * blockDim.x;
+    x = wave_sum(x);
+    if ((tid & (WAVE - 1)) == 0) lds[tid / WAVE] = x;
+    __syncthreads();
+    double t = 0.0;
+    if (tid == 0) {
+#pragma unroll
+        for (int i = 0; i < NWAVES; i++) t += lds[i];
+    }
+    return t;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Canonical-stencil pass, z-marching: block = 64 x 4 threads, each lane owns 2 consecutive
+// x-points (one dwordx4), each wave one y-row; the block walks ZC planes keeping v(z-1), v(z),
+// v(z+1) of its own points in registers (the next plane is prefetched one step ahead), the
+// in-plane x/y neighbours come through L1/L2.
+//   KIND 0: Jacobi sweep         out = v_new
+//   KIND 1: residual             out = r (nullable), partials = per-block sum r^2 (nullable)
+//   KIND 2: FAS coarse operator  out = A(u) (ADD=false) or out += A(u) (ADD=true)
+constexpr int ZM_TXP = 2;
+constexpr int ZM_TX = WAVE * ZM_TXP; // 128
+constexpr int ZM_TY = 4;
+constexpr int ZM_ZC = 32;
+
+template <int MODE, int KIND, bool ADD>
+__global__ __launch_bounds__(256) void k_zmarch(Coef k, const double* __restrict__ v, const double* __restrict__ f,
+                                                const double* __restrict__ w, double* __restrict__ out,
+                                                double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
+                                                int64_t ldz)
+{
+    __shared__ double red[ZM_TY];
+    const int lane = threadIdx.x;
+    const int x = 1 + blockIdx.x * ZM_TX + ZM_TXP * lane;
+    const int y = 1 + blockIdx.y * ZM_TY + threadIdx.y;
+    const int zb = 1 + blockIdx.z * ZM_ZC;
+    const int ze = min(zb + ZM_ZC - 1, nz);
+    const bool act = (x <= nx) && (y <= ny);
+    const bool two = act && (x + 1 <= nx);
+
+    double sumsq = 0.0;
+    if (act) {
+        const int64_t row = x + (int64_t)y * ldy;
+        const double* vp = v + row;
+        double2 vm = *reinterpret_cast<const double2*>(vp + (int64_t)(zb - 1) * ldz);
+        double2 vc = *reinterpret_cast<const double2*>(vp + (int64_t)zb * ldz);
+        double2 vn = *reinterpret_cast<const double2*>(vp + (int64_t)(zb + 1) * ldz);
+        for (int z = zb; z <= ze; z++) {
+            const int64_t p = row + (int64_t)z * ldz;
+            // prefetch plane z+2 (always inside the padded array while z+2 <= nz+1)
+            double2 vnn = vn;
+            if (z + 2 <= nz + 1) vnn = *reinterpret_cast<const double2*>(v + p + 2 * ldz);
+            const double xm = v[p - 1];
+            const double xp = v[p + 2];
+            const double2 ym = *reinterpret_cast<const double2*>(v + p - ldy);
+            const double2 yp = *reinterpret_cast<const double2*>(v + p + ldy);
+            double2 wv = make_double2(0.0, 0.0);
+            if (MODE == GS_NEWTON) wv = *reinterpret_cast<const double2*>(w + p);
+            double2 fv = make_double2(0.0, 0.0);
+            if (KIND != 2 || ADD) fv = *reinterpret_cast<const double2*>((KIND == 2 ? out : f) + p);
+
+            const double a0 = op_value<MODE>(k, vc.x, vc.y, xm, yp.x, ym.x, vn.x, vm.x, wv.x);
+            const double a1 = op_value<MODE>(k, vc.y, xp, vc.x, yp.y, ym.y, vn.y, vm.y, wv.y);
+            double o0, o1;
+            if (KIND == 0) {
+                o0 = jacobi_update<MODE>(k, vc.x, fv.x - a0, wv.x);
+                o1 = jacobi_update<MODE>(k, vc.y, fv.y - a1, wv.y);
+            } else if (KIND == 1) {
+                o0 = fv.x - a0;
+                o1 = fv.y - a1;
+                sumsq += o0 * o0;
+                if (two) sumsq += o1 * o1;
+            } else {
+                o0 = ADD ? fv.x + a0 : a0;
+                o1 = ADD ? fv.y + a1 : a1;
+            }
+            if (KIND != 1 || out) {
+                if (two) *reinterpret_cast<double2*>(out + p) = make_double2(o0, o1);
+                else out[p] = o0;
+            }
+            vm = vc;
+            vc = vn;
+            vn = vnn;
+        }
+    }
+    if (KIND == 1 && partials) {
+        const double t = block_sum<ZM_TY>(sumsq, red);
+        if (threadIdx.x == 0 && threadIdx.y == 0)
+            partials[blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z)] = t;
+    }
+}
+
+dim3 zm_grid(const gs_level* L)
+{
+    return dim3((unsigned)((L->nx + ZM_TX - 1) / ZM_TX), (unsigned)((L->ny + ZM_TY - 1) / ZM_TY),
+                (unsigned)((L->nz + ZM_ZC - 1) / ZM_ZC));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic-stencil pass (any 7 offsets in {-1,0,1}^3, any order): one point per thread.
+constexpr int GN_BX = 64, GN_BY = 4;
+
+template <int MODE, int KIND, bool ADD>
+__global__ __launch_bounds__(256) void k_generic(Coef k, const double* __restrict__ v, const double* __restrict__ f,
+                                                 const double* __restrict__ w, double* __restrict__ out,
+                                                 double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
+                                                 int64_t ldz)
+{
+    __shared__ double red[GN_BY];
+    const int x = 1 + blockIdx.x * GN_BX + threadIdx.x;
+    const int y = 1 + blockIdx.y * GN_BY + threadIdx.y;
+    const int z = 1 + blockIdx.z;
+    double sumsq = 0.0;
+    if (x <= nx && y <= ny) {
+        const int64_t p = x + y * ldy + (int64_t)z * ldz;
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 7; i++) s += k.s[i] * v[p + k.off[i]];
+        s /= k.hh;
+        const double c = v[p];
+        const double wv = (MODE == GS_NEWTON) ? w[p] : 0.0;
+        if (MODE == GS_NEWTON) {
+            const double ew = exp(wv);
+            s += k.gamma * (1 + wv) * c * ew;
+        } else if (MODE == GS_NONLINEAR) {
+            const double ev = exp(c);
+            const double nl = k.gamma * c * ev;
+            s += nl;
+        }
+        if (KIND == 0) {
+            out[p] = jacobi_update<MODE>(k, c, f[p] - s, wv);
+        } else if (KIND == 1) {
+            const double r = f[p] - s;
+            sumsq = r * r;
+            if (out) out[p] = r;
+        } else {
+            out[p] = ADD ? out[p] + s : s;
+        }
+    }
+    if (KIND == 1 && partials) {
+        const double t = block_sum<GN_BY>(sumsq, red);
+        if (threadIdx.x == 0 && threadIdx.y == 0)
+            partials[blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z)] = t;
+    }
+}
+
+dim3 gn_grid(const gs_level* L)
+{
+    return dim3((unsigned)((L->nx + GN_BX - 1) / GN_BX), (unsigned)((L->ny + GN_BY - 1) / GN_BY), (unsigned)L->nz);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deterministic finish of the per-block partial sums: one block, fixed strided order.
+constexpr int FIN_T = 1024;
+__global__ __launch_bounds__(FIN_T) void k_sumsq_finish(const double* __restrict__ partials, int64_t n,
+                                                        double* __restrict__ out, int accumulate)
+{
+    __shared__ double red[FIN_T / WAVE];
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += FIN_T) s += partials[i];
+    const double t = block_sum<FIN_T / WAVE>(s, red);
+    if (threadIdx.x == 0) *out = accumulate ? t : sqrt(t);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 27-point full weighting (CpuSolver.cpp:211-238): coarse interior point per thread, terms summed
+// with ii outermost, kk innermost. The weights are exact powers of two.
+__global__ __launch_bounds__(256) void k_restrict(const double* __restrict__ fine, double* __restrict__ ca,
+                                                  double* __restrict__ cb, int cnx, int cny, int cnz, int64_t fldy,
+                                                  int64_t fldz, int64_t cldy, int64_t cldz)
+{
+    const int x = 1 + blockIdx.x * 64 + threadIdx.x;
+    const int y = 1 + blockIdx.y * 4 + threadIdx.y;
+    const int z = 1 + blockIdx.z;
+    if (x > cnx || y > cny) return;
+    const double* c0 = fine + 2 * x + (int64_t)(2 * y) * fldy + (int64_t)(2 * z) * fldz;
+    double acc = 0.0;
+#pragma unroll
+    for (int a = -1; a <= 1; a++)
+#pragma unroll
+        for (int b = -1; b <= 1; b++)
+#pragma unroll
+            for (int c = -1; c <= 1; c++) {
+                const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) * ((2.0 - (b < 0 ? -b : b)) / 2.0) *
+                                   ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                acc += wgt * c0[a + b * fldy + c * fldz];
+            }
+    const int64_t q = x + y * cldy + (int64_t)z * cldz;
+    ca[q] = acc;
+    if (cb) cb[q] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Trilinear prolongation, closed form per fine point (the reference's inject + X, Y, Z passes,
+// CpuSolver.cpp:240-290, combined in the same X -> Y -> Z order). Fine index P-1 is never written by
+// the reference (stays 0) and coarse index Pc-1 is the zero boundary, so along each axis:
+//   i even -> c(i/2);  i odd -> 0.5*c(i/2) + 0.5*c(i/2+1).
+template <bool SUB>
+__device__ __forceinline__ double coarse_at(const double* __restrict__ c, const double* __restrict__ sub, int64_t q)
+{
+    return SUB ? c[q] - sub[q] : c[q];
+}
+
+template <bool SUB>
+__device__ __forceinline__ double prolong_value(const double* __restrict__ c, const double* __restrict__ sub, int x,
+                                                int y, int z, int64_t cldy, int64_t cldz)
+{
+    const int cx = x >> 1, cy = y >> 1, cz = z >> 1;
+    const bool ox = x & 1, oy = y & 1, oz = z & 1;
+    auto X = [&](int jy, int jz) -> double {
+        const int64_t q = cx + jy * cldy + (int64_t)jz * cldz;
+        const double a = coarse_at<SUB>(c, sub, q);
+        if (!ox) return a;
+        const double b = coarse_at<SUB>(c, sub, q + 1);
+        return 0.5 * a + 0.5 * b;
+    };
+    auto Y = [&](int jz) -> double {
+        const double a = X(cy, jz);
+        if (!oy) return a;
+        const double b = X(cy + 1, jz);
+        return 0.5 * a + 0.5 * b;
+    };
+    const double a = Y(cz);
+    if (!oz) return a;
+    const double b = Y(cz + 1);
+    return 0.5 * a + 0.5 * b;
+}
+
+template <bool SUB>
+__global__ __launch_bounds__(256) void k_prolong_add(const double* __restrict__ c, const double* __restrict__ sub,
+                                                     double* __restrict__ fv, int fnx, int fny, int fnz, int64_t fldy,
+                                                     int64_t fldz, int64_t cldy, int64_t cldz)
+{
+    const int x = 1 + blockIdx.x * 64 + threadIdx.x;
+    const int y = 1 + blockIdx.y * 4 + threadIdx.y;
+    const int z = 1 + blockIdx.z;
+    if (x > fnx || y > fny) return;
+    const int64_t p = x + y * fldy + (int64_t)z * fldz;
+    fv[p] = fv[p] + prolong_value<SUB>(c, sub, x, y, z, cldy, cldz);
+}
+
+// Unfused reference-shaped interpolate (whole padded fine array), used by parity tests.
+__global__ __launch_bounds__(256) void k_interpolate(const double* __restrict__ c, double* __restrict__ e, int fPx,
+                                                     int fPy, int fPz, int64_t fldy, int64_t fldz, int64_t cldy,
+                                                     int64_t cldz)
+{
+    const int x = blockIdx.x * 64 + threadIdx.x;
+    const int y = blockIdx.y * 4 + threadIdx.y;
+    const int z = blockIdx.z;
+    if (x >= fPx || y >= fPy) return;
+    const int64_t p = x + y * fldy + (int64_t)z * fldz;
+    if (x == fPx - 1 || y == fPy - 1 || z == fPz - 1) {
+        e[p] = 0.0;
+        return;
+    }
+    e[p] = prolong_value<false>(c, nullptr, x, y, z, cldy, cldz);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Level-0 right-hand side, CpuGridData.cpp:7-12, 44-78 (same expression order).
+__device__ __forceinline__ double rhs_f0(double x)
+{
+    return 100 * x * (x - 1.0) * x * (x - 1.0) * x * (x - 1.0) * x * (x - 1.0);
+}
+__device__ __forceinline__ double rhs_f2(double x)
+{
+    return 100.0 * 4.0 * (x - 1.0) * (x - 1.0) * x * x * (14.0 * x * x - 14.0 * x + 3);
+}
+
+__global__ __launch_bounds__(256) void k_rhs(double* __restrict__ f, int mode, double h, double gamma, int nx, int ny,
+                                             int nz, int64_t z0, int64_t ldy, int64_t ldz)
+{
+    const int X = blockIdx.x * 64 + threadIdx.x; // padded indices
+    const int Y = blockIdx.y * 4 + threadIdx.y;
+    const int Z = blockIdx.z;
+    if (X > nx + 1 || Y > ny + 1) return;
+    const int64_t p = X + Y * ldy + (int64_t)Z * ldz;
+    const int64_t Zg = Z + z0;
+    if (mode == GS_LINEAR) {
+        if (X < 1 || X > nx || Y < 1 || Y > ny || Z < 1 || Z > nz) return;
+        const double x = (int)(X - 1) * h, y = (int)(Y - 1) * h, z = (int)(Zg - 1) * h;
+        f[p] = -(rhs_f2(x) * rhs_f0(y) * rhs_f0(z) + rhs_f0(x) * rhs_f2(y) * rhs_f0(z) +
+                 rhs_f0(x) * rhs_f0(y) * rhs_f2(z));
+    } else {
+        const double x = (int)X * h, y = (int)Y * h, z = (int)Zg * h;
+        const double ux = x - x * x, uy = y - y * y, uz = z - z * z;
+        f[p] = 2.0 * ((y - y * y) * (z - z * z) + (x - x * x) * (z - z * z) + (x - x * x) * (y - y * y)) +
+               gamma * ux * uy * uz * exp(ux * uy * uz);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_axpy(double* __restrict__ y, const double* __restrict__ x, double a,
+                                              int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (a == 1.0) y[i] = y[i] + x[i];
+        else if (a == -1.0) y[i] = y[i] - x[i];
+        else y[i] = y[i] + a * x[i];
+    }
+}
+
+int launch_status()
+{
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+bool bad_level(const gs_level* L)
+{
+    return !L || L->nx < 0 || L->ny < 0 || L->nz < 0 || L->ldy < L->nx + 2 || L->ldz < L->ldy * (L->ny + 2) ||
+           L->nx > INT32_MAX / 2 || L->ny > INT32_MAX / 2 || L->nz > INT32_MAX / 2;
+}
+
+// Dispatch a stencil pass over (mode, kind) to the fast or the generic kernel.
+template <int KIND, bool ADD>
+int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma, const double* v,
+                const double* f, const double* w, double* out, double* partials, hipStream_t st)
+{
+    if (!S || bad_level(L) || !valid_stencil(S) || !v) return GS_EINVAL;
+    if (mode < GS_LINEAR || mode > GS_NEWTON) return GS_EINVAL;
+    if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
+    const Coef k = make_coef(S, L, omega, gamma);
+    const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
+    if (canonical_order(S)) {
+        const dim3 g = zm_grid(L), b(WAVE, ZM_TY);
+#define GS_ZM(M) hipLaunchKernelGGL((k_zmarch<M, KIND, ADD>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
+        if (mode == GS_LINEAR) GS_ZM(GS_LINEAR);
+        else if (mode == GS_NONLINEAR) GS_ZM(GS_NONLINEAR);
+        else GS_ZM(GS_NEWTON);
+#undef GS_ZM
+    } else {
+        const dim3 g = gn_grid(L), b(GN_BX, GN_BY);
+#define GS_GN(M) hipLaunchKernelGGL((k_generic<M, KIND, ADD>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
+        if (mode == GS_LINEAR) GS_GN(GS_LINEAR);
+        else if (mode == GS_NONLINEAR) GS_GN(GS_NONLINEAR);
+        else GS_GN(GS_NEWTON);
+#undef GS_GN
+    }
+    return launch_status();
+}
+
+} // namespace
+
+// =============================================================================================
+extern "C" {
+
+int gs_field_layout(int64_t nx, int64_t ny, int64_t nz, int64_t* ldy, int64_t* ldz, int64_t* alloc_elems,
+                    int64_t* origin_offset)
+{
+    if (nx < 0 || ny < 0 || nz < 0 || !ldy || !ldz || !alloc_elems || !origin_offset) return GS_EINVAL;
+    // x=1 of every row 128-B aligned: pitch a multiple of 16 doubles, origin at 15 (mod 16).
+    const int64_t py = ((nx + 2 + 15) / 16) * 16;
+    *ldy = py;
+    *ldz = py * (ny + 2);
+    *origin_offset = 15;
+    *alloc_elems = *ldz * (nz + 2) + 32;
+    return 0;
+}
+
+int gs_rhs_init(const gs_level* L, double* f, int mode, double h0, double gamma, hipStream_t st)
+{
+    if (bad_level(L) || !f) return GS_EINVAL;
+    const dim3 g((unsigned)((L->nx + 2 + 63) / 64), (unsigned)((L->ny + 2 + 3) / 4), (unsigned)(L->nz + 2)), b(64, 4);
+    hipLaunchKernelGGL(k_rhs, g, b, 0, st, f, mode, h0, gamma, (int)L->nx, (int)L->ny, (int)L->nz, L->z0, L->ldy,
+                       L->ldz);
+    return launch_status();
+}
+
+int gs_jacobi_sweep(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                    const double* v_in, double* v_out, const double* f, const double* w, hipStream_t st)
+{
+    if (!v_out || !f || v_in == v_out || (mode == GS_NEWTON && !w)) return GS_EINVAL;
+    return launch_pass<0, false>(S, L, mode, omega, gamma, v_in, f, w, v_out, nullptr, st);
+}
+
+int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L)
+{
+    if (!S || !L) return 0;
+    if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 1;
+    const dim3 g = canonical_order(S) ? zm_grid(L) : gn_grid(L);
+    return (int64_t)g.x * g.y * g.z;
+}
+
+int gs_residual(const gs_stencil* S, const gs_level* L, int mode, double gamma, const double* v, const double* f,
+                const double* w, double* r, double* partials, hipStream_t st)
+{
+    if (!f || (mode == GS_NEWTON && !w)) return GS_EINVAL;
+    if (partials && (L && (L->nx == 0 || L->ny == 0 || L->nz == 0)))
+        return (int)hipMemsetAsync(partials, 0, sizeof(double), st);
+    return launch_pass<1, false>(S, L, mode, 0.0, gamma, v, f, w, r, partials, st);
+}
+
+int gs_sumsq_finish(const double* partials, int64_t n, double* out, int accumulate, hipStream_t st)
+{
+    if (!partials || !out || n < 0) return GS_EINVAL;
+    hipLaunchKernelGGL(k_sumsq_finish, dim3(1), dim3(FIN_T), 0, st, partials, n, out, accumulate);
+    return launch_status();
+}
+
+int gs_restrict2(const double* fine, const gs_level* fl, double* ca, double* cb, const gs_level* cl, hipStream_t st)
+{
+    if (!fine || !ca || bad_level(fl) || bad_level(cl)) return GS_EINVAL;
+    if (2 * cl->nx + 1 > fl->nx + 1 || 2 * cl->ny + 1 > fl->ny + 1 || 2 * cl->nz + 1 > fl->nz + 1) return GS_EINVAL;
+    if (cl->nx == 0 || cl->ny == 0 || cl->nz == 0) return 0;
+    const dim3 g((unsigned)((cl->nx + 63) / 64), (unsigned)((cl->ny + 3) / 4), (unsigned)cl->nz), b(64, 4);
+    hipLaunchKernelGGL(k_restrict, g, b, 0, st, fine, ca, cb, (int)cl->nx, (int)cl->ny, (int)cl->nz, fl->ldy, fl->ldz,
+                       cl->ldy, cl->ldz);
+    return launch_status();
+}
+
+int gs_restrict(const double* fine, const gs_level* fl, double* coarse, const gs_level* cl, hipStream_t st)
+{
+    return gs_restrict2(fine, fl, coarse, nullptr, cl, st);
+}
+
+int gs_interpolate(const double* coarse, const gs_level* cl, double* e, const gs_level* fl, hipStream_t st)
+{
+    if (!coarse || !e || bad_level(fl) || bad_level(cl)) return GS_EINVAL;
+    if ((fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 || (fl->nz + 1) / 2 > cl->nz + 1) return GS_EINVAL;
+    const dim3 g((unsigned)((fl->nx + 2 + 63) / 64), (unsigned)((fl->ny + 2 + 3) / 4), (unsigned)(fl->nz + 2)), b(64, 4);
+    hipLaunchKernelGGL(k_interpolate, g, b, 0, st, coarse, e, (int)fl->nx + 2, (int)fl->ny + 2, (int)fl->nz + 2,
+                       fl->ldy, fl->ldz, cl->ldy, cl->ldz);
+    return launch_status();
+}
+
+int gs_prolong_add(const double* coarse_v, const double* coarse_sub, const gs_level* cl, double* fine_v,
+                   const gs_level* fl, hipStream_t st)
+{
+    if (!coarse_v || !fine_v || bad_level(fl) || bad_level(cl)) return GS_EINVAL;
+    if ((fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 || (fl->nz + 1) / 2 > cl->nz + 1) return GS_EINVAL;
+    if (fl->nx == 0 || fl->ny == 0 || fl->nz == 0) return 0;
+    const dim3 g((unsigned)((fl->nx + 63) / 64), (unsigned)((fl->ny + 3) / 4), (unsigned)fl->nz), b(64, 4);
+    if (coarse_sub)
+        hipLaunchKernelGGL(k_prolong_add<true>, g, b, 0, st, coarse_v, coarse_sub, fine_v, (int)fl->nx, (int)fl->ny,
+                           (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz);
+    else
+        hipLaunchKernelGGL(k_prolong_add<false>, g, b, 0, st, coarse_v, nullptr, fine_v, (int)fl->nx, (int)fl->ny,
+                           (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz);
+    return launch_status();
+}
+
+int gs_apply_op(const gs_stencil* S, const gs_level* L, double gamma, const double* u, double* out, hipStream_t st)
+{
+    if (!out) return GS_EINVAL;
+    return launch_pass<2, false>(S, L, GS_NONLINEAR, 0.0, gamma, u, nullptr, nullptr, out, nullptr, st);
+}
+
+int gs_apply_op_add(const gs_stencil* S, const gs_level* L, double gamma, const double* u, double* f, hipStream_t st)
+{
+    if (!f) return GS_EINVAL;
+    return launch_pass<2, true>(S, L, GS_NONLINEAR, 0.0, gamma, u, nullptr, nullptr, f, nullptr, st);
+}
+
+int gs_newton_F(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* F, double* f,
+                double* partials, hipStream_t st)
+{
+    if (!f || !F) return GS_EINVAL;
+    // compF (NewtonSolver.cpp:48-81) is the NONLINEAR residual of newtonV against newtonF
+    return gs_residual(S, L, GS_NONLINEAR, gamma, w, F, nullptr, f, partials, st);
+}
+
+int gs_axpy(double* y, const double* x, double a, int64_t n, hipStream_t st)
+{
+    if (!y || !x || n < 0) return GS_EINVAL;
+    if (n == 0) return 0;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_axpy, dim3((unsigned)blocks), dim3(256), 0, st, y, x, a, n);
+    return launch_status();
+}
+
+const char* gs_strerror(int code)
+{
+    if (code == 0) return "success";
+    if (code == GS_EINVAL) return "gpusolve: invalid argument";
+    return hipGetErrorString((hipError_t)code);
+}
+
+const char* gs_build_info(void) { return "gpusolve_hip v1: zmarch(64x4,2pt/lane,zc32) + generic; fp-contract=off"; }
+
+} // extern "C"

@@ -1,0 +1,57 @@
+// gs_main.cpp — the GpuSolve-hip executable: drop-in for GpuSolve-cpu with the same CLI and stdout
+// contract (src/main.cpp:15-114): `GpuSolve-hip <path/to/config.conf>`.
+//
+//   Using config file "<path>"
+//   Solving linear|nonlinear|newton problem
+//   Inital residual: R                       (sic, CpuSolver.cpp:17)
+//   iter: i residual: R Took Tms             (CpuSolver.cpp:28 + Timer.cpp:17-26)
+//   Inital newton residual: R / newton iter: i residual: R Took Tms   (NewtonSolver.cpp:16,27)
+//
+// Exit codes as the reference: 1 for a missing/non-file config or an invalid mode; a backend
+// error prints "Exception: <what>" to stderr and exits 0 (the reference's GPU-backend behaviour,
+// src/main.cpp:96-111). Added: stencil offsets outside {-1,0,1} (out-of-bounds reads in the
+// reference) are rejected like an invalid mode.
+#include <iostream>
+#include <string>
+
+#include <hip/hip_runtime.h>
+
+#include "gs_grid.hpp"
+#include "gs_params.hpp"
+
+int main(int argc, char* argv[])
+{
+    if (argc < 2) {
+        std::cerr << "Missing config file. Usage program.exe path/to/config.conf\n";
+        return 1;
+    }
+    const std::string path = argv[1];
+    gs::GridParams gridParams;
+    // read the mode first so the "Using"/"Solving" lines come out in the reference's order
+    const gs::ConfigStatus st = gs::readConfig(path, gridParams);
+    if (st == gs::ConfigStatus::NotAFile) {
+        std::cerr << '"' << path << "\" does not exist or is not a file\n";
+        return 1;
+    }
+    std::cout << "Using config file \"" << path << "\"\n";
+    if (st == gs::ConfigStatus::InvalidMode) {
+        std::cerr << "Invalid mode\n";
+        return 1;
+    }
+    if (gridParams.mode == gs::GridParams::LINEAR) std::cout << "Solving linear problem\n";
+    else if (gridParams.mode == gs::GridParams::NONLINEAR) std::cout << "Solving nonlinear problem\n";
+    else std::cout << "Solving newton problem\n";
+    if (st == gs::ConfigStatus::BadStencil) {
+        std::cerr << "Invalid stencil offset (must be -1, 0 or 1)\n";
+        return 1;
+    }
+
+    try {
+        gs::HipGridData grid(gridParams);
+        if (gridParams.mode == gs::GridParams::NEWTON) gs::NewtonSolver::solve(grid);
+        else gs::HipSolver::solve(grid);
+    } catch (std::exception& e) {
+        std::cerr << "Exception: " << e.what() << '\n';
+    }
+    return 0;
+}

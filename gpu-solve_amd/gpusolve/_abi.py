@@ -1,0 +1,108 @@
+"""ctypes declarations of the two C ABIs (include/gpusolve_hip.h, include/gpusolve_driver.h).
+
+The shared libraries are built in-tree by gpu-solve_amd/Makefile (``__graft_entry__.build()``).
+There is no fallback: if a library is missing, loading raises ``ImportError`` naming the build step.
+"""
+import ctypes as C
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # gpu-solve_amd/
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+BIN_DIR = os.path.join(PKG_ROOT, "bin")
+KERNEL_LIB = os.path.join(LIB_DIR, "libgpusolve_hip.so")
+DRIVER_LIB = os.path.join(LIB_DIR, "libgpusolve_driver.so")
+EXECUTABLE = os.path.join(BIN_DIR, "GpuSolve-hip")
+
+GS_LINEAR, GS_NONLINEAR, GS_NEWTON = 0, 1, 2
+GS_EINVAL = 100001
+
+dptr = C.POINTER(C.c_double)
+i64 = C.c_int64
+
+
+class gs_stencil(C.Structure):
+    _fields_ = [("s", C.c_double * 7), ("ox", C.c_int * 7), ("oy", C.c_int * 7), ("oz", C.c_int * 7)]
+
+
+class gs_level(C.Structure):
+    _fields_ = [("nx", i64), ("ny", i64), ("nz", i64), ("ldy", i64), ("ldz", i64), ("z0", i64), ("h", C.c_double)]
+
+
+class gs_params(C.Structure):
+    _fields_ = [("maxiter", i64), ("tol", C.c_double), ("dims", i64 * 3), ("mode", C.c_int), ("pre", i64),
+                ("post", i64), ("omega", C.c_double), ("gamma", C.c_double), ("stencil", gs_stencil)]
+
+
+# name -> (restype, argtypes); void* is used for device pointers and streams
+KERNEL_API = {
+    "gs_field_layout": (C.c_int, [i64, i64, i64, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]),
+    "gs_rhs_init": (C.c_int, [C.POINTER(gs_level), C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p]),
+    "gs_jacobi_sweep": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double, C.c_double,
+                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gs_residual": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double, C.c_void_p,
+                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gs_residual_num_partials": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),
+    "gs_sumsq_finish": (C.c_int, [C.c_void_p, i64, C.c_void_p, C.c_int, C.c_void_p]),
+    "gs_restrict": (C.c_int, [C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.POINTER(gs_level), C.c_void_p]),
+    "gs_restrict2": (C.c_int, [C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.c_void_p, C.POINTER(gs_level),
+                               C.c_void_p]),
+    "gs_interpolate": (C.c_int, [C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.POINTER(gs_level), C.c_void_p]),
+    "gs_prolong_add": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.POINTER(gs_level),
+                                 C.c_void_p]),
+    "gs_apply_op": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
+                              C.c_void_p]),
+    "gs_apply_op_add": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
+                                  C.c_void_p]),
+    "gs_newton_F": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
+                              C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gs_axpy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_double, i64, C.c_void_p]),
+    "gs_strerror": (C.c_char_p, [C.c_int]),
+    "gs_build_info": (C.c_char_p, []),
+}
+
+DRIVER_API = {
+    "gs_parse_config": (C.c_int, [C.c_char_p, C.POINTER(gs_params)]),
+    "gs_grid_create": (C.c_void_p, [C.POINTER(gs_params)]),
+    "gs_grid_destroy": (None, [C.c_void_p]),
+    "gs_grid_solve": (C.c_int, [C.c_void_p, C.c_int, dptr, C.c_int, C.POINTER(C.c_int)]),
+    "gs_grid_vcycle": (C.c_int, [C.c_void_p, dptr]),
+    "gs_grid_jacobi": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "gs_grid_residual_norm": (C.c_int, [C.c_void_p, C.c_int, dptr]),
+    "gs_grid_num_levels": (C.c_int, [C.c_void_p]),
+    "gs_grid_level": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(gs_level)]),
+    "gs_grid_field": (C.c_void_p, [C.c_void_p, C.c_int, C.c_int]),
+    "gs_grid_stream": (C.c_void_p, [C.c_void_p]),
+    "gs_grid_download": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
+    "gs_grid_upload": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
+    "gs_grid_sync": (C.c_int, [C.c_void_p]),
+    "gs_grid_time_jacobi": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]),
+    "gs_grid_time_vcycles": (C.c_int, [C.c_void_p, C.c_int, dptr, dptr]),
+    "gs_last_error": (C.c_char_p, []),
+}
+
+_cache = {}
+
+
+def _load(path, api):
+    if path in _cache:
+        return _cache[path]
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is not built: run `make -C gpu-solve_amd` (or __graft_entry__.build())")
+    lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in api.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _cache[path] = lib
+    return lib
+
+
+def kernels():
+    """The thin C-ABI launcher library (libgpusolve_hip.so)."""
+    return _load(KERNEL_LIB, KERNEL_API)
+
+
+def driver():
+    """The host driver library (libgpusolve_driver.so); loads the kernel library first."""
+    kernels()
+    return _load(DRIVER_LIB, DRIVER_API)

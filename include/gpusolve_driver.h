@@ -1,0 +1,75 @@
+/* gpusolve_driver.h — C ABI of the GpuSolve-hip host driver (libgpusolve_driver.so).
+ *
+ * The reference's backend contract is a C++ one (a grid object + static solver functions selected
+ * at compile time, src/main.cpp:5-13,88-111). This header exposes the same objects through a
+ * plain C ABI (opaque handle, plain pointers and sizes) so non-C++ hosts (ctypes tests, bench.py,
+ * a cgo/JNI wrapper) can drive the identical code path the GpuSolve-hip executable runs:
+ *
+ *   gs_grid_create         CpuGridData(const GridParams&)   src/cpu/CpuGridData.cpp:15-79
+ *   gs_grid_solve          main's dispatch: NewtonSolver::solve (mode 2) else CpuSolver::solve
+ *                                                          src/main.cpp:88-94
+ *   gs_grid_vcycle         CpuSolver::vcycle                src/cpu/CpuSolver.cpp:85-139
+ *   gs_grid_jacobi         CpuSolver::jacobi                src/cpu/CpuSolver.cpp:141-180
+ *   gs_grid_residual_norm  CpuSolver::compResidual          src/cpu/CpuSolver.cpp:45-83
+ *
+ * Errors: functions return 0 / a non-NULL handle on success; otherwise gs_last_error() holds the
+ * message the GpuSolve-hip executable would print after "Exception: ".
+ */
+#ifndef GPUSOLVE_DRIVER_H
+#define GPUSOLVE_DRIVER_H
+
+#include <stdint.h>
+#include "gpusolve_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* GridParams (src/gridParams.h:29-47) in plain C. */
+typedef struct {
+    int64_t maxiter;
+    double tol;
+    int64_t dims[3];
+    int mode; /* GS_LINEAR / GS_NONLINEAR / GS_NEWTON */
+    int64_t pre, post;
+    double omega, gamma;
+    gs_stencil stencil;
+} gs_params;
+
+/* Parses the reference's 14-line config text. Returns 0, 1 (invalid mode), 2 (bad stencil). */
+int gs_parse_config(const char* text, gs_params* out);
+
+void* gs_grid_create(const gs_params* p); /* device-resident hierarchy on the current HIP device */
+void gs_grid_destroy(void* grid);
+
+/* Runs the solve selected by the mode. print: 0 silent, 1 reference stdout lines.
+ * Writes up to cap residual values (initial, then one per V-cycle / Newton iteration) into hist
+ * and their total count into *count. */
+int gs_grid_solve(void* grid, int print, double* hist, int cap, int* count);
+
+int gs_grid_vcycle(void* grid, double* residual);
+int gs_grid_jacobi(void* grid, int level, int sweeps);
+int gs_grid_residual_norm(void* grid, int level, double* norm);
+int gs_grid_num_levels(void* grid);
+int gs_grid_level(void* grid, int level, gs_level* out);
+/* field: 0 v (current iterate), 1 restV, 2 newtonV, 3 f, 4 r, 5 newtonF (level 0). NULL if absent. */
+double* gs_grid_field(void* grid, int level, int field);
+hipStream_t gs_grid_stream(void* grid);
+/* Synchronous copies of a whole padded field to / from a dense host array laid out
+ * [nz+2][ny+2][nx+2] (x fastest). */
+int gs_grid_download(void* grid, int level, int field, double* host);
+int gs_grid_upload(void* grid, int level, int field, const double* host);
+int gs_grid_sync(void* grid);
+
+/* Times `sweeps` level-`level` Jacobi sweeps with hipEvents on the grid's stream (after `warmup`
+ * untimed sweeps); *ms = elapsed milliseconds of the timed sweeps. */
+int gs_grid_time_jacobi(void* grid, int level, int warmup, int sweeps, float* ms);
+/* Times `cycles` V-cycles (each including its norm readback) with a host clock; *ms total. */
+int gs_grid_time_vcycles(void* grid, int cycles, double* ms, double* last_residual);
+
+const char* gs_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUSOLVE_DRIVER_H */

@@ -1,0 +1,122 @@
+/* gpusolve_hip.h — the thin C-ABI launcher of the MI355X GMG V-cycle kernels (libgpusolve_hip.so).
+ *
+ * Every entry point replaces one operator of the reference CPU backend (Bricktricker/gpu-solve,
+ * snapshot 2025-02-27; paths relative to that repository):
+ *
+ *   gs_rhs_init          CpuGridData ctor RHS fill            src/cpu/CpuGridData.cpp:44-78
+ *   gs_jacobi_sweep      CpuSolver::jacobi (one sweep)         src/cpu/CpuSolver.cpp:141-180
+ *   gs_residual          CpuSolver::compResidual (+ l2 norm)   src/cpu/CpuSolver.cpp:45-83
+ *   gs_sumsq_finish      the sqrt(sum r^2) of compResidual     src/cpu/CpuSolver.cpp:51,77,82
+ *   gs_restrict          CpuSolver::restrict                   src/cpu/CpuSolver.cpp:211-238
+ *   gs_restrict2         two restrict calls of the FAS branch  src/cpu/CpuSolver.cpp:104-107
+ *   gs_interpolate       CpuSolver::interpolate                src/cpu/CpuSolver.cpp:240-290
+ *   gs_prolong_add       interpolate + (v_c -= restV_c) + (v_f += e_f)
+ *                                                              src/cpu/CpuSolver.cpp:121-132
+ *   gs_apply_op          CpuSolver::applyStencil               src/cpu/CpuSolver.cpp:182-208
+ *   gs_apply_op_add      applyStencil then f += r (FAS)        src/cpu/CpuSolver.cpp:110-112
+ *   gs_newton_F          NewtonSolver::compF                   src/cpu/NewtonSolver.cpp:48-81
+ *   gs_axpy              Vector3::operator+= / -=              src/cpu/Vector3.cpp:34-53
+ *
+ * Conventions
+ *  - fp64 everywhere. A field of level (nx,ny,nz) is padded to (nx+2, ny+2, nz+2); element
+ *    (x,y,z), 0 <= x <= nx+1 etc., lives at ptr[x + y*ldy + z*ldz]  (x unit-stride, z slowest;
+ *    the reference's (x,y,z) semantics, not its z-fastest storage). `ptr` is the address of
+ *    padded element (0,0,0). gs_field_layout() gives the pitches and an allocation recipe that
+ *    makes every interior x=1 element 128-byte aligned (speed only; any pitch >= nx+2 is correct).
+ *  - Stencil: 7 (value, offset) pairs in config order, offsets in {-1,0,1}. The canonical order
+ *    (centre, +x, -x, +y, -y, +z, -z) of every reference config runs the LDS/register-tiled fast
+ *    kernels; any other order or shape runs a generic kernel. Sums are evaluated in config order.
+ *  - Launchers are asynchronous on `stream`, never allocate, never synchronise, are reentrant.
+ *    Scratch (residual partials) is caller-owned. Return 0 on success, else a hipError_t value
+ *    (or GS_EINVAL) — see gs_strerror().
+ *  - Boundary (padding) values of v / e / r / restV are never written and must hold 0, as on
+ *    every reference path.
+ */
+#ifndef GPUSOLVE_HIP_H
+#define GPUSOLVE_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_EINVAL 100001 /* bad argument (shape, stencil offset outside {-1,0,1}, null pointer) */
+
+enum { GS_LINEAR = 0, GS_NONLINEAR = 1, GS_NEWTON = 2 }; /* GridParams::Mode, src/gridParams.h:29-33 */
+
+/* GridParams::stencil (src/gridParams.h:7-27): values + (x,y,z) offsets, config order. */
+typedef struct {
+    double s[7];
+    int ox[7], oy[7], oz[7];
+} gs_stencil;
+
+/* One level (or one Z-slab of a level) of the hierarchy. */
+typedef struct {
+    int64_t nx, ny, nz; /* interior extents of this level; for a slab nz is the local plane count */
+    int64_t ldy, ldz;   /* element pitch of a y-row / a z-plane (ldy >= nx+2, ldz >= ldy*(ny+2)) */
+    int64_t z0;         /* global index offset of local plane 0 (0 unless Z-slab partitioned)     */
+    double h;           /* mesh width h_l = 1/(ny_l + 1)  (src/cpu/CpuGridData.cpp:41)              */
+} gs_level;
+
+/* Pitches and allocation recipe for a level with interior (nx,ny,nz): allocate alloc_elems
+ * doubles 256-B aligned and use base + origin_offset as the field pointer. */
+int gs_field_layout(int64_t nx, int64_t ny, int64_t nz, int64_t* ldy, int64_t* ldz, int64_t* alloc_elems,
+                    int64_t* origin_offset);
+
+/* Level-0 right-hand side (mode LINEAR: interior, x = (X-1)*h0; otherwise the whole padded
+ * array, x = X*h0, with gamma). h0 = 1/(Y+1) (src/main.cpp:84). */
+int gs_rhs_init(const gs_level* L, double* f, int mode, double h0, double gamma, hipStream_t stream);
+
+/* One damped-Jacobi sweep, residual and update fused: v_out = v_in + omega * D^-1 (f - A v_in).
+ * w = newtonV of this level (mode NEWTON), ignored otherwise. v_in and v_out must differ. */
+int gs_jacobi_sweep(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                    const double* v_in, double* v_out, const double* f, const double* w, hipStream_t stream);
+
+/* r = f - A(v) on the interior. r may be NULL (norm only). partials may be NULL (no norm);
+ * otherwise it receives gs_residual_num_partials(S, L) per-block sums of r^2 in a fixed order. */
+int gs_residual(const gs_stencil* S, const gs_level* L, int mode, double gamma, const double* v, const double* f,
+                const double* w, double* r, double* partials, hipStream_t stream);
+int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L);
+
+/* *out = sqrt(sum partials[0..n)) summed in a fixed order (deterministic). If accumulate is
+ * non-zero the square root is skipped and the sum is written (for cross-slab reductions). */
+int gs_sumsq_finish(const double* partials, int64_t n, double* out, int accumulate, hipStream_t stream);
+
+/* 27-point full weighting of fine onto the coarse interior. */
+int gs_restrict(const double* fine, const gs_level* fl, double* coarse, const gs_level* cl, hipStream_t stream);
+/* Same, writing two coarse outputs (FAS restV and v). */
+int gs_restrict2(const double* fine, const gs_level* fl, double* coarse_a, double* coarse_b, const gs_level* cl,
+                 hipStream_t stream);
+
+/* Trilinear prolongation of the coarse field into the fine e (whole padded fine array; index
+ * P-1 of each axis is written 0). */
+int gs_interpolate(const double* coarse, const gs_level* cl, double* e, const gs_level* fl, hipStream_t stream);
+
+/* Fused correction: fine_v(interior) += P(coarse_v - coarse_sub) (coarse_sub may be NULL). */
+int gs_prolong_add(const double* coarse_v, const double* coarse_sub, const gs_level* cl, double* fine_v,
+                   const gs_level* fl, hipStream_t stream);
+
+/* out = A(u)/h^2 + gamma*u*exp(u) on the interior (FAS coarse operator). */
+int gs_apply_op(const gs_stencil* S, const gs_level* L, double gamma, const double* u, double* out,
+                hipStream_t stream);
+/* f += A(u)/h^2 + gamma*u*exp(u) on the interior. */
+int gs_apply_op_add(const gs_stencil* S, const gs_level* L, double gamma, const double* u, double* f,
+                    hipStream_t stream);
+
+/* Newton outer residual f = F - [A(w)/h^2 + gamma*w*exp(w)] (+ partial sums of f^2 as gs_residual). */
+int gs_newton_F(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* F, double* f,
+                double* partials, hipStream_t stream);
+
+/* y[i] += a*x[i] for i < n (a = +-1 is exact: the reference's Vector3 += / -=). */
+int gs_axpy(double* y, const double* x, double a, int64_t n, hipStream_t stream);
+
+const char* gs_strerror(int code);
+/* Library build tag (kernel variant names), for logs. */
+const char* gs_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUSOLVE_HIP_H */

@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Runs oracle/_ref/ref_probe and oracle/_ref/GpuSolve-cpu — both compiled by oracle/Makefile from
+/root/reference/src/{main.cpp,Timer.cpp,cpu/*.cpp} where they lie (nothing copied) — and stores
+only data: residual histories (17 significant digits), reference stdout transcripts, level tables,
+right-hand sides and per-operator input/output fields on seeded random grids.
+
+Outputs (all data, no reference source):
+  histories.json        17-digit residual histories, keyed by case name (+ the case's config)
+  large_histories.json  the BASELINE-size anchors (511^3/512^3), a few cycles each   (--large)
+  stdout.json           6-digit reference stdout transcripts (timings stripped)
+  levels.json           level dims + h for several grid shapes
+  rhs.npz               level-0 f for linear / non-linear RHS on small grids
+  ops.npz               per-operator fixtures (inputs + outputs, reference layout (Px,Py,Pz))
+
+Usage:  python tests/golden/make_golden.py [--large]
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+PROBE = os.path.join(REPO, "oracle", "_ref", "ref_probe")
+REFEXE = os.path.join(REPO, "oracle", "_ref", "GpuSolve-cpu")
+STENCIL = "6 -1 -1 -1 -1 -1 -1\n0 1 -1 0 0 0 0\n0 0 0 1 -1 0 0\n0 0 0 0 0 1 -1\n"
+
+
+def config_text(c):
+    return (f"{c['maxiter']}\n{c['tol']}\n{c['X']}\n{c['Y']}\n{c['Z']}\n{c['mode']}\n{c['pre']}\n"
+            f"{c['post']}\n{c['omega']}\n{c['gamma']}\n" + c.get("stencil", STENCIL))
+
+
+def case(X, Y=None, Z=None, mode=0, pre=2, post=2, maxiter=10, tol=0, omega=0.8, gamma=1.0, stencil=None):
+    c = dict(X=X, Y=Y if Y is not None else X, Z=Z if Z is not None else X, mode=mode, pre=pre, post=post,
+             maxiter=maxiter, tol=tol, omega=omega, gamma=gamma)
+    if stencil:
+        c["stencil"] = stencil
+    return c
+
+
+HIST_LINE = re.compile(r"^(Inital residual|Inital newton residual|iter: \d+ residual|newton iter: \d+ residual): (\S+)")
+
+
+def run_history(c, exe=PROBE, args=("solve",)):
+    with tempfile.NamedTemporaryFile("w", suffix=".conf", delete=False) as f:
+        f.write(config_text(c))
+        path = f.name
+    try:
+        out = subprocess.run([exe, *args, path], check=True, capture_output=True, text=True).stdout
+    finally:
+        os.unlink(path)
+    return out
+
+
+def parse_history(out):
+    return [float(m.group(2)) for m in map(HIST_LINE.match, out.splitlines()) if m]
+
+
+def small_cases():
+    cases = {}
+    for n in (7, 15, 16, 31, 32, 63, 127, 128):
+        for mode in (0, 1, 2):
+            cases[f"m{mode}_n{n}_2+2"] = case(n, mode=mode, maxiter=3 if mode == 2 else 10)
+    for n in (31, 32):
+        for mode in (0, 1, 2):
+            for pre, post in ((1, 0), (3, 3), (0, 2)):
+                cases[f"m{mode}_n{n}_{pre}+{post}"] = case(n, mode=mode, pre=pre, post=post,
+                                                            maxiter=3 if mode == 2 else 6)
+    for dims in ((17, 9, 12), (31, 32, 33), (20, 33, 15), (64, 48, 40), (9, 40, 23)):
+        for mode in (0, 1, 2):
+            cases[f"m{mode}_{dims[0]}x{dims[1]}x{dims[2]}_2+2"] = case(*dims, mode=mode,
+                                                                        maxiter=3 if mode == 2 else 8)
+    # relaxation / gamma variations and early exits through `tol`
+    cases["m0_n63_w0.6"] = case(63, omega=0.6, maxiter=6)
+    cases["m1_n63_g0.5"] = case(63, mode=1, gamma=0.5, maxiter=6)
+    cases["m2_n63_g2.0"] = case(63, mode=2, gamma=2.0, maxiter=3)
+    cases["m0_n63_tol1e-3"] = case(63, tol=1e-3, maxiter=20)
+    cases["m1_n63_tol1e-4"] = case(63, mode=1, tol=1e-4, maxiter=20)
+    cases["m2_n63_tol1e-6"] = case(63, mode=2, tol=1e-6, maxiter=10)
+    # a permuted-order stencil (same operator, different summation order) and an anisotropic one
+    cases["m0_n31_permuted"] = case(31, maxiter=5, stencil="-1 -1 6 -1 -1 -1 -1\n0 -1 0 0 1 0 0\n1 0 0 0 0 0 -1\n0 0 0 -1 0 1 0\n")
+    cases["m0_n31_aniso"] = case(31, maxiter=5, stencil="4 -1 -1 -0.5 -0.5 -0.5 -0.5\n0 1 -1 0 0 0 0\n0 0 0 1 -1 0 0\n0 0 0 0 0 1 -1\n")
+    # the reference's own example (Newton 127^3, 3+3, tol 1e-5)
+    cases["example_data-2nd_order"] = case(127, mode=2, pre=3, post=3, maxiter=10, tol=1e-5)
+    return cases
+
+
+def large_cases():
+    return {
+        "m0_n511_2+2": case(511, maxiter=3),
+        "m0_n512_2+2": case(512, maxiter=3),
+        "m1_n511_2+2": case(511, mode=1, maxiter=2),
+        "m1_n512_2+2": case(512, mode=1, maxiter=2),
+        "m2_n511_2+2": case(511, mode=2, maxiter=2),
+        "m2_n512_2+2": case(512, mode=2, maxiter=2),
+    }
+
+
+def gen_histories(cases, path):
+    res = {}
+    for name, c in cases.items():
+        out = run_history(c)
+        res[name] = {"config": c, "history": parse_history(out)}
+        print(f"  {name}: {len(res[name]['history'])} values", flush=True)
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+def gen_stdout(path):
+    res = {}
+    for name, c in {"example_data-2nd_order": case(127, mode=2, pre=3, post=3, maxiter=10, tol=1e-5),
+                    "m0_n31_2+2": case(31, maxiter=5), "m1_n15_2+2": case(15, mode=1, maxiter=4),
+                    "m0_n16_diverging": case(16, maxiter=10)}.items():
+        out = run_history(c, exe=REFEXE, args=())
+        lines = [re.sub(r"Took \d+ms", "Took <T>ms", l) for l in out.splitlines()]
+        # the config path is a temp file name: keep the line shape only
+        lines = [re.sub(r'^Using config file ".*"$', 'Using config file "<PATH>"', l) for l in lines]
+        res[name] = {"config": c, "stdout": lines}
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+def gen_levels(path):
+    res = {}
+    for dims in ((7, 7, 7), (16, 16, 16), (127, 127, 127), (128, 128, 128), (512, 512, 512), (1024, 1024, 1024),
+                 (17, 9, 12), (31, 32, 33), (1023, 1023, 1023)):
+        out = subprocess.run([PROBE, "levels", *map(str, dims)], check=True, capture_output=True, text=True).stdout
+        rows = [l.split() for l in out.splitlines()]
+        res["x".join(map(str, dims))] = [[int(r[1]), int(r[2]), int(r[3]), float(r[4]), int(r[5])] for r in rows]
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+def load_field(path, dims):
+    return np.fromfile(path, dtype="<f8").reshape(dims[0] + 2, dims[1] + 2, dims[2] + 2)
+
+
+def gen_rhs(path):
+    arrs = {}
+    with tempfile.TemporaryDirectory() as td:
+        for dims in ((9, 7, 8), (16, 16, 16), (5, 11, 6)):
+            for mode, gamma in ((0, 1.0), (1, 1.0), (2, 1.0), (1, 0.5)):
+                p = os.path.join(td, "f.bin")
+                subprocess.run([PROBE, "rhs", *map(str, dims), str(mode), str(gamma), p], check=True)
+                arrs[f"f_{'x'.join(map(str, dims))}_m{mode}_g{gamma}"] = load_field(p, dims)
+    np.savez_compressed(path, **arrs)
+
+
+def level_dims(dims, lvl):
+    d = list(dims)
+    for _ in range(lvl):
+        d = [x // 2 for x in d]
+    return d
+
+
+def gen_ops(path):
+    arrs = {}
+    meta = {}
+    seed = 20250227
+    with tempfile.TemporaryDirectory() as td:
+        def run(name, dims, mode, lvl, extra=()):
+            nonlocal seed
+            seed += 1
+            for f in os.listdir(td):
+                os.unlink(os.path.join(td, f))
+            out = subprocess.run([PROBE, "op", name, *map(str, dims), str(mode), str(lvl), str(seed), td, *extra],
+                                 check=True, capture_output=True, text=True).stdout
+            key = f"{name}_{'x'.join(map(str, dims))}_m{mode}_l{lvl}" + ("_" + "_".join(extra) if extra else "")
+            info = {"name": name, "dims": list(dims), "mode": mode, "level": lvl, "seed": seed, "extra": list(extra)}
+            m = re.search(r"norm (\S+)", out)
+            if m:
+                info["norm"] = float(m.group(1))
+            for fn in sorted(os.listdir(td)):
+                base = fn[:-4]
+                if name in ("restrict",) and base == "coarse":
+                    d = level_dims(dims, lvl + 1)
+                elif name == "interpolate" and base == "coarse":
+                    d = level_dims(dims, lvl + 1)
+                elif name == "vcycle" and base.startswith("newtonV"):
+                    d = level_dims(dims, int(base[len("newtonV"):]))
+                else:
+                    d = level_dims(dims, lvl)
+                arrs[f"{key}/{base}"] = load_field(os.path.join(td, fn), d)
+            meta[key] = info
+
+        for dims in ((9, 7, 8), (16, 16, 16), (13, 6, 10)):
+            for mode in (0, 1, 2):
+                run("residual", dims, mode, 0)
+                run("jacobi", dims, mode, 0)
+                run("jacobi", dims, mode, 0, ("0.8", "1.0", "3"))
+            run("residual", dims, 0, 1)
+            run("jacobi", dims, 1, 1, ("0.7", "0.5", "2"))
+            run("restrict", dims, 0, 0)
+            run("interpolate", dims, 0, 0)
+            run("applyStencil", dims, 1, 0)
+            run("applyStencil", dims, 1, 1)
+            run("compF", dims, 2, 0)
+        for dims in ((15, 15, 15), (16, 16, 16), (17, 9, 12)):
+            for mode in (0, 1, 2):
+                run("vcycle", dims, mode, 0)
+        run("interpolate", (31, 32, 33), 0, 0)
+        run("interpolate", (32, 31, 30), 0, 1)
+        run("restrict", (31, 32, 33), 0, 0)
+        run("restrict", (32, 31, 30), 0, 1)
+    np.savez_compressed(path, **{k.replace("/", "__"): v for k, v in arrs.items()})
+    with open(path.replace(".npz", ".json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--large", action="store_true", help="also the 511^3/512^3 anchors (several minutes)")
+    ap.add_argument("--only-large", action="store_true")
+    a = ap.parse_args()
+    for exe in (PROBE, REFEXE):
+        if not os.path.exists(exe):
+            sys.exit(f"{exe} missing: run `make -C oracle ref` (needs /root/reference)")
+    if not a.only_large:
+        print("histories ...", flush=True)
+        gen_histories(small_cases(), os.path.join(HERE, "histories.json"))
+        print("stdout ...", flush=True)
+        gen_stdout(os.path.join(HERE, "stdout.json"))
+        print("levels ...", flush=True)
+        gen_levels(os.path.join(HERE, "levels.json"))
+        print("rhs ...", flush=True)
+        gen_rhs(os.path.join(HERE, "rhs.npz"))
+        print("ops ...", flush=True)
+        gen_ops(os.path.join(HERE, "ops.npz"))
+    if a.large or a.only_large:
+        print("large histories ...", flush=True)
+        gen_histories(large_cases(), os.path.join(HERE, "large_histories.json"))
+
+
+if __name__ == "__main__":
+    main()

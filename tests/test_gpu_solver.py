@@ -1,0 +1,131 @@
+"""The full GpuSolve-hip path (HipGridData + HipSolver / NewtonSolver via libgpusolve_driver.so)
+vs the reference's residual histories (tests/golden/histories.json, 17 digits from the reference
+itself) and vs the pinned CPU oracle's fields.
+
+Contract (BASELINE.json north_star): final residual norms within 1e-6 relative of src/cpu.
+Measured here much tighter: LINEAR histories to 1e-9 (only the norm's summation order differs) and
+LINEAR fields bit-identical to the oracle after whole solves."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import gpusolve as gsv  # noqa: E402
+import oracle as O  # noqa: E402
+from conftest import REPO, rel, stencil_from_text  # noqa: E402
+
+CONTRACT = 1e-6
+
+
+def params_from_case(c):
+    st = gsv.Stencil()
+    if "stencil" in c:
+        vals, offs = stencil_from_text(c["stencil"])
+        st = gsv.Stencil(vals, offs)
+    return gsv.GridParams(maxiter=c["maxiter"], tol=c["tol"], gridDim=(c["X"], c["Y"], c["Z"]), mode=c["mode"],
+                          preSmoothing=c["pre"], postSmoothing=c["post"], omega=c["omega"], gamma=c["gamma"],
+                          stencil=st)
+
+
+def tol_for(mode):
+    return 1e-9 if mode == 0 else CONTRACT
+
+
+def test_all_small_histories(histories):
+    assert torch.cuda.is_available()
+    worst = {}
+    for name, case in histories.items():
+        p = params_from_case(case["config"])
+        with gsv.HipGridData(p) as g:
+            got = gsv.HipSolver.solve(g)
+        ref = case["history"]
+        assert len(got) == len(ref), (name, got, ref)
+        for a, b in zip(got, ref):
+            assert rel(a, b) < tol_for(p.mode), (name, a, b)
+        worst[name] = max(rel(a, b) for a, b in zip(got, ref))
+    print("worst relative deviation per case:", max(worst.values()))
+
+
+@pytest.mark.parametrize("dims", [(31, 31, 31), (32, 32, 32), (17, 9, 12), (64, 48, 40), (127, 127, 127)])
+def test_linear_fields_bit_identical(dims):
+    p = gsv.GridParams(maxiter=4, tol=0.0, gridDim=dims, mode=0)
+    with gsv.HipGridData(p) as g:
+        hist = gsv.HipSolver.solve(g)
+        got = {l: g.field(l, "v") for l in range(g.numLevels())}
+    og = O.Grid(dims, mode=0, maxiter=4)
+    oh = og.solve()
+    for l, a in got.items():
+        np.testing.assert_array_equal(a, og.field(l, "v"), err_msg=f"level {l}")
+    for a, b in zip(hist, oh):
+        assert rel(a, b) < 1e-12
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_nonlinear_fields_close(mode):
+    dims = (33, 31, 29)
+    p = gsv.GridParams(maxiter=3, tol=0.0, gridDim=dims, mode=mode)
+    with gsv.HipGridData(p) as g:
+        gsv.HipSolver.solve(g)
+        v = g.field(0, "newtonV" if mode == 2 else "v")
+    og = O.Grid(dims, mode=mode, maxiter=3)
+    og.solve()
+    ref = og.field(0, "newtonV" if mode == 2 else "v")
+    assert np.abs(v - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["m0_n511_2+2", "m0_n512_2+2", "m1_n511_2+2", "m1_n512_2+2", "m2_n511_2+2",
+                                  "m2_n512_2+2"])
+def test_baseline_size_anchors(large_histories, name):
+    """BASELINE sizes (512^3) and their converging companions (511^3) against the reference."""
+    case = large_histories[name]
+    p = params_from_case(case["config"])
+    with gsv.HipGridData(p) as g:
+        got = gsv.HipSolver.solve(g)
+    ref = case["history"]
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert rel(a, b) < tol_for(p.mode), (name, a, b)
+
+
+def _norm_lines(lines):
+    out = []
+    for l in lines:
+        l = re.sub(r"Took \d+ms", "Took <T>ms", l)
+        l = re.sub(r'^Using config file ".*"$', 'Using config file "<PATH>"', l)
+        out.append(l)
+    return out
+
+
+def test_executable_stdout_contract(tmp_path):
+    """GpuSolve-hip prints the reference's stdout line for line (6-digit residuals, sic 'Inital')."""
+    from conftest import load_json
+    exe = gsv._abi.EXECUTABLE
+    assert os.path.exists(exe)
+    for name, case in load_json("stdout.json").items():
+        conf = tmp_path / f"{name}.conf"
+        conf.write_text(params_from_case(case["config"]).config_text())
+        out = subprocess.run([exe, str(conf)], capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr
+        assert _norm_lines(out.stdout.splitlines()) == case["stdout"], (name, out.stdout)
+        # the reference harness regex (runExperiments.py:46) finds every V-cycle line
+        pat = re.compile(r"iter: (\d+) residual: ([\d\.e-]+) Took (\d+)ms")
+        n_iter = sum(1 for l in case["stdout"] if re.match(r"^(newton )?iter:", l))
+        if "e+" not in out.stdout:
+            assert len(pat.findall(out.stdout)) == n_iter
+
+
+def test_example_config_verbatim():
+    ex = os.path.join(REPO, "tests", "golden", "data-2nd_order.conf")
+    out = subprocess.run([gsv._abi.EXECUTABLE, ex], capture_output=True, text=True, timeout=300)
+    lines = out.stdout.splitlines()
+    assert lines[1] == "Solving newton problem"
+    assert lines[2] == "Inital newton residual: 281.289"
+    assert [re.sub(r" Took \d+ms", "", l) for l in lines[3:]] == [
+        "newton iter: 0 residual: 12.3816", "newton iter: 1 residual: 0.527004",
+        "newton iter: 2 residual: 0.0222718", "newton iter: 3 residual: 0.00093763"]
