@@ -214,6 +214,171 @@ dim3 zm_grid(const gs_level* L)
 }
 
 // ---------------------------------------------------------------------------------------------
+// Register-blocked z-march ("rb"): each lane owns 2 consecutive x-points (one dwordx4) of RY
+// consecutive y-rows, a wave owns a 128 x RY tile, W waves stack in y, the block walks ZC planes.
+//  - y-neighbours come from the lane's own registers (plus 2 halo rows per wave and plane),
+//  - x-neighbours from the adjacent lane by a DPP wave shift (wave_shr:1 / wave_shl:1); the two
+//    tile-edge values per row are wave-uniform scalar loads,
+//  - z-neighbours are the previous / next plane held in registers,
+//  - every load of plane z+1 (next-next v rows, halo rows, f, edges) is issued before plane z is
+//    computed, so a full plane of HBM traffic is in flight behind the arithmetic.
+// Loads use a clamped column min(x, nx+1); a pair load there reads one element past the padded
+// row, which the allocation recipe of gs_field_layout (+32 elements) keeps in bounds.
+template <bool DPP>
+__device__ __forceinline__ double lane_from_left(double src, double edge)
+{
+    // lane i <- src of lane i-1; lane 0 <- edge
+    if (DPP) {
+        const long long s = __double_as_longlong(src), e = __double_as_longlong(edge);
+        const int lo = __builtin_amdgcn_update_dpp((int)e, (int)s, 0x138, 0xf, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp((int)(e >> 32), (int)(s >> 32), 0x138, 0xf, 0xf, false);
+        return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    } else {
+        const double t = __shfl_up(src, 1, WAVE);
+        return (threadIdx.x & (WAVE - 1)) == 0 ? edge : t;
+    }
+}
+
+template <bool DPP>
+__device__ __forceinline__ double lane_from_right(double src, double edge)
+{
+    // lane i <- src of lane i+1; lane 63 <- edge
+    if (DPP) {
+        const long long s = __double_as_longlong(src), e = __double_as_longlong(edge);
+        const int lo = __builtin_amdgcn_update_dpp((int)e, (int)s, 0x130, 0xf, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp((int)(e >> 32), (int)(s >> 32), 0x130, 0xf, 0xf, false);
+        return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    } else {
+        const double t = __shfl_down(src, 1, WAVE);
+        return (threadIdx.x & (WAVE - 1)) == WAVE - 1 ? edge : t;
+    }
+}
+
+__device__ __forceinline__ double2 ld2(const double* __restrict__ p) { return *reinterpret_cast<const double2*>(p); }
+
+template <int MODE, int KIND, bool ADD, int RY, int W, int ZC, bool DPP>
+__global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict__ v, const double* __restrict__ f,
+                                                 const double* __restrict__ w, double* __restrict__ out,
+                                                 double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
+                                                 int64_t ldz)
+{
+    __shared__ double red[W];
+    const int lane = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int x0 = 1 + blockIdx.x * (2 * WAVE);
+    const int x = x0 + 2 * lane;
+    const int xl = min(x, nx + 1);
+    const int y0 = 1 + (blockIdx.y * W + wv) * RY;
+    const int zb = 1 + blockIdx.z * ZC;
+    const int ze = min(zb + ZC - 1, nz);
+    const int xle = x0 - 1;
+    const int xre = min(x0 + 2 * WAVE, nx + 1);
+    const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
+    const double* fin = (KIND == 2) ? out : f;
+
+    int64_t roff[RY + 2]; // rows y0-1 .. y0+RY (clamped into the padded range)
+#pragma unroll
+    for (int r = 0; r < RY + 2; r++) roff[r] = (int64_t)min(y0 - 1 + r, ny + 1) * ldy;
+
+    double2 P[RY], C[RY + 2], N[RY], F[RY], Wc[RY];
+    double CL[RY], CR[RY];
+    double sumsq = 0.0;
+    if (zb <= ze) {
+        const int64_t zo = (int64_t)zb * ldz;
+#pragma unroll
+        for (int r = 0; r < RY; r++) {
+            P[r] = ld2(v + xl + roff[r + 1] + zo - ldz);
+            N[r] = ld2(v + xl + roff[r + 1] + zo + ldz);
+            if (KIND != 2 || ADD) F[r] = ld2(fin + xl + roff[r + 1] + zo);
+            if (MODE == GS_NEWTON) Wc[r] = ld2(w + xl + roff[r + 1] + zo);
+            CL[r] = v[xle + roff[r + 1] + zo];
+            CR[r] = v[xre + roff[r + 1] + zo];
+        }
+#pragma unroll
+        for (int r = 0; r < RY + 2; r++) C[r] = ld2(v + xl + roff[r] + zo);
+    }
+    for (int z = zb; z <= ze; z++) {
+        const int64_t zo = (int64_t)z * ldz;
+        // ---- issue every load of plane z+1 (and the v rows of plane z+2) ----
+        double2 NN[RY], H0, H1, FN[RY], WN[RY];
+        double ELn[RY], ERn[RY];
+        const bool more = z < ze;
+        if (more) {
+            const int64_t z1 = zo + ldz;
+#pragma unroll
+            for (int r = 0; r < RY; r++) {
+                NN[r] = ld2(v + xl + roff[r + 1] + z1 + ldz);
+                if (KIND != 2 || ADD) FN[r] = ld2(fin + xl + roff[r + 1] + z1);
+                if (MODE == GS_NEWTON) WN[r] = ld2(w + xl + roff[r + 1] + z1);
+                ELn[r] = v[xle + roff[r + 1] + z1];
+                ERn[r] = v[xre + roff[r + 1] + z1];
+            }
+            H0 = ld2(v + xl + roff[0] + z1);
+            H1 = ld2(v + xl + roff[RY + 1] + z1);
+        }
+        // ---- plane z ----
+#pragma unroll
+        for (int r = 0; r < RY; r++) {
+            const double2 c = C[r + 1], ym = C[r], yp = C[r + 2], zm = P[r], zp = N[r];
+            const double xm0 = lane_from_left<DPP>(c.y, CL[r]);
+            const double xp1 = lane_from_right<DPP>(c.x, CR[r]);
+            const double wx = (MODE == GS_NEWTON) ? Wc[r].x : 0.0, wy = (MODE == GS_NEWTON) ? Wc[r].y : 0.0;
+            const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
+            const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
+            double o0, o1;
+            if (KIND == 0) {
+                o0 = jacobi_update<MODE>(k, c.x, F[r].x - a0, wx);
+                o1 = jacobi_update<MODE>(k, c.y, F[r].y - a1, wy);
+            } else if (KIND == 1) {
+                o0 = F[r].x - a0;
+                o1 = F[r].y - a1;
+            } else {
+                o0 = ADD ? F[r].x + a0 : a0;
+                o1 = ADD ? F[r].y + a1 : a1;
+            }
+            const bool rowok = y0 + r <= ny;
+            if (KIND == 1) {
+                if (rowok && okx0) sumsq += o0 * o0;
+                if (rowok && okx1) sumsq += o1 * o1;
+            }
+            if (rowok && (KIND != 1 || out)) {
+                double* q = out + x + roff[r + 1] + zo;
+                if (okx1) *reinterpret_cast<double2*>(q) = make_double2(o0, o1);
+                else if (okx0) *q = o0;
+            }
+        }
+        // ---- rotate the plane window ----
+        if (more) {
+#pragma unroll
+            for (int r = 0; r < RY; r++) P[r] = C[r + 1];
+            C[0] = H0;
+            C[RY + 1] = H1;
+#pragma unroll
+            for (int r = 0; r < RY; r++) {
+                C[r + 1] = N[r];
+                N[r] = NN[r];
+                if (KIND != 2 || ADD) F[r] = FN[r];
+                if (MODE == GS_NEWTON) Wc[r] = WN[r];
+                CL[r] = ELn[r];
+                CR[r] = ERn[r];
+            }
+        }
+    }
+    if (KIND == 1 && partials) {
+        const double t = block_sum<W>(sumsq, red);
+        if (threadIdx.x == 0 && threadIdx.y == 0)
+            partials[blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z)] = t;
+    }
+}
+
+template <int RY, int W, int ZC>
+dim3 rb_grid(const gs_level* L)
+{
+    return dim3((unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), (unsigned)((L->ny + RY * W - 1) / (RY * W)),
+                (unsigned)((L->nz + ZC - 1) / ZC));
+}
+
+// ---------------------------------------------------------------------------------------------
 // Generic-stencil pass (any 7 offsets in {-1,0,1}^3, any order): one point per thread.
 constexpr int GN_BX = 64, GN_BY = 4;
 
@@ -430,6 +595,9 @@ bool bad_level(const gs_level* L)
 }
 
 // Dispatch a stencil pass over (mode, kind) to the fast or the generic kernel.
+// Production shape of the register-blocked kernel (chosen by tools/kbench.py on MI355X).
+constexpr int RB_RY = 4, RB_W = 4, RB_ZC = 32;
+
 template <int KIND, bool ADD>
 int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma, const double* v,
                 const double* f, const double* w, double* out, double* partials, hipStream_t st)
@@ -440,12 +608,12 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
     if (canonical_order(S)) {
-        const dim3 g = zm_grid(L), b(WAVE, ZM_TY);
-#define GS_ZM(M) hipLaunchKernelGGL((k_zmarch<M, KIND, ADD>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
-        if (mode == GS_LINEAR) GS_ZM(GS_LINEAR);
-        else if (mode == GS_NONLINEAR) GS_ZM(GS_NONLINEAR);
-        else GS_ZM(GS_NEWTON);
-#undef GS_ZM
+        const dim3 g = rb_grid<RB_RY, RB_W, RB_ZC>(L), b(WAVE, RB_W);
+#define GS_RB(M) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, RB_ZC, true>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
+        if (mode == GS_LINEAR) GS_RB(GS_LINEAR);
+        else if (mode == GS_NONLINEAR) GS_RB(GS_NONLINEAR);
+        else GS_RB(GS_NEWTON);
+#undef GS_RB
     } else {
         const dim3 g = gn_grid(L), b(GN_BX, GN_BY);
 #define GS_GN(M) hipLaunchKernelGGL((k_generic<M, KIND, ADD>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
@@ -455,6 +623,35 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
 #undef GS_GN
     }
     return launch_status();
+}
+
+// ---- tuning variants of the LINEAR sweep (tools/kbench.py) -------------------------------------
+struct Variant {
+    const char* name;
+    dim3 (*grid)(const gs_level*);
+    int wy;
+    void (*kern)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t, int64_t);
+};
+#define GS_V(RY, W, ZC, D, TAG) \
+    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, rb_grid<RY, W, ZC>, W, k_rb<GS_LINEAR, 0, false, RY, W, ZC, D>}
+const Variant kVariants[] = {
+    {"zmarch v1 64x4 zc32", zm_grid, ZM_TY, k_zmarch<GS_LINEAR, 0, false>},
+    GS_V(1, 4, 32, true, "dpp"),   GS_V(2, 4, 32, true, "dpp"), GS_V(4, 4, 32, true, "dpp"),
+    GS_V(4, 2, 32, true, "dpp"),   GS_V(8, 2, 32, true, "dpp"), GS_V(4, 4, 64, true, "dpp"),
+    GS_V(4, 4, 16, true, "dpp"),   GS_V(2, 8, 32, true, "dpp"), GS_V(4, 4, 32, false, "shfl"),
+    GS_V(2, 4, 64, true, "dpp"),   GS_V(8, 1, 32, true, "dpp"), GS_V(2, 2, 32, true, "dpp"),
+};
+#undef GS_V
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+__global__ __launch_bounds__(256) void k_triad(double* __restrict__ out, const double* __restrict__ a,
+                                               const double* __restrict__ b, int64_t n2)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const double2 x = reinterpret_cast<const double2*>(a)[i], y = reinterpret_cast<const double2*>(b)[i];
+        reinterpret_cast<double2*>(out)[i] = make_double2(x.x + 0.8 * y.x, x.y + 0.8 * y.y);
+    }
 }
 
 } // namespace
@@ -495,7 +692,7 @@ int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L)
 {
     if (!S || !L) return 0;
     if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 1;
-    const dim3 g = canonical_order(S) ? zm_grid(L) : gn_grid(L);
+    const dim3 g = canonical_order(S) ? rb_grid<RB_RY, RB_W, RB_ZC>(L) : gn_grid(L);
     return (int64_t)g.x * g.y * g.z;
 }
 
@@ -594,6 +791,37 @@ const char* gs_strerror(int code)
     return hipGetErrorString((hipError_t)code);
 }
 
-const char* gs_build_info(void) { return "gpusolve_hip v1: zmarch(64x4,2pt/lane,zc32) + generic; fp-contract=off"; }
+const char* gs_build_info(void)
+{
+    return "gpusolve_hip v2: rb(ry4 w4 zc32 dpp) + generic; fp-contract=off";
+}
+
+int gs_debug_num_variants(void) { return kNumVariants; }
+
+const char* gs_debug_variant_name(int variant)
+{
+    return (variant >= 0 && variant < kNumVariants) ? kVariants[variant].name : "";
+}
+
+int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
+                           double* v_out, const double* f, hipStream_t st)
+{
+    if (variant < 0 || variant >= kNumVariants || !S || bad_level(L) || !canonical_order(S) || !v_in || !v_out ||
+        !f || v_in == v_out)
+        return GS_EINVAL;
+    if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
+    const Variant& V = kVariants[variant];
+    const Coef k = make_coef(S, L, omega, 0.0);
+    hipLaunchKernelGGL(V.kern, V.grid(L), dim3(WAVE, V.wy), 0, st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx,
+                       (int)L->ny, (int)L->nz, L->ldy, L->ldz);
+    return launch_status();
+}
+
+int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t n, hipStream_t st)
+{
+    if (!out || !a || !b || n < 0 || (n & 1)) return GS_EINVAL;
+    hipLaunchKernelGGL(k_triad, dim3(4096), dim3(256), 0, st, out, a, b, n / 2);
+    return launch_status();
+}
 
 } // extern "C"

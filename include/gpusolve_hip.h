@@ -113,6 +113,16 @@ int gs_newton_F(const gs_stencil* S, const gs_level* L, double gamma, const doub
 int gs_axpy(double* y, const double* x, double a, int64_t n, hipStream_t stream);
 
 const char* gs_strerror(int code);
+
+/* ---- tuning / diagnostics (tools/kbench.py) ----
+ * Alternative tilings of the LINEAR fused sweep (bit-identical results), and a streaming
+ * out = a + 0.8*b kernel (24 B per element, the smoother's byte pattern) for the achievable
+ * HBM ceiling. n must be even and the arrays 16-B aligned. */
+int gs_debug_num_variants(void);
+const char* gs_debug_variant_name(int variant);
+int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
+                           double* v_out, const double* f, hipStream_t stream);
+int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t n, hipStream_t stream);
 /* Library build tag (kernel variant names), for logs. */
 const char* gs_build_info(void);
 
