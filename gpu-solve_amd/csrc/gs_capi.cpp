@@ -1,8 +1,14 @@
 // gs_capi.cpp — extern "C" facade of the host driver (include/gpusolve_driver.h).
+#include <algorithm>
+#include <array>
 #include <chrono>
+#include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <iostream>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -45,7 +51,27 @@ gs::GridParams toParams(const gs_params* p)
     return g;
 }
 
-gs::HipGridData& G(void* h) { return *static_cast<gs::HipGridData*>(h); }
+// The opaque handle: the grid plus the communicator it runs on (owned here, not by the grid).
+struct Handle {
+    std::unique_ptr<gs::Comm> comm;
+    std::unique_ptr<gs::HipGridData> grid;
+};
+
+gs::HipGridData& G(void* h) { return *static_cast<Handle*>(h)->grid; }
+
+std::vector<std::array<int64_t, 3>> levelDims(const int64_t d[3])
+{
+    std::vector<std::array<int64_t, 3>> out;
+    const int64_t mn = std::min(std::min(d[0], d[1]), d[2]);
+    if (mn <= 0) return out;
+    const int nlev = (int)std::floor(std::log((double)mn) / std::log(2.0)) + 1;
+    std::array<int64_t, 3> c{d[0], d[1], d[2]};
+    for (int l = 0; l < nlev; l++) {
+        if (l) c = {c[0] / 2, c[1] / 2, c[2] / 2};
+        out.push_back(c);
+    }
+    return out;
+}
 
 } // namespace
 
@@ -81,14 +107,23 @@ void* gs_grid_create(const gs_params* p)
         return nullptr;
     }
     try {
-        return new gs::HipGridData(toParams(p));
+        auto* h = new Handle;
+        h->grid = std::make_unique<gs::HipGridData>(toParams(p));
+        return h;
     } catch (const std::exception& e) {
         g_err = e.what();
         return nullptr;
     }
 }
 
-void gs_grid_destroy(void* grid) { delete static_cast<gs::HipGridData*>(grid); }
+void gs_grid_destroy(void* grid)
+{
+    auto* h = static_cast<Handle*>(grid);
+    if (!h) return;
+    h->grid.reset(); // before its communicator
+    h->comm.reset();
+    delete h;
+}
 
 int gs_grid_solve(void* grid, int print, double* hist, int cap, int* count)
 {
@@ -247,6 +282,121 @@ int gs_grid_time_vcycles(void* grid, int cycles, double* ms, double* last_residu
         if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         if (last_residual) *last_residual = r;
     });
+}
+
+int gs_zslab_plan(const int64_t dims[3], int nranks, int64_t min_points, int max_levels, int* distributed,
+                  int64_t* lo, int64_t* hi)
+{
+    const auto ld = levelDims(dims);
+    if (ld.empty() || nranks < 1) return 0;
+    std::vector<int64_t> nz, pts;
+    for (auto& d : ld) {
+        nz.push_back(d[2]);
+        pts.push_back(d[0] * d[1] * d[2]);
+    }
+    if (min_points < 0) {
+        const char* e = std::getenv("GS_ZSLAB_MIN_POINTS");
+        min_points = e ? std::atoll(e) : 32768;
+    }
+    const gs::SlabPlan plan = gs::planZSlabs(nz, pts, nranks, min_points);
+    for (int l = 0; l < (int)ld.size() && l < max_levels; l++) {
+        if (distributed) distributed[l] = plan.distributed[l];
+        for (int r = 0; r < nranks; r++) {
+            if (lo) lo[l * nranks + r] = plan.lo[l][r];
+            if (hi) hi[l * nranks + r] = plan.hi[l][r];
+        }
+    }
+    return (int)ld.size();
+}
+
+int gs_rccl_unique_id(unsigned char uid[128])
+{
+    return guarded([&] { gs::rcclUniqueId(uid); });
+}
+
+void* gs_grid_create_rccl(const gs_params* p, int rank, int nranks, const unsigned char uid[128])
+{
+    if (!p || !uid || rank < 0 || rank >= nranks) {
+        g_err = "bad arguments";
+        return nullptr;
+    }
+    try {
+        auto* h = new Handle;
+        try {
+            h->comm = gs::makeRcclComm(rank, nranks, uid);
+            h->grid = std::make_unique<gs::HipGridData>(toParams(p), h->comm.get());
+        } catch (...) {
+            gs_grid_destroy(h);
+            throw;
+        }
+        return h;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, int sweeps, int solve, double* hist,
+                          int cap, int* count, double* v_host)
+{
+    if (!p || nranks < 1) return 1;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        g_err = "no HIP device";
+        return 1;
+    }
+    auto hub = gs::makeLoopbackHub(nranks);
+    std::vector<std::string> errs(nranks);
+    std::vector<double> h0;
+    const gs::GridParams params = toParams(p);
+    auto body = [&](int r) {
+        try {
+            gs::check((int)hipSetDevice(dev), "hipSetDevice");
+            auto comm = gs::makeLoopbackComm(hub, r);
+            gs::HipGridData g(params, comm.get(), min_points);
+            gs::HipSolver::jacobi(g, 0, (std::size_t)sweeps);
+            if (solve) {
+                g.printProgress = false;
+                std::vector<double> h;
+                if (g.mode == gs::GridParams::NEWTON) {
+                    gs::NewtonSolver::history = &h;
+                    std::streambuf* old = std::cout.rdbuf(nullptr);
+                    gs::NewtonSolver::solve(g);
+                    std::cout.rdbuf(old);
+                    gs::NewtonSolver::history = nullptr;
+                } else {
+                    gs::HipSolver::history = &h;
+                    gs::HipSolver::solve(g);
+                    gs::HipSolver::history = nullptr;
+                }
+                if (r == 0) h0 = h;
+            }
+            gs::check((int)hipStreamSynchronize(g.stream()), "hipStreamSynchronize");
+            if (v_host) {
+                auto& L = g.getLevel(0);
+                const gs_level& G0 = L.geom;
+                const size_t w = sizeof(double) * (size_t)(G0.nx + 2);
+                double* dst = v_host + (size_t)L.lo * (size_t)((G0.ny + 2) * (G0.nx + 2));
+                gs::check((int)hipMemcpy2D(dst, w, L.v.data() + G0.ldz, sizeof(double) * (size_t)G0.ldy, w,
+                                           (size_t)((G0.ny + 2) * G0.nz), hipMemcpyDeviceToHost),
+                          "hipMemcpy2D");
+            }
+        } catch (const std::exception& e) {
+            errs[r] = e.what();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int r = 0; r < nranks; r++) th.emplace_back(body, r);
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+        if (!e.empty()) {
+            g_err = e;
+            return 1;
+        }
+    if (count) *count = (int)h0.size();
+    if (hist)
+        for (int i = 0; i < cap && i < (int)h0.size(); i++) hist[i] = h0[i];
+    return 0;
 }
 
 const char* gs_last_error(void) { return g_err.c_str(); }

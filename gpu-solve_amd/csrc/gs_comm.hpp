@@ -1,0 +1,57 @@
+// gs_comm.hpp — the exchange layer of the Z-slab decomposition.
+//
+// The reference has no distributed path; this is new. A level of the hierarchy is either
+// Z-slab-partitioned (rank r owns the contiguous global interior planes [lo[r], hi[r]] plus one
+// ghost plane on each side) or replicated (every rank holds the full level and computes it
+// redundantly; used below the agglomeration threshold). Everything a rank needs from another one is:
+//   halo()          its z-neighbours' boundary planes (send/recv of one padded plane each way),
+//   allgather1()    one double per rank (the l2-norm partial sums; summed in rank order after),
+//   gatherPlanes()  the owned planes of a replicated level, assembled on every rank.
+// Implementations: RCCL over xGMI (one process per GPU, or one thread per GPU), and a loopback that
+// runs N ranks as N threads on one device with device-to-device copies (tests on a single GPU).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include <hip/hip_runtime_api.h>
+
+namespace gs {
+
+class Comm {
+public:
+    virtual ~Comm() = default;
+    virtual int rank() const = 0;
+    virtual int size() const = 0;
+    // field: padded plane p of this rank's slab at field + p*ldz, local interior planes 1..nzl.
+    // Sends plane 1 to rank-1 and plane nzl to rank+1; receives rank-1's top plane into plane 0 and
+    // rank+1's bottom plane into plane nzl+1. Asynchronous on s.
+    virtual void halo(double* field, int64_t ldz, int64_t nzl, hipStream_t s) = 0;
+    // out[r] <- rank r's *in, on every rank (out holds size() doubles). Asynchronous on s.
+    virtual void allgather1(const double* in, double* out, hipStream_t s) = 0;
+    // field: a full-size level on every rank; rank r has computed planes [lo[r], hi[r]]; afterwards
+    // every rank holds every rank's planes. Asynchronous on s.
+    virtual void gatherPlanes(double* field, int64_t ldz, const std::vector<int64_t>& lo, const std::vector<int64_t>& hi,
+                              hipStream_t s) = 0;
+};
+
+// RCCL (NCCL API); uid is the 128-byte ncclUniqueId created by rank 0 (rcclUniqueId) and shared.
+std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid);
+void rcclUniqueId(void* uid);
+
+// Loopback: nranks threads of one process on one device share a hub.
+class LoopbackHub;
+std::shared_ptr<LoopbackHub> makeLoopbackHub(int nranks);
+std::unique_ptr<Comm> makeLoopbackComm(const std::shared_ptr<LoopbackHub>& hub, int rank);
+
+// Plane ownership of every level (pure host logic).
+struct SlabPlan {
+    std::vector<char> distributed;            // per level
+    std::vector<std::vector<int64_t>> lo, hi; // [level][rank], 1-based global interior planes
+};
+// levelNz: global interior planes per level; a level stays partitioned while its parent is,
+// it is not the coarsest, every rank keeps >= 1 plane and its global point count is >= minPoints.
+SlabPlan planZSlabs(const std::vector<int64_t>& levelNz, const std::vector<int64_t>& levelPoints, int nranks,
+                    int64_t minPoints);
+
+} // namespace gs

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <iostream>
 #include <string>
 #include <utility>
@@ -72,7 +73,8 @@ StreamGuard::~StreamGuard()
 // ---------------------------------------------------------------------------------------------
 // Level hierarchy: L = floor(log2(min dim)) + 1, dims halve per level, h_l = 1/(ny_l+1)
 // (src/cpu/CpuGridData.cpp:19-41). Fields a mode never touches are not allocated.
-HipGridData::HipGridData(const GridParams& grid) : GridParams(grid)
+HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomeratePoints)
+    : GridParams(grid), comm_(comm)
 {
     const std::size_t mn = std::min(std::min(gridDim[0], gridDim[1]), gridDim[2]);
     if (mn == 0) throw Error("grid dimensions must be positive");
@@ -84,14 +86,37 @@ HipGridData::HipGridData(const GridParams& grid) : GridParams(grid)
         stencilAbi.oy[i] = stencil.getYOffset(i);
         stencilAbi.oz[i] = stencil.getZOffset(i);
     }
-    const hipStream_t s = stream_.s;
-    int64_t maxParts = 1;
+    std::vector<int64_t> nzs, pts;
     for (int l = 0; l < nlev; l++) {
         LevelData& L = levels_[l];
         L.levelDim = l == 0 ? gridDim
                             : std::array<std::size_t, 3>{levels_[l - 1].levelDim[0] / 2, levels_[l - 1].levelDim[1] / 2,
                                                          levels_[l - 1].levelDim[2] / 2};
-        const int64_t nx = (int64_t)L.levelDim[0], ny = (int64_t)L.levelDim[1], nz = (int64_t)L.levelDim[2];
+        nzs.push_back((int64_t)L.levelDim[2]);
+        pts.push_back((int64_t)(L.levelDim[0] * L.levelDim[1] * L.levelDim[2]));
+    }
+    if (agglomeratePoints < 0) {
+        const char* e = std::getenv("GS_ZSLAB_MIN_POINTS");
+        agglomeratePoints = e ? std::atoll(e) : 32768;
+    }
+    const SlabPlan plan = planZSlabs(nzs, pts, nranks(), agglomeratePoints);
+
+    const hipStream_t s = stream_.s;
+    int64_t maxParts = 1;
+    for (int l = 0; l < nlev; l++) {
+        LevelData& L = levels_[l];
+        const int64_t nx = (int64_t)L.levelDim[0], ny = (int64_t)L.levelDim[1];
+        L.distributed = plan.distributed[l];
+        L.ranksLo = plan.lo[l];
+        L.ranksHi = plan.hi[l];
+        if (L.distributed) {
+            L.lo = plan.lo[l][rank()];
+            L.hi = plan.hi[l][rank()];
+        } else {
+            L.lo = 1;
+            L.hi = (int64_t)L.levelDim[2];
+        }
+        const int64_t nz = L.hi - L.lo + 1;
         L.h = 1.0 / (L.levelDim[1] + 1);
         L.v = DeviceField(nx, ny, nz, s);
         L.vAlt = DeviceField(nx, ny, nz, s);
@@ -99,14 +124,18 @@ HipGridData::HipGridData(const GridParams& grid) : GridParams(grid)
         if (l + 1 < nlev) L.r = DeviceField(nx, ny, nz, s); // restriction source
         if (mode == NONLINEAR && l > 0) L.restV = DeviceField(nx, ny, nz, s);
         if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s);
-        L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), 0, L.h};
+        L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), L.lo - 1, L.h};
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
     }
-    if (mode == NEWTON) newtonF = DeviceField((int64_t)gridDim[0], (int64_t)gridDim[1], (int64_t)gridDim[2], s);
+    if (mode == NEWTON) newtonF = DeviceField(levels_[0].geom.nx, levels_[0].geom.ny, levels_[0].geom.nz, s);
     check((int)hipMalloc((void**)&partials_, sizeof(double) * maxParts), "hipMalloc(partials)");
     check((int)hipMalloc((void**)&dNorm_, sizeof(double)), "hipMalloc(norm)");
+    check((int)hipMalloc((void**)&dRankSums_, sizeof(double) * nranks()), "hipMalloc(rank sums)");
     check((int)hipHostMalloc((void**)&hNorm_, sizeof(double), hipHostMallocDefault), "hipHostMalloc");
-    // level-0 right-hand side on the device (src/cpu/CpuGridData.cpp:44-78), h = 1/(Y+1) (main.cpp:84)
+    check((int)hipEventCreateWithFlags(&evA_, hipEventDisableTiming), "hipEventCreate");
+    check((int)hipEventCreateWithFlags(&evB_, hipEventDisableTiming), "hipEventCreate");
+    // level-0 right-hand side on the device (src/cpu/CpuGridData.cpp:44-78), h = 1/(Y+1) (main.cpp:84);
+    // a slab evaluates it at its global plane indices (geom.z0)
     check(gs_rhs_init(&levels_[0].geom, levels_[0].f.data(), (int)mode, 1.0 / (gridDim[1] + 1), gamma, s),
           "gs_rhs_init");
     check((int)hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -115,9 +144,13 @@ HipGridData::HipGridData(const GridParams& grid) : GridParams(grid)
 HipGridData::~HipGridData()
 {
     if (stream_.s) (void)hipStreamSynchronize(stream_.s);
+    if (commStream_.s) (void)hipStreamSynchronize(commStream_.s);
     if (partials_) (void)hipFree(partials_);
     if (dNorm_) (void)hipFree(dNorm_);
+    if (dRankSums_) (void)hipFree(dRankSums_);
     if (hNorm_) (void)hipHostFree(hNorm_);
+    if (evA_) (void)hipEventDestroy(evA_);
+    if (evB_) (void)hipEventDestroy(evB_);
 }
 
 double HipGridData::readNorm()
@@ -127,22 +160,90 @@ double HipGridData::readNorm()
     return *hNorm_;
 }
 
+void HipGridData::halo(LevelData& L, DeviceField& fld, hipStream_t s)
+{
+    if (L.distributed && nranks() > 1) comm_->halo(fld.data(), fld.ldz(), L.geom.nz, s);
+}
+
+void HipGridData::gather(LevelData& L, DeviceField& fld)
+{
+    comm_->gatherPlanes(fld.data(), fld.ldz(), L.ranksLo, L.ranksHi, stream_.s);
+}
+
+gs_level HipGridData::ownedGeom(const LevelData& L, int64_t* off) const
+{
+    gs_level g = L.geom;
+    *off = 0;
+    const std::size_t l = &L - levels_.data();
+    const bool transition = l > 0 && !L.distributed && levels_[l - 1].distributed;
+    if (transition) {
+        const int64_t lo = L.ranksLo[rank()], hi = L.ranksHi[rank()];
+        g.nz = std::max<int64_t>(0, hi - lo + 1);
+        g.z0 = lo - 1;
+        *off = (lo - 1) * L.geom.ldz;
+    }
+    return g;
+}
+
 // ---------------------------------------------------------------------------------------------
 thread_local std::vector<double>* HipSolver::history = nullptr;
 thread_local std::vector<double>* NewtonSolver::history = nullptr;
 
+namespace {
+
+// one fused sweep over local planes [z1, z2] of level L: reads L.v, writes L.vAlt
+void sweepPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_t z2, hipStream_t s)
+{
+    if (z2 < z1) return;
+    gs_level sub = L.geom;
+    sub.nz = z2 - z1 + 1;
+    sub.z0 += z1 - 1;
+    const int64_t off = (z1 - 1) * L.geom.ldz;
+    check(gs_jacobi_sweep(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.v.data() + off, L.vAlt.data() + off,
+                          L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr, s),
+          "gs_jacobi_sweep");
+}
+
+bool transitionLevel(HipGridData& g, std::size_t l)
+{
+    return l > 0 && g.nranks() > 1 && !g.getLevel(l).distributed && g.getLevel(l - 1).distributed;
+}
+
+// fine level l -> coarse level l+1 (one or two coarse outputs), then ghost refresh / gather
+void restrictTo(HipGridData& g, const DeviceField& src, std::size_t l, DeviceField& a, DeviceField* b,
+                bool needGhosts)
+{
+    auto& F = g.getLevel(l);
+    auto& C = g.getLevel(l + 1);
+    const hipStream_t s = g.stream();
+    int64_t off = 0;
+    const gs_level cg = g.ownedGeom(C, &off);
+    if (cg.nz > 0)
+        check(gs_restrict2(src.data(), &F.geom, a.data() + off, b ? b->data() + off : nullptr, &cg, s), "gs_restrict");
+    if (transitionLevel(g, l + 1)) {
+        g.gather(C, a);
+        if (b) g.gather(C, *b);
+    } else if (needGhosts) {
+        g.halo(C, a, s);
+        if (b) g.halo(C, *b, s);
+    }
+}
+
+} // namespace
+
 // src/cpu/CpuSolver.cpp:12-43
 void HipSolver::solve(HipGridData& grid)
 {
+    const bool print = grid.printProgress && grid.rank() == 0;
     const double initialResidual = compResidual(grid, 0, false, true);
     if (history) history->push_back(initialResidual);
-    if (grid.printProgress) std::cout << "Inital residual: " << initialResidual << '\n';
+    if (print) std::cout << "Inital residual: " << initialResidual << '\n';
 
     for (std::size_t i = 0; i < grid.maxiter; i++) {
-        if (grid.printProgress) Timer::start();
+        if (print) Timer::start();
         const double res = vcycle(grid);
         if (history) history->push_back(res);
-        if (grid.printProgress) {
+        if (print) {
             std::cout << "iter: " << i << " residual: " << res << ' ';
             Timer::stop();
         }
@@ -150,8 +251,23 @@ void HipSolver::solve(HipGridData& grid)
     }
 }
 
+// Global ||.|| from this rank's per-block partials: fixed-order sums per rank, then over ranks in
+// rank order, so every rank (and every run) gets the same bits.
+double HipSolver::finishNorm(HipGridData& grid, int64_t nparts)
+{
+    const hipStream_t s = grid.stream();
+    if (grid.nranks() > 1 && grid.getLevel(0).distributed) {
+        check(gs_sumsq_finish(grid.partials(), nparts, grid.dNorm(), 1, s), "gs_sumsq_finish");
+        grid.comm()->allgather1(grid.dNorm(), grid.dRankSums(), s);
+        check(gs_sumsq_finish(grid.dRankSums(), grid.nranks(), grid.dNorm(), 0, s), "gs_sumsq_finish");
+    } else {
+        check(gs_sumsq_finish(grid.partials(), nparts, grid.dNorm(), 0, s), "gs_sumsq_finish");
+    }
+    return grid.readNorm();
+}
+
 // compResidual (src/cpu/CpuSolver.cpp:45-83): r is written only when a restriction consumes it,
-// the norm only when a caller reads it.
+// the norm only when a caller reads it (level 0).
 double HipSolver::compResidual(HipGridData& grid, std::size_t l, bool storeR, bool norm)
 {
     auto& L = grid.getLevel(l);
@@ -160,29 +276,43 @@ double HipSolver::compResidual(HipGridData& grid, std::size_t l, bool storeR, bo
                       L.newtonV ? L.newtonV.data() : nullptr, storeR ? L.r.data() : nullptr,
                       norm ? grid.partials() : nullptr, s),
           "gs_residual");
+    if (storeR) grid.halo(L, L.r, s);
     if (!norm) return 0.0;
-    check(gs_sumsq_finish(grid.partials(), gs_residual_num_partials(&grid.stencilAbi, &L.geom), grid.dNorm(), 0, s),
-          "gs_sumsq_finish");
-    return grid.readNorm();
+    return finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L.geom));
 }
 
 // k fused sweeps (src/cpu/CpuSolver.cpp:141-180): each reads v, writes vAlt, then the two swap.
+// On a Z-slab the two boundary planes are computed first; their halo exchange then runs on the
+// comm stream while the interior planes are swept on the compute stream.
 void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
 {
     auto& L = grid.getLevel(l);
+    const hipStream_t s = grid.stream();
+    const bool dist = L.distributed && grid.nranks() > 1;
+    const int64_t nz = L.geom.nz;
     for (std::size_t i = 0; i < sweeps; i++) {
-        check(gs_jacobi_sweep(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.omega, grid.gamma, L.v.data(),
-                              L.vAlt.data(), L.f.data(), L.newtonV ? L.newtonV.data() : nullptr, grid.stream()),
-              "gs_jacobi_sweep");
+        if (!dist) {
+            sweepPlanes(grid, L, 1, nz, s);
+        } else if (grid.overlapHalo && nz >= 3) {
+            sweepPlanes(grid, L, 1, 1, s);
+            sweepPlanes(grid, L, nz, nz, s);
+            check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
+            check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
+            grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, grid.commStream());
+            check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+            sweepPlanes(grid, L, 2, nz - 1, s);
+            check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
+        } else {
+            sweepPlanes(grid, L, 1, nz, s);
+            grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, s);
+        }
         L.v.swap(L.vAlt);
     }
 }
 
 void HipSolver::restrict(HipGridData& grid, const DeviceField& src, std::size_t srcLevel, DeviceField& dst)
 {
-    check(gs_restrict(src.data(), &grid.getLevel(srcLevel).geom, dst.data(), &grid.getLevel(srcLevel + 1).geom,
-                      grid.stream()),
-          "gs_restrict");
+    restrictTo(grid, src, srcLevel, dst, nullptr, true);
 }
 
 // src/cpu/CpuSolver.cpp:85-139
@@ -195,12 +325,12 @@ double HipSolver::vcycle(HipGridData& grid)
         auto& L = grid.getLevel(i);
         auto& C = grid.getLevel(i + 1);
         compResidual(grid, i, true, false);
-        restrict(grid, L.r, i, C.f); // f^2h = R r^h
+        restrictTo(grid, L.r, i, C.f, nullptr, false); // f^2h = R r^h (read point-wise only: no ghosts)
         if (grid.mode != GridParams::NONLINEAR) {
             C.v.zero(s);
         } else {
             // FAS: restV = v^2h = R v^h, then f^2h += A^2h(restV)  (CpuSolver.cpp:104-113)
-            check(gs_restrict2(L.v.data(), &L.geom, C.restV.data(), C.v.data(), &C.geom, s), "gs_restrict2");
+            restrictTo(grid, L.v, i, C.restV, &C.v, true);
             check(gs_apply_op_add(&grid.stencilAbi, &C.geom, grid.gamma, C.restV.data(), C.f.data(), s),
                   "gs_apply_op_add");
         }
@@ -213,6 +343,7 @@ double HipSolver::vcycle(HipGridData& grid)
         check(gs_prolong_add(C.v.data(), grid.mode == GridParams::NONLINEAR ? C.restV.data() : nullptr, &C.geom,
                              F.v.data(), &F.geom, s),
               "gs_prolong_add");
+        grid.halo(F, F.v, s);
         jacobi(grid, i - 1, grid.postSmoothing);
     }
     return compResidual(grid, 0, false, true);
@@ -224,23 +355,26 @@ void NewtonSolver::solve(HipGridData& grid)
 {
     auto& L0 = grid.getLevel(0);
     const hipStream_t s = grid.stream();
+    const bool print = grid.rank() == 0;
     check((int)hipMemcpyAsync(grid.newtonF.data(), L0.f.data(), sizeof(double) * L0.f.span(), hipMemcpyDeviceToDevice,
                               s),
           "hipMemcpyAsync");
     const double initialResidual = compF(grid);
     if (history) history->push_back(initialResidual);
-    std::cout << "Inital newton residual: " << initialResidual << '\n';
+    if (print) std::cout << "Inital newton residual: " << initialResidual << '\n';
 
     for (std::size_t i = 0; i < grid.maxiter; i++) {
-        Timer::start();
+        if (print) Timer::start();
         // The reference recomputes compF here (NewtonSolver.cpp:21); f^0 already holds exactly that
         // value from the previous compF and nothing wrote it since, so the pass is skipped.
         L0.v.zero(s);
         findError(grid);
         const double res = compF(grid);
         if (history) history->push_back(res);
-        std::cout << "newton iter: " << i << " residual: " << res << ' ';
-        Timer::stop();
+        if (print) {
+            std::cout << "newton iter: " << i << " residual: " << res << ' ';
+            Timer::stop();
+        }
         if (res <= initialResidual / (1.0 / grid.tol)) return;
     }
 }
@@ -249,13 +383,10 @@ void NewtonSolver::solve(HipGridData& grid)
 double NewtonSolver::compF(HipGridData& grid)
 {
     auto& L0 = grid.getLevel(0);
-    const hipStream_t s = grid.stream();
     check(gs_newton_F(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), grid.newtonF.data(), L0.f.data(),
-                      grid.partials(), s),
+                      grid.partials(), grid.stream()),
           "gs_newton_F");
-    check(gs_sumsq_finish(grid.partials(), gs_residual_num_partials(&grid.stencilAbi, &L0.geom), grid.dNorm(), 0, s),
-          "gs_sumsq_finish");
-    return grid.readNorm();
+    return HipSolver::finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L0.geom));
 }
 
 // NewtonSolver.cpp:83-108
@@ -264,6 +395,7 @@ void NewtonSolver::findError(HipGridData& grid)
     for (std::size_t i = 1; i + 1 < grid.numLevels(); i++)
         HipSolver::restrict(grid, grid.getLevel(i - 1).newtonV, i - 1, grid.getLevel(i).newtonV);
 
+    const bool keepPrint = grid.printProgress;
     grid.printProgress = false;
     const std::size_t origIter = grid.maxiter;
     const double origTol = grid.tol;
@@ -273,11 +405,12 @@ void NewtonSolver::findError(HipGridData& grid)
     HipSolver::history = nullptr;
     HipSolver::solve(grid);
     HipSolver::history = keep;
-    grid.printProgress = true;
+    grid.printProgress = keepPrint;
     grid.maxiter = origIter;
     grid.tol = origTol;
 
     auto& L0 = grid.getLevel(0);
+    // whole local array, ghost planes included: both operands' ghosts are current, so the sum's are
     check(gs_axpy(L0.newtonV.data(), L0.v.data(), 1.0, L0.v.span(), grid.stream()), "gs_axpy");
 }
 

@@ -6,6 +6,10 @@
 //   NewtonSolver (src/cpu/NewtonSolver.{h,cpp})  -> gs::NewtonSolver
 // All fields live in HBM for the whole solve; the only device->host traffic per V-cycle is the
 // 8-byte residual norm.
+//
+// Multi-GPU (new; the reference has none): with a Comm of size > 1 each level is either Z-slab
+// partitioned (local planes + one ghost plane per side, kept current after every write of a field
+// that is read with neighbours) or replicated below the agglomeration threshold.
 #pragma once
 #include <array>
 #include <cstddef>
@@ -14,6 +18,7 @@
 #include <vector>
 
 #include "gpusolve_hip.h"
+#include "gs_comm.hpp"
 #include "gs_params.hpp"
 
 namespace gs {
@@ -60,12 +65,16 @@ public:
         DeviceField newtonV; // Newton linearisation point
         DeviceField f;       // right-hand side
         DeviceField r;       // residual (restriction source)
-        std::array<std::size_t, 3> levelDim{};
+        std::array<std::size_t, 3> levelDim{}; // global interior extents
         double h = 0.0;
-        gs_level geom{};     // kernel-side geometry
+        gs_level geom{};     // kernel-side geometry of the stored array (slab or full level)
+        bool distributed = false;
+        int64_t lo = 1, hi = 0; // this rank's owned global planes (== 1..nz when not distributed)
+        std::vector<int64_t> ranksLo, ranksHi; // every rank's owned planes (gather of replicated levels)
     };
 
-    explicit HipGridData(const GridParams& grid);
+    // comm == nullptr or comm->size() == 1: the single-GPU path. The grid does not own comm.
+    explicit HipGridData(const GridParams& grid, Comm* comm = nullptr, int64_t agglomeratePoints = -1);
     ~HipGridData();
 
     LevelData& getLevel(std::size_t l) { return levels_[l]; }
@@ -75,18 +84,36 @@ public:
     DeviceField newtonF;  // Newton: the original right-hand side (src/cpu/CpuGridData.h:36)
     gs_stencil stencilAbi{};
     hipStream_t stream() const { return stream_.s; }
+    hipStream_t commStream() const { return commStream_.s; }
+    Comm* comm() const { return comm_; }
+    int rank() const { return comm_ ? comm_->rank() : 0; }
+    int nranks() const { return comm_ ? comm_->size() : 1; }
+    bool overlapHalo = true; // boundary planes first, halo on the comm stream beside the interior
 
-    // residual-norm plumbing: per-block partials, device scalar, pinned host scalar
+    // residual-norm plumbing: per-block partials, device scalars, pinned host scalar
     double* partials() const { return partials_; }
     double* dNorm() const { return dNorm_; }
+    double* dRankSums() const { return dRankSums_; }
     double readNorm(); // async D2H of dNorm + stream sync: the one host sync per V-cycle
+
+    // ghost planes of a distributed level's field (no-op otherwise)
+    void halo(LevelData& L, DeviceField& fld, hipStream_t s);
+    // replicated level fed from a distributed parent: assemble every rank's owned planes
+    void gather(LevelData& L, DeviceField& fld);
+    // geometry + pointer offset of the planes this rank computes on level L
+    gs_level ownedGeom(const LevelData& L, int64_t* planeOffset) const;
 
 private:
     std::vector<LevelData> levels_;
+    Comm* comm_ = nullptr;
     StreamGuard stream_;
+    StreamGuard commStream_;
     double* partials_ = nullptr;
     double* dNorm_ = nullptr;
+    double* dRankSums_ = nullptr;
     double* hNorm_ = nullptr;
+    hipEvent_t evA_ = nullptr, evB_ = nullptr;
+    friend class HipSolver;
 };
 
 class HipSolver {
@@ -98,6 +125,7 @@ public:
     static double compResidual(HipGridData& grid, std::size_t level, bool storeR, bool norm);
     static double vcycle(HipGridData& grid);
     static void jacobi(HipGridData& grid, std::size_t level, std::size_t sweeps);
+    static double finishNorm(HipGridData& grid, int64_t nparts);
 
     // solve() records its residual history here when non-null (initial, then one per V-cycle)
     static thread_local std::vector<double>* history;

@@ -447,15 +447,17 @@ __global__ __launch_bounds__(FIN_T) void k_sumsq_finish(const double* __restrict
 // ---------------------------------------------------------------------------------------------
 // 27-point full weighting (CpuSolver.cpp:211-238): coarse interior point per thread, terms summed
 // with ii outermost, kk innermost. The weights are exact powers of two.
+// Z-slabs: coarse local plane z is global z + cz0, its centre fine plane global 2(z + cz0), local
+// 2(z + cz0) - fz0 (both z0 = 0 on an unpartitioned level).
 __global__ __launch_bounds__(256) void k_restrict(const double* __restrict__ fine, double* __restrict__ ca,
                                                   double* __restrict__ cb, int cnx, int cny, int cnz, int64_t fldy,
-                                                  int64_t fldz, int64_t cldy, int64_t cldz)
+                                                  int64_t fldz, int64_t cldy, int64_t cldz, int zoff)
 {
     const int x = 1 + blockIdx.x * 64 + threadIdx.x;
     const int y = 1 + blockIdx.y * 4 + threadIdx.y;
     const int z = 1 + blockIdx.z;
     if (x > cnx || y > cny) return;
-    const double* c0 = fine + 2 * x + (int64_t)(2 * y) * fldy + (int64_t)(2 * z) * fldz;
+    const double* c0 = fine + 2 * x + (int64_t)(2 * y) * fldy + (int64_t)(2 * z + zoff) * fldz;
     double acc = 0.0;
 #pragma unroll
     for (int a = -1; a <= 1; a++)
@@ -483,12 +485,13 @@ __device__ __forceinline__ double coarse_at(const double* __restrict__ c, const 
     return SUB ? c[q] - sub[q] : c[q];
 }
 
+// (x, y, gz) are fine indices, gz global along z; the coarse field's local plane 0 is global cz0.
 template <bool SUB>
 __device__ __forceinline__ double prolong_value(const double* __restrict__ c, const double* __restrict__ sub, int x,
-                                                int y, int z, int64_t cldy, int64_t cldz)
+                                                int y, int gz, int64_t cldy, int64_t cldz, int cz0)
 {
-    const int cx = x >> 1, cy = y >> 1, cz = z >> 1;
-    const bool ox = x & 1, oy = y & 1, oz = z & 1;
+    const int cx = x >> 1, cy = y >> 1, cz = (gz >> 1) - cz0;
+    const bool ox = x & 1, oy = y & 1, oz = gz & 1;
     auto X = [&](int jy, int jz) -> double {
         const int64_t q = cx + jy * cldy + (int64_t)jz * cldz;
         const double a = coarse_at<SUB>(c, sub, q);
@@ -511,14 +514,14 @@ __device__ __forceinline__ double prolong_value(const double* __restrict__ c, co
 template <bool SUB>
 __global__ __launch_bounds__(256) void k_prolong_add(const double* __restrict__ c, const double* __restrict__ sub,
                                                      double* __restrict__ fv, int fnx, int fny, int fnz, int64_t fldy,
-                                                     int64_t fldz, int64_t cldy, int64_t cldz)
+                                                     int64_t fldz, int64_t cldy, int64_t cldz, int fz0, int cz0)
 {
     const int x = 1 + blockIdx.x * 64 + threadIdx.x;
     const int y = 1 + blockIdx.y * 4 + threadIdx.y;
     const int z = 1 + blockIdx.z;
     if (x > fnx || y > fny) return;
     const int64_t p = x + y * fldy + (int64_t)z * fldz;
-    fv[p] = fv[p] + prolong_value<SUB>(c, sub, x, y, z, cldy, cldz);
+    fv[p] = fv[p] + prolong_value<SUB>(c, sub, x, y, z + fz0, cldy, cldz, cz0);
 }
 
 // Unfused reference-shaped interpolate (whole padded fine array), used by parity tests.
@@ -535,7 +538,7 @@ __global__ __launch_bounds__(256) void k_interpolate(const double* __restrict__ 
         e[p] = 0.0;
         return;
     }
-    e[p] = prolong_value<false>(c, nullptr, x, y, z, cldy, cldz);
+    e[p] = prolong_value<false>(c, nullptr, x, y, z, cldy, cldz, 0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -715,11 +718,14 @@ int gs_sumsq_finish(const double* partials, int64_t n, double* out, int accumula
 int gs_restrict2(const double* fine, const gs_level* fl, double* ca, double* cb, const gs_level* cl, hipStream_t st)
 {
     if (!fine || !ca || bad_level(fl) || bad_level(cl)) return GS_EINVAL;
-    if (2 * cl->nx + 1 > fl->nx + 1 || 2 * cl->ny + 1 > fl->ny + 1 || 2 * cl->nz + 1 > fl->nz + 1) return GS_EINVAL;
     if (cl->nx == 0 || cl->ny == 0 || cl->nz == 0) return 0;
+    const int64_t zoff = 2 * cl->z0 - fl->z0; // fine local centre plane = 2 z + zoff
+    if (2 * cl->nx + 1 > fl->nx + 1 || 2 * cl->ny + 1 > fl->ny + 1 || 2 + zoff - 1 < 0 ||
+        2 * cl->nz + zoff + 1 > fl->nz + 1)
+        return GS_EINVAL;
     const dim3 g((unsigned)((cl->nx + 63) / 64), (unsigned)((cl->ny + 3) / 4), (unsigned)cl->nz), b(64, 4);
     hipLaunchKernelGGL(k_restrict, g, b, 0, st, fine, ca, cb, (int)cl->nx, (int)cl->ny, (int)cl->nz, fl->ldy, fl->ldz,
-                       cl->ldy, cl->ldz);
+                       cl->ldy, cl->ldz, (int)zoff);
     return launch_status();
 }
 
@@ -730,7 +736,7 @@ int gs_restrict(const double* fine, const gs_level* fl, double* coarse, const gs
 
 int gs_interpolate(const double* coarse, const gs_level* cl, double* e, const gs_level* fl, hipStream_t st)
 {
-    if (!coarse || !e || bad_level(fl) || bad_level(cl)) return GS_EINVAL;
+    if (!coarse || !e || bad_level(fl) || bad_level(cl) || fl->z0 != 0 || cl->z0 != 0) return GS_EINVAL;
     if ((fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 || (fl->nz + 1) / 2 > cl->nz + 1) return GS_EINVAL;
     const dim3 g((unsigned)((fl->nx + 2 + 63) / 64), (unsigned)((fl->ny + 2 + 3) / 4), (unsigned)(fl->nz + 2)), b(64, 4);
     hipLaunchKernelGGL(k_interpolate, g, b, 0, st, coarse, e, (int)fl->nx + 2, (int)fl->ny + 2, (int)fl->nz + 2,
@@ -742,15 +748,18 @@ int gs_prolong_add(const double* coarse_v, const double* coarse_sub, const gs_le
                    const gs_level* fl, hipStream_t st)
 {
     if (!coarse_v || !fine_v || bad_level(fl) || bad_level(cl)) return GS_EINVAL;
-    if ((fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 || (fl->nz + 1) / 2 > cl->nz + 1) return GS_EINVAL;
     if (fl->nx == 0 || fl->ny == 0 || fl->nz == 0) return 0;
+    // coarse planes read: global floor(gz/2) and +1 for fine global gz in [fz0+1, fz0+fnz]
+    const int64_t clo = (fl->z0 + 1) / 2 - cl->z0, chi = (fl->z0 + fl->nz) / 2 + 1 - cl->z0;
+    if ((fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 || clo < 0 || chi > cl->nz + 1)
+        return GS_EINVAL;
     const dim3 g((unsigned)((fl->nx + 63) / 64), (unsigned)((fl->ny + 3) / 4), (unsigned)fl->nz), b(64, 4);
     if (coarse_sub)
         hipLaunchKernelGGL(k_prolong_add<true>, g, b, 0, st, coarse_v, coarse_sub, fine_v, (int)fl->nx, (int)fl->ny,
-                           (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz);
+                           (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz, (int)fl->z0, (int)cl->z0);
     else
         hipLaunchKernelGGL(k_prolong_add<false>, g, b, 0, st, coarse_v, nullptr, fine_v, (int)fl->nx, (int)fl->ny,
-                           (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz);
+                           (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz, (int)fl->z0, (int)cl->z0);
     return launch_status();
 }
 

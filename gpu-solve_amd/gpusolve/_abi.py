@@ -82,6 +82,12 @@ DRIVER_API = {
     "gs_grid_sync": (C.c_int, [C.c_void_p]),
     "gs_grid_time_jacobi": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "gs_grid_time_vcycles": (C.c_int, [C.c_void_p, C.c_int, dptr, dptr]),
+    "gs_zslab_plan": (C.c_int, [C.POINTER(i64), C.c_int, i64, C.c_int, C.POINTER(C.c_int), C.POINTER(i64),
+                                C.POINTER(i64)]),
+    "gs_rccl_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
+    "gs_grid_create_rccl": (C.c_void_p, [C.POINTER(gs_params), C.c_int, C.c_int, C.POINTER(C.c_ubyte)]),
+    "gs_zslab_loopback_run": (C.c_int, [C.POINTER(gs_params), C.c_int, i64, C.c_int, C.c_int, dptr, C.c_int,
+                                        C.POINTER(C.c_int), dptr]),
     "gs_last_error": (C.c_char_p, []),
 }
 

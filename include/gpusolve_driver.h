@@ -67,6 +67,27 @@ int gs_grid_time_jacobi(void* grid, int level, int warmup, int sweeps, float* ms
 /* Times `cycles` V-cycles (each including its norm readback) with a host clock; *ms total. */
 int gs_grid_time_vcycles(void* grid, int cycles, double* ms, double* last_residual);
 
+/* ---- Z-slab multi-GPU (new) ----
+ * Ownership plan of every level for `nranks` ranks (pure host logic): distributed[l] = 1 when
+ * level l is Z-slab partitioned; lo/hi[l*nranks + r] = rank r's owned global interior planes
+ * (1-based, inclusive). min_points < 0 selects the default agglomeration threshold. Returns the
+ * level count (at most max_levels entries are written). */
+int gs_zslab_plan(const int64_t dims[3], int nranks, int64_t min_points, int max_levels, int* distributed,
+                  int64_t* lo, int64_t* hi);
+/* 128-byte RCCL unique id (rank 0 creates it, every rank passes the same bytes). */
+int gs_rccl_unique_id(unsigned char uid[128]);
+/* Grid whose levels are Z-slab partitioned over an RCCL communicator (one GPU per rank; the
+ * current HIP device). The other gs_grid_* calls then run the distributed solver; fields and
+ * levels describe this rank's slab; rank 0 prints. */
+void* gs_grid_create_rccl(const gs_params* p, int rank, int nranks, const unsigned char uid[128]);
+/* Single-process emulation of an nranks Z-slab run on the current device: nranks threads, each a
+ * rank with its own slab and streams, device-to-device copies as the exchange. Runs `sweeps`
+ * level-0 Jacobi sweeps, then (solve != 0) the solve of p. Writes rank 0's residual history and
+ * the assembled level-0 v (dense [nz+2][ny+2][nx+2], interior planes only; NULL to skip).
+ * min_points as in gs_zslab_plan. For testing the distributed path on one GPU. */
+int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, int sweeps, int solve, double* hist,
+                          int cap, int* count, double* v_host);
+
 const char* gs_last_error(void);
 
 #ifdef __cplusplus
