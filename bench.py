@@ -8,7 +8,10 @@ updates; value = lattice updates of all ranks / max-over-ranks wall time (MLUPS)
 resident in HBM before the timed region. The V-cycle wall time (512^3, 2+2, including the 8-byte
 norm readback) is measured after the timed region and reported under "vcycle".
 
-Multi-GPU (torchrun, one process per GPU): weak scaling, every rank owns 512^3 lattice points.
+Multi-GPU (torchrun, one process per GPU): the grid is Z-slab partitioned over RCCL (xGMI), ghost
+planes exchanged every sweep on a second stream while the interior planes are swept; weak scaling
+with 512^3 lattice points per rank: N=2 -> 1024x512x512, N=4 -> 1024x1024x512, N=8 -> 1024^3
+(BASELINE config #5); other N -> 512x512x(512N).
 
 Roofline: the smoother is HBM-bound (0.5 flop/B); algorithmic bytes = 24 B per lattice update
 (read v, read f, write v_new) x 512^3 per launch / average launch duration measured
@@ -92,24 +95,51 @@ def cpu_baseline(n, sweeps, vcycles):
     return out
 
 
+def global_dims(n, world):
+    table = {1: (n, n, n), 2: (2 * n, n, n), 4: (2 * n, 2 * n, n), 8: (2 * n, 2 * n, 2 * n)}
+    return table.get(world, (n, n, n * world))
+
+
+def make_grid(params, rank, world):
+    """Single-GPU grid, or this rank's Z-slab of an RCCL-partitioned grid."""
+    import ctypes as C
+    if world == 1:
+        return gsv.HipGridData(params)
+    drv = gsv.driver()
+    uid = (C.c_ubyte * 128)()
+    if rank == 0 and drv.gs_rccl_unique_id(uid) != 0:
+        raise gsv.GpuSolveError(drv.gs_last_error().decode())
+    t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device="cuda")
+    dist.broadcast(t, 0)
+    uid = (C.c_ubyte * 128)(*t.cpu().tolist())
+    grid = gsv.HipGridData.__new__(gsv.HipGridData)
+    grid.params = params
+    grid._abi_params = params.to_abi()
+    grid.handle = drv.gs_grid_create_rccl(C.byref(grid._abi_params), rank, world, uid)
+    if not grid.handle:
+        raise gsv.GpuSolveError(drv.gs_last_error().decode())
+    return grid
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local % max(1, torch.cuda.device_count())))
 
     def barrier():
         if world > 1:
             dist.barrier()
 
     n = a.n
-    params = gsv.GridParams(maxiter=1, tol=0.0, gridDim=(n, n, n), mode=gsv.GS_LINEAR, preSmoothing=2,
+    dims = global_dims(n, world)
+    params = gsv.GridParams(maxiter=1, tol=0.0, gridDim=dims, mode=gsv.GS_LINEAR, preSmoothing=2,
                             postSmoothing=2)
-    grid = gsv.HipGridData(params)
+    grid = make_grid(params, rank, world)
     drv = gsv.driver()
     stream = torch.cuda.ExternalStream(grid.stream())
 
@@ -138,7 +168,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
 
-    lups_per_rank = float(n) ** 3
+    lups_per_rank = float(dims[0]) * dims[1] * dims[2] / world
     total_lups = lups_per_rank * a.steps * world
     value = total_lups / elapsed / 1e6
     achieved = BYTES_PER_LUP * lups_per_rank / (kernel_ms * 1e-3) / 1e9
@@ -156,8 +186,8 @@ def main():
         vt = torch.tensor([ms.value / a.vcycles], dtype=torch.float64, device="cuda")
         if world > 1:
             dist.all_reduce(vt, op=dist.ReduceOp.MAX)
-        vc = {"ms": round(vt.item(), 3), "cycles": a.vcycles, "config": f"{n}^3 linear 2+2, norm readback included",
-              "first_residual": res}
+        vc = {"ms": round(vt.item(), 3), "cycles": a.vcycles,
+              "config": f"{dims[0]}x{dims[1]}x{dims[2]} linear 2+2, norm readback included", "first_residual": res}
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sweeps > 0:
@@ -180,9 +210,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (analytic RHS of the reference, v0 = 0)",
-            "config": {"workload": f"{n}^3 linear 7-point fused Jacobi sweep (level 0), BASELINE config #3",
-                       "grid_per_rank": [n, n, n], "mode": "linear", "omega": 0.8,
-                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "config": {"workload": (f"{n}^3 linear 7-point fused Jacobi sweep (level 0), BASELINE config #3"
+                                    if world == 1 else
+                                    f"{dims[0]}x{dims[1]}x{dims[2]} linear 7-point fused Jacobi sweep (level 0), "
+                                    f"Z-slab over {world} GPUs (BASELINE config #5 at N=8)"),
+                       "grid": list(dims), "points_per_rank": int(lups_per_rank), "mode": "linear", "omega": 0.8,
+                       "parallelism": f"zslab{world}-rccl" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_GBPS, 4),
                          "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
