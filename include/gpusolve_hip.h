@@ -74,6 +74,12 @@ int gs_rhs_init(const gs_level* L, double* f, int mode, double h0, double gamma,
 int gs_jacobi_sweep(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                     const double* v_in, double* v_out, const double* f, const double* w, hipStream_t stream);
 
+/* The same sweep, also writing the per-block sums of r^2 of the residual r = f - A(v_in) it computes
+ * (the reference's compResidual norm of the pre-sweep iterate; layout as gs_residual's partials). */
+int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                         const double* v_in, double* v_out, const double* f, const double* w, double* partials,
+                         hipStream_t stream);
+
 /* r = f - A(v) on the interior. r may be NULL (norm only). partials may be NULL (no norm);
  * otherwise it receives gs_residual_num_partials(S, L) per-block sums of r^2 in a fixed order. */
 int gs_residual(const gs_stencil* S, const gs_level* L, int mode, double gamma, const double* v, const double* f,
