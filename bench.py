@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=512, help="per-rank cube edge (BASELINE config #3: 512)")
+    ap.add_argument("--size", type=int, default=512, help="per-rank cube edge (BASELINE config #3: 512)")
     ap.add_argument("--vcycles", type=int, default=5, help="timed V-cycles after one warm-up cycle (0: skip)")
     ap.add_argument("--cpu-sweeps", type=int, default=6, help="cpu_baseline sample size (0: skip)")
     ap.add_argument("--cpu-vcycles", type=int, default=1, help="cpu_baseline V-cycles (0: skip)")
@@ -135,7 +135,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    n = a.n
+    n = a.size
     dims = global_dims(n, world)
     params = gsv.GridParams(maxiter=1, tol=0.0, gridDim=dims, mode=gsv.GS_LINEAR, preSmoothing=2,
                             postSmoothing=2)

@@ -256,7 +256,37 @@ __device__ __forceinline__ double lane_from_right(double src, double edge)
 
 __device__ __forceinline__ double2 ld2(const double* __restrict__ p) { return *reinterpret_cast<const double2*>(p); }
 
-template <int MODE, int KIND, bool ADD, int RY, int W, int ZC, bool DPP>
+typedef double dv2 __attribute__((ext_vector_type(2)));
+// streamed-once operands (f, the output) optionally bypass the caches' retention (nt)
+template <bool NT>
+__device__ __forceinline__ double2 ld2s(const double* __restrict__ p)
+{
+    if (NT) {
+        const dv2 t = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(p));
+        return make_double2(t.x, t.y);
+    }
+    return ld2(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st2s(double* __restrict__ p, double a, double b)
+{
+    if (NT) {
+        const dv2 t = {a, b};
+        __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p));
+    } else {
+        *reinterpret_cast<double2*>(p) = make_double2(a, b);
+    }
+}
+
+// Bijective XCD-aware tile order (cdna_hip_programming.md T1): hardware block b runs on XCD b % 8;
+// give each XCD a contiguous run of tiles so y-neighbour tiles share an L2 while they run.
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb)
+{
+    const int64_t q = nb / 8, r = nb % 8, x = b % 8, k = b / 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+template <int MODE, int KIND, bool ADD, int RY, int W, int ZC, bool DPP, bool NT = false, bool XCD = false>
 __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict__ v, const double* __restrict__ f,
                                                  const double* __restrict__ w, double* __restrict__ out,
                                                  double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
@@ -265,11 +295,20 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
     __shared__ double red[W];
     const int lane = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.y);
-    const int x0 = 1 + blockIdx.x * (2 * WAVE);
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    int64_t tile = blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z);
+    if (XCD) {
+        const int nbx = (nx + 2 * WAVE - 1) / (2 * WAVE), nby = (ny + RY * W - 1) / (RY * W);
+        tile = xcd_tile(blockIdx.x, gridDim.x);
+        bx = (int)(tile % nbx);
+        by = (int)((tile / nbx) % nby);
+        bz = (int)(tile / ((int64_t)nbx * nby));
+    }
+    const int x0 = 1 + bx * (2 * WAVE);
     const int x = x0 + 2 * lane;
     const int xl = min(x, nx + 1);
-    const int y0 = 1 + (blockIdx.y * W + wv) * RY;
-    const int zb = 1 + blockIdx.z * ZC;
+    const int y0 = 1 + (by * W + wv) * RY;
+    const int zb = 1 + bz * ZC;
     const int ze = min(zb + ZC - 1, nz);
     const int xle = x0 - 1;
     const int xre = min(x0 + 2 * WAVE, nx + 1);
@@ -289,7 +328,7 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
         for (int r = 0; r < RY; r++) {
             P[r] = ld2(v + xl + roff[r + 1] + zo - ldz);
             N[r] = ld2(v + xl + roff[r + 1] + zo + ldz);
-            if (KIND != 2 || ADD) F[r] = ld2(fin + xl + roff[r + 1] + zo);
+            if (KIND != 2 || ADD) F[r] = ld2s<NT>(fin + xl + roff[r + 1] + zo);
             if (MODE == GS_NEWTON) Wc[r] = ld2(w + xl + roff[r + 1] + zo);
             CL[r] = v[xle + roff[r + 1] + zo];
             CR[r] = v[xre + roff[r + 1] + zo];
@@ -308,7 +347,7 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
 #pragma unroll
             for (int r = 0; r < RY; r++) {
                 NN[r] = ld2(v + xl + roff[r + 1] + z1 + ldz);
-                if (KIND != 2 || ADD) FN[r] = ld2(fin + xl + roff[r + 1] + z1);
+                if (KIND != 2 || ADD) FN[r] = ld2s<NT>(fin + xl + roff[r + 1] + z1);
                 if (MODE == GS_NEWTON) WN[r] = ld2(w + xl + roff[r + 1] + z1);
                 ELn[r] = v[xle + roff[r + 1] + z1];
                 ERn[r] = v[xre + roff[r + 1] + z1];
@@ -344,7 +383,7 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
             }
             if (rowok && (KIND != 1 || out)) {
                 double* q = out + x + roff[r + 1] + zo;
-                if (okx1) *reinterpret_cast<double2*>(q) = make_double2(o0, o1);
+                if (okx1) st2s<NT>(q, o0, o1);
                 else if (okx0) *q = o0;
             }
         }
@@ -367,8 +406,7 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
     }
     if (KIND != 2 && partials) {
         const double t = block_sum<W>(sumsq, red);
-        if (threadIdx.x == 0 && threadIdx.y == 0)
-            partials[blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z)] = t;
+        if (threadIdx.x == 0 && threadIdx.y == 0) partials[tile] = t;
     }
 }
 
@@ -377,6 +415,12 @@ dim3 rb_grid(const gs_level* L)
 {
     return dim3((unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), (unsigned)((L->ny + RY * W - 1) / (RY * W)),
                 (unsigned)((L->nz + ZC - 1) / ZC));
+}
+template <int RY, int W, int ZC>
+dim3 rb_grid1d(const gs_level* L)
+{
+    const dim3 g = rb_grid<RY, W, ZC>(L);
+    return dim3(g.x * g.y * g.z);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -640,15 +684,55 @@ struct Variant {
 };
 #define GS_V(RY, W, ZC, D, TAG) \
     {"rb ry" #RY " w" #W " zc" #ZC " " TAG, rb_grid<RY, W, ZC>, W, k_rb<GS_LINEAR, 0, false, RY, W, ZC, D>}
+#define GS_VX(RY, W, ZC, NT, X, TAG)                                                                   \
+    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, X ? rb_grid1d<RY, W, ZC> : rb_grid<RY, W, ZC>, W,          \
+     k_rb<GS_LINEAR, 0, false, RY, W, ZC, true, NT, X>}
 const Variant kVariants[] = {
     {"zmarch v1 64x4 zc32", zm_grid, ZM_TY, k_zmarch<GS_LINEAR, 0, false>},
     GS_V(1, 4, 32, true, "dpp"),   GS_V(2, 4, 32, true, "dpp"), GS_V(4, 4, 32, true, "dpp"),
     GS_V(4, 2, 32, true, "dpp"),   GS_V(8, 2, 32, true, "dpp"), GS_V(4, 4, 64, true, "dpp"),
     GS_V(4, 4, 16, true, "dpp"),   GS_V(2, 8, 32, true, "dpp"), GS_V(4, 4, 32, false, "shfl"),
     GS_V(2, 4, 64, true, "dpp"),   GS_V(8, 1, 32, true, "dpp"), GS_V(2, 2, 32, true, "dpp"),
+    GS_VX(8, 2, 32, true, false, "dpp nt"), GS_VX(8, 2, 32, false, true, "dpp xcd"),
+    GS_VX(8, 2, 32, true, true, "dpp nt xcd"), GS_VX(8, 1, 64, false, false, "dpp"),
+    GS_VX(8, 1, 128, false, false, "dpp"), GS_VX(8, 2, 64, true, true, "dpp nt xcd"),
+    GS_VX(1, 4, 32, true, true, "dpp nt xcd"), GS_VX(6, 2, 32, true, true, "dpp nt xcd"),
+    GS_VX(8, 4, 32, true, true, "dpp nt xcd"), GS_VX(8, 1, 32, true, true, "dpp nt xcd"),
 };
 #undef GS_V
+#undef GS_VX
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// Bandwidth ceilings. KIND 0 read a, 1 write out, 2 copy a->out, 3 triad out = a + 0.8 b.
+// UNROLL independent dwordx4 per thread per iteration, NT non-temporal loads/stores.
+template <int KIND, int UNROLL, bool NT>
+__global__ __launch_bounds__(256) void k_bw(double* __restrict__ out, const double* __restrict__ a,
+                                            const double* __restrict__ b, int64_t n2, double* __restrict__ sink)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    double acc = 0.0;
+    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n2; i0 += stride * UNROLL) {
+        double2 va[UNROLL], vb[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) {
+            const int64_t i = i0 + u * stride;
+            if (i < n2) {
+                if (KIND != 1) va[u] = ld2s<NT>(a + 2 * i);
+                if (KIND == 3) vb[u] = ld2s<NT>(b + 2 * i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) {
+            const int64_t i = i0 + u * stride;
+            if (i >= n2) continue;
+            if (KIND == 0) acc += va[u].x + va[u].y;
+            else if (KIND == 1) st2s<NT>(out + 2 * i, 1.0, 2.0);
+            else if (KIND == 2) st2s<NT>(out + 2 * i, va[u].x, va[u].y);
+            else st2s<NT>(out + 2 * i, va[u].x + 0.8 * vb[u].x, va[u].y + 0.8 * vb[u].y);
+        }
+    }
+    if (KIND == 0 && acc == -1.2345e300) *sink = acc; // keeps the loads alive
+}
 
 __global__ __launch_bounds__(256) void k_triad(double* __restrict__ out, const double* __restrict__ a,
                                                const double* __restrict__ b, int64_t n2)
@@ -835,6 +919,21 @@ int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, 
     const Coef k = make_coef(S, L, omega, 0.0);
     hipLaunchKernelGGL(V.kern, V.grid(L), dim3(WAVE, V.wy), 0, st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx,
                        (int)L->ny, (int)L->nz, L->ldy, L->ldz);
+    return launch_status();
+}
+
+int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
+                double* sink, hipStream_t st)
+{
+    if (n < 0 || (n & 1) || kind < 0 || kind > 3 || blocks <= 0) return GS_EINVAL;
+    using K = void (*)(double*, const double*, const double*, int64_t, double*);
+    static const K tab[4][2][2] = {
+        {{k_bw<0, 1, false>, k_bw<0, 1, true>}, {k_bw<0, 4, false>, k_bw<0, 4, true>}},
+        {{k_bw<1, 1, false>, k_bw<1, 1, true>}, {k_bw<1, 4, false>, k_bw<1, 4, true>}},
+        {{k_bw<2, 1, false>, k_bw<2, 1, true>}, {k_bw<2, 4, false>, k_bw<2, 4, true>}},
+        {{k_bw<3, 1, false>, k_bw<3, 1, true>}, {k_bw<3, 4, false>, k_bw<3, 4, true>}},
+    };
+    hipLaunchKernelGGL(tab[kind][unroll > 1][nt != 0], dim3(blocks), dim3(256), 0, st, out, a, b, n / 2, sink);
     return launch_status();
 }
 

@@ -64,6 +64,8 @@ KERNEL_API = {
     "gs_debug_sweep_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double,
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_debug_stream_triad": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p]),
+    "gs_debug_bw": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p,
+                              C.c_void_p]),
     "gs_build_info": (C.c_char_p, []),
 }
 

@@ -129,6 +129,10 @@ const char* gs_debug_variant_name(int variant);
 int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
                            double* v_out, const double* f, hipStream_t stream);
 int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t n, hipStream_t stream);
+/* Streaming ceilings: kind 0 read a, 1 write out, 2 copy, 3 triad; unroll 1 or 4 dwordx4 per thread,
+ * nt = non-temporal, `blocks` workgroups of 256 threads (grid-stride). */
+int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
+                double* sink, hipStream_t stream);
 /* Library build tag (kernel variant names), for logs. */
 const char* gs_build_info(void);
 

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--sweeps", type=int, default=10)
     ap.add_argument("--variants", type=str, default="")
     ap.add_argument("--out", type=str, default="")
+    ap.add_argument("--bw", action="store_true", help="also sweep the streaming-ceiling kernels")
     a = ap.parse_args()
     k = gsv.kernels()
     nx = a.n
@@ -113,6 +114,36 @@ def main():
     med = statistics.median(ts)
     result["triad"] = {"elements": n, "median_ms": round(med, 4), "gbps": round(24 * n / med / 1e6, 1),
                        "pct_peak": round(100 * 24 * n / med / 1e6 / PEAK, 1)}
+    if a.bw:
+        sink = torch.zeros(1, dtype=torch.float64, device="cuda")
+        bytes_per = {0: 8, 1: 8, 2: 16, 3: 24}
+        names_k = {0: "read", 1: "write", 2: "copy", 3: "triad"}
+        bw = {}
+        for kind in (0, 1, 2, 3):
+            for unroll in (1, 4):
+                for nt in (0, 1):
+                    for blocks in (1024, 2048, 4096, 8192, 16384):
+                        def run():
+                            k.gs_debug_bw(kind, unroll, nt, blocks, O.data_ptr(), A.data_ptr(), B.data_ptr(), n,
+                                          sink.data_ptr(), st)
+                        run()
+                        ts = []
+                        for _ in range(3):
+                            ev[0].record()
+                            for _ in range(a.sweeps):
+                                run()
+                            ev[1].record()
+                            torch.cuda.synchronize()
+                            ts.append(ev[0].elapsed_time(ev[1]) / a.sweeps)
+                        med = statistics.median(ts)
+                        bw[f"{names_k[kind]} u{unroll} nt{nt} b{blocks}"] = round(bytes_per[kind] * n / med / 1e6, 1)
+        result["bw"] = bw
+        best = {}
+        for key, val in bw.items():
+            kk = key.split()[0]
+            if val > best.get(kk, (0, ""))[0]:
+                best[kk] = (val, key)
+        result["bw_best"] = best
     # torch's own copy as a second reference point
     for _ in range(2):
         O.copy_(A)
