@@ -286,7 +286,8 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb)
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
-template <int MODE, int KIND, bool ADD, int RY, int W, int ZC, bool DPP, bool NT = false, bool XCD = false>
+template <int MODE, int KIND, bool ADD, int RY, int W, int ZC, bool DPP, bool NT = false, bool XCD = false,
+          bool NTV = false>
 __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict__ v, const double* __restrict__ f,
                                                  const double* __restrict__ w, double* __restrict__ out,
                                                  double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
             const int64_t z1 = zo + ldz;
 #pragma unroll
             for (int r = 0; r < RY; r++) {
-                NN[r] = ld2(v + xl + roff[r + 1] + z1 + ldz);
+                NN[r] = ld2s<NTV>(v + xl + roff[r + 1] + z1 + ldz);
                 if (KIND != 2 || ADD) FN[r] = ld2s<NT>(fin + xl + roff[r + 1] + z1);
                 if (MODE == GS_NEWTON) WN[r] = ld2(w + xl + roff[r + 1] + z1);
                 ELn[r] = v[xle + roff[r + 1] + z1];
@@ -645,8 +646,11 @@ bool bad_level(const gs_level* L)
 }
 
 // Dispatch a stencil pass over (mode, kind) to the fast or the generic kernel.
-// Production shape of the register-blocked kernel (chosen by tools/kbench.py on MI355X).
-constexpr int RB_RY = 4, RB_W = 4, RB_ZC = 32;
+// Production shape of the register-blocked kernel (chosen by tools/kbench.py on MI355X,
+// profiles/r01_kbench.json): 8 rows x 128 columns per wave, 2 waves per block, 32-plane chunks,
+// non-temporal f / output streams.
+constexpr int RB_RY = 8, RB_W = 2, RB_ZC = 32;
+constexpr bool RB_NT = true;
 
 template <int KIND, bool ADD>
 int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma, const double* v,
@@ -659,7 +663,7 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
     if (canonical_order(S)) {
         const dim3 g = rb_grid<RB_RY, RB_W, RB_ZC>(L), b(WAVE, RB_W);
-#define GS_RB(M) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, RB_ZC, true>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
+#define GS_RB(M) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, RB_ZC, true, RB_NT>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
         if (mode == GS_LINEAR) GS_RB(GS_LINEAR);
         else if (mode == GS_NONLINEAR) GS_RB(GS_NONLINEAR);
         else GS_RB(GS_NEWTON);
@@ -687,18 +691,21 @@ struct Variant {
 #define GS_VX(RY, W, ZC, NT, X, TAG)                                                                   \
     {"rb ry" #RY " w" #W " zc" #ZC " " TAG, X ? rb_grid1d<RY, W, ZC> : rb_grid<RY, W, ZC>, W,          \
      k_rb<GS_LINEAR, 0, false, RY, W, ZC, true, NT, X>}
+#define GS_VV(RY, W, ZC, TAG) \
+    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, rb_grid<RY, W, ZC>, W, k_rb<GS_LINEAR, 0, false, RY, W, ZC, true, true, false, true>}
 const Variant kVariants[] = {
     {"zmarch v1 64x4 zc32", zm_grid, ZM_TY, k_zmarch<GS_LINEAR, 0, false>},
-    GS_V(1, 4, 32, true, "dpp"),   GS_V(2, 4, 32, true, "dpp"), GS_V(4, 4, 32, true, "dpp"),
-    GS_V(4, 2, 32, true, "dpp"),   GS_V(8, 2, 32, true, "dpp"), GS_V(4, 4, 64, true, "dpp"),
-    GS_V(4, 4, 16, true, "dpp"),   GS_V(2, 8, 32, true, "dpp"), GS_V(4, 4, 32, false, "shfl"),
-    GS_V(2, 4, 64, true, "dpp"),   GS_V(8, 1, 32, true, "dpp"), GS_V(2, 2, 32, true, "dpp"),
-    GS_VX(8, 2, 32, true, false, "dpp nt"), GS_VX(8, 2, 32, false, true, "dpp xcd"),
-    GS_VX(8, 2, 32, true, true, "dpp nt xcd"), GS_VX(8, 1, 64, false, false, "dpp"),
-    GS_VX(8, 1, 128, false, false, "dpp"), GS_VX(8, 2, 64, true, true, "dpp nt xcd"),
-    GS_VX(1, 4, 32, true, true, "dpp nt xcd"), GS_VX(6, 2, 32, true, true, "dpp nt xcd"),
-    GS_VX(8, 4, 32, true, true, "dpp nt xcd"), GS_VX(8, 1, 32, true, true, "dpp nt xcd"),
+    GS_V(4, 4, 32, true, "dpp"),   GS_V(8, 2, 32, true, "dpp"), GS_V(4, 4, 32, false, "shfl"),
+    GS_VX(8, 2, 32, true, false, "dpp nt"), GS_VX(8, 1, 32, true, false, "dpp nt"),
+    GS_VX(8, 4, 32, true, false, "dpp nt"), GS_VX(8, 2, 64, true, false, "dpp nt"),
+    GS_VX(8, 2, 16, true, false, "dpp nt"), GS_VX(1, 4, 32, true, false, "dpp nt"),
+    GS_VX(2, 4, 32, true, false, "dpp nt"), GS_VX(4, 4, 32, true, false, "dpp nt"),
+    GS_VX(4, 2, 32, true, false, "dpp nt"), GS_VX(6, 2, 32, true, false, "dpp nt"),
+    GS_VX(1, 8, 32, true, false, "dpp nt"), GS_VX(2, 2, 32, true, false, "dpp nt"),
+    GS_VV(8, 2, 32, "dpp nt ntv"), GS_VV(4, 4, 32, "dpp nt ntv"), GS_VV(1, 4, 32, "dpp nt ntv"),
+    GS_VX(8, 2, 32, true, true, "dpp nt xcd"),
 };
+#undef GS_VV
 #undef GS_V
 #undef GS_VX
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
@@ -898,7 +905,7 @@ const char* gs_strerror(int code)
 
 const char* gs_build_info(void)
 {
-    return "gpusolve_hip v2: rb(ry4 w4 zc32 dpp) + generic; fp-contract=off";
+    return "gpusolve_hip v3: rb(ry8 w2 zc32 dpp nt) + generic; fp-contract=off";
 }
 
 int gs_debug_num_variants(void) { return kNumVariants; }
