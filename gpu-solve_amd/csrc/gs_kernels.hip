@@ -128,91 +128,10 @@ __device__ __forceinline__ double block_sum(double x, double* lds)
 }
 
 // ---------------------------------------------------------------------------------------------
-// Canonical-stencil pass, z-marching: block = 64 x 4 threads, each lane owns 2 consecutive
-// x-points (one dwordx4), each wave one y-row; the block walks ZC planes keeping v(z-1), v(z),
-// v(z+1) of its own points in registers (the next plane is prefetched one step ahead), the
-// in-plane x/y neighbours come through L1/L2.
-//   KIND 0: Jacobi sweep         out = v_new
+// Stencil passes come in three kinds:
+//   KIND 0: Jacobi sweep         out = v_new (partials: sum r^2 of the input's residual, nullable)
 //   KIND 1: residual             out = r (nullable), partials = per-block sum r^2 (nullable)
 //   KIND 2: FAS coarse operator  out = A(u) (ADD=false) or out += A(u) (ADD=true)
-constexpr int ZM_TXP = 2;
-constexpr int ZM_TX = WAVE * ZM_TXP; // 128
-constexpr int ZM_TY = 4;
-constexpr int ZM_ZC = 32;
-
-template <int MODE, int KIND, bool ADD>
-__global__ __launch_bounds__(256) void k_zmarch(Coef k, const double* __restrict__ v, const double* __restrict__ f,
-                                                const double* __restrict__ w, double* __restrict__ out,
-                                                double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
-                                                int64_t ldz)
-{
-    __shared__ double red[ZM_TY];
-    const int lane = threadIdx.x;
-    const int x = 1 + blockIdx.x * ZM_TX + ZM_TXP * lane;
-    const int y = 1 + blockIdx.y * ZM_TY + threadIdx.y;
-    const int zb = 1 + blockIdx.z * ZM_ZC;
-    const int ze = min(zb + ZM_ZC - 1, nz);
-    const bool act = (x <= nx) && (y <= ny);
-    const bool two = act && (x + 1 <= nx);
-
-    double sumsq = 0.0;
-    if (act) {
-        const int64_t row = x + (int64_t)y * ldy;
-        const double* vp = v + row;
-        double2 vm = *reinterpret_cast<const double2*>(vp + (int64_t)(zb - 1) * ldz);
-        double2 vc = *reinterpret_cast<const double2*>(vp + (int64_t)zb * ldz);
-        double2 vn = *reinterpret_cast<const double2*>(vp + (int64_t)(zb + 1) * ldz);
-        for (int z = zb; z <= ze; z++) {
-            const int64_t p = row + (int64_t)z * ldz;
-            // prefetch plane z+2 (always inside the padded array while z+2 <= nz+1)
-            double2 vnn = vn;
-            if (z + 2 <= nz + 1) vnn = *reinterpret_cast<const double2*>(v + p + 2 * ldz);
-            const double xm = v[p - 1];
-            const double xp = v[p + 2];
-            const double2 ym = *reinterpret_cast<const double2*>(v + p - ldy);
-            const double2 yp = *reinterpret_cast<const double2*>(v + p + ldy);
-            double2 wv = make_double2(0.0, 0.0);
-            if (MODE == GS_NEWTON) wv = *reinterpret_cast<const double2*>(w + p);
-            double2 fv = make_double2(0.0, 0.0);
-            if (KIND != 2 || ADD) fv = *reinterpret_cast<const double2*>((KIND == 2 ? out : f) + p);
-
-            const double a0 = op_value<MODE>(k, vc.x, vc.y, xm, yp.x, ym.x, vn.x, vm.x, wv.x);
-            const double a1 = op_value<MODE>(k, vc.y, xp, vc.x, yp.y, ym.y, vn.y, vm.y, wv.y);
-            double o0, o1;
-            if (KIND == 0) {
-                o0 = jacobi_update<MODE>(k, vc.x, fv.x - a0, wv.x);
-                o1 = jacobi_update<MODE>(k, vc.y, fv.y - a1, wv.y);
-            } else if (KIND == 1) {
-                o0 = fv.x - a0;
-                o1 = fv.y - a1;
-                sumsq += o0 * o0;
-                if (two) sumsq += o1 * o1;
-            } else {
-                o0 = ADD ? fv.x + a0 : a0;
-                o1 = ADD ? fv.y + a1 : a1;
-            }
-            if (KIND != 1 || out) {
-                if (two) *reinterpret_cast<double2*>(out + p) = make_double2(o0, o1);
-                else out[p] = o0;
-            }
-            vm = vc;
-            vc = vn;
-            vn = vnn;
-        }
-    }
-    if (KIND == 1 && partials) {
-        const double t = block_sum<ZM_TY>(sumsq, red);
-        if (threadIdx.x == 0 && threadIdx.y == 0)
-            partials[blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z)] = t;
-    }
-}
-
-dim3 zm_grid(const gs_level* L)
-{
-    return dim3((unsigned)((L->nx + ZM_TX - 1) / ZM_TX), (unsigned)((L->ny + ZM_TY - 1) / ZM_TY),
-                (unsigned)((L->nz + ZM_ZC - 1) / ZM_ZC));
-}
-
 // ---------------------------------------------------------------------------------------------
 // Register-blocked z-march ("rb"): each lane owns 2 consecutive x-points (one dwordx4) of RY
 // consecutive y-rows, a wave owns a 128 x RY tile, W waves stack in y, the block walks ZC planes.
@@ -286,12 +205,11 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb)
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
-template <int MODE, int KIND, bool ADD, int RY, int W, int ZC, bool DPP, bool NT = false, bool XCD = false,
-          bool NTV = false>
+template <int MODE, int KIND, bool ADD, int RY, int W, bool DPP, bool NT = false, bool XCD = false, bool NTV = false>
 __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict__ v, const double* __restrict__ f,
                                                  const double* __restrict__ w, double* __restrict__ out,
                                                  double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
-                                                 int64_t ldz)
+                                                 int64_t ldz, int ZC)
 {
     __shared__ double red[W];
     const int lane = threadIdx.x;
@@ -411,17 +329,11 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
     }
 }
 
-template <int RY, int W, int ZC>
-dim3 rb_grid(const gs_level* L)
+dim3 rb_grid(const gs_level* L, int RY, int W, int ZC, bool oneD = false)
 {
-    return dim3((unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), (unsigned)((L->ny + RY * W - 1) / (RY * W)),
-                (unsigned)((L->nz + ZC - 1) / ZC));
-}
-template <int RY, int W, int ZC>
-dim3 rb_grid1d(const gs_level* L)
-{
-    const dim3 g = rb_grid<RY, W, ZC>(L);
-    return dim3(g.x * g.y * g.z);
+    const dim3 g((unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), (unsigned)((L->ny + RY * W - 1) / (RY * W)),
+                 (unsigned)((L->nz + ZC - 1) / ZC));
+    return oneD ? dim3(g.x * g.y * g.z) : g;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -559,17 +471,57 @@ __device__ __forceinline__ double prolong_value(const double* __restrict__ c, co
     return 0.5 * a + 0.5 * b;
 }
 
+// Fused correction, two fine x-points per lane (x odd, x+1 even): one pair load / store of v, and
+// per coarse row the two coarse values c(x>>1), c(x>>1 + 1) that both points interpolate from.
 template <bool SUB>
 __global__ __launch_bounds__(256) void k_prolong_add(const double* __restrict__ c, const double* __restrict__ sub,
                                                      double* __restrict__ fv, int fnx, int fny, int fnz, int64_t fldy,
                                                      int64_t fldz, int64_t cldy, int64_t cldz, int fz0, int cz0)
 {
-    const int x = 1 + blockIdx.x * 64 + threadIdx.x;
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    const int x = 1 + 2 * t;
     const int y = 1 + blockIdx.y * 4 + threadIdx.y;
     const int z = 1 + blockIdx.z;
     if (x > fnx || y > fny) return;
+    const int gz = z + fz0;
+    const int cx = x >> 1, cy = y >> 1, cz = (gz >> 1) - cz0;
+    const bool oy = y & 1, oz = gz & 1;
+    // X pass: e0 at fine x (odd: average of c(cx), c(cx+1)), e1 at x+1 (even: injection of c(cx+1))
+    auto X2 = [&](int jy, int jz, double& e0, double& e1) {
+        const int64_t q = cx + jy * cldy + (int64_t)jz * cldz;
+        const double a = coarse_at<SUB>(c, sub, q), b = coarse_at<SUB>(c, sub, q + 1);
+        e0 = 0.5 * a + 0.5 * b;
+        e1 = b;
+    };
+    // Y pass on top of X
+    auto Y2 = [&](int jz, double& e0, double& e1) {
+        double a0, a1;
+        X2(cy, jz, a0, a1);
+        if (!oy) {
+            e0 = a0;
+            e1 = a1;
+            return;
+        }
+        double b0, b1;
+        X2(cy + 1, jz, b0, b1);
+        e0 = 0.5 * a0 + 0.5 * b0;
+        e1 = 0.5 * a1 + 0.5 * b1;
+    };
+    double e0, e1;
+    Y2(cz, e0, e1);
+    if (oz) { // Z pass
+        double g0, g1;
+        Y2(cz + 1, g0, g1);
+        e0 = 0.5 * e0 + 0.5 * g0;
+        e1 = 0.5 * e1 + 0.5 * g1;
+    }
     const int64_t p = x + y * fldy + (int64_t)z * fldz;
-    fv[p] = fv[p] + prolong_value<SUB>(c, sub, x, y, z + fz0, cldy, cldz, cz0);
+    if (x + 1 <= fnx) {
+        const double2 v = ld2(fv + p);
+        st2s<true>(fv + p, v.x + e0, v.y + e1);
+    } else {
+        fv[p] = fv[p] + e0;
+    }
 }
 
 // Unfused reference-shaped interpolate (whole padded fine array), used by parity tests.
@@ -647,10 +599,38 @@ bool bad_level(const gs_level* L)
 
 // Dispatch a stencil pass over (mode, kind) to the fast or the generic kernel.
 // Production shape of the register-blocked kernel (chosen by tools/kbench.py on MI355X,
-// profiles/r01_kbench.json): 8 rows x 128 columns per wave, 2 waves per block, 32-plane chunks,
-// non-temporal f / output streams.
-constexpr int RB_RY = 8, RB_W = 2, RB_ZC = 32;
+// profiles/r01a_kbench.json): 8 rows x 128 columns per wave, 2 waves per block, non-temporal f /
+// output streams. The z-chunk is chosen per launch so the grid keeps >= 2048 blocks (at most 32
+// planes, at least 4); a level too small for that many 4-plane chunks runs the one-point-per-thread
+// kernel instead (coarse levels are latency-bound: parallelism beats register blocking there).
+constexpr int RB_RY = 8, RB_W = 2, RB_ZCMAX = 32, RB_ZCMIN = 4;
 constexpr bool RB_NT = true;
+
+struct PassPlan {
+    bool rb;
+    int zc;
+    dim3 grid;
+};
+
+PassPlan pass_plan(const gs_stencil* S, const gs_level* L)
+{
+    PassPlan p{false, 0, dim3(1)};
+    if (!canonical_order(S)) {
+        p.grid = gn_grid(L);
+        return p;
+    }
+    const int64_t tiles = ((L->nx + 2 * WAVE - 1) / (2 * WAVE)) * ((L->ny + RB_RY * RB_W - 1) / (RB_RY * RB_W));
+    if (tiles * ((L->nz + RB_ZCMIN - 1) / RB_ZCMIN) < 1024) {
+        p.grid = gn_grid(L);
+        return p;
+    }
+    int64_t zc = L->nz * tiles / 2048;
+    zc = zc < RB_ZCMIN ? RB_ZCMIN : (zc > RB_ZCMAX ? RB_ZCMAX : zc);
+    p.rb = true;
+    p.zc = (int)zc;
+    p.grid = rb_grid(L, RB_RY, RB_W, p.zc);
+    return p;
+}
 
 template <int KIND, bool ADD>
 int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma, const double* v,
@@ -661,15 +641,16 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
     if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
-    if (canonical_order(S)) {
-        const dim3 g = rb_grid<RB_RY, RB_W, RB_ZC>(L), b(WAVE, RB_W);
-#define GS_RB(M) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, RB_ZC, true, RB_NT>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
+    const PassPlan plan = pass_plan(S, L);
+    if (plan.rb) {
+        const dim3 g = plan.grid, b(WAVE, RB_W);
+#define GS_RB(M) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, true, RB_NT>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz, plan.zc)
         if (mode == GS_LINEAR) GS_RB(GS_LINEAR);
         else if (mode == GS_NONLINEAR) GS_RB(GS_NONLINEAR);
         else GS_RB(GS_NEWTON);
 #undef GS_RB
     } else {
-        const dim3 g = gn_grid(L), b(GN_BX, GN_BY);
+        const dim3 g = plan.grid, b(GN_BX, GN_BY);
 #define GS_GN(M) hipLaunchKernelGGL((k_generic<M, KIND, ADD>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
         if (mode == GS_LINEAR) GS_GN(GS_LINEAR);
         else if (mode == GS_NONLINEAR) GS_GN(GS_NONLINEAR);
@@ -680,33 +661,30 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
 }
 
 // ---- tuning variants of the LINEAR sweep (tools/kbench.py) -------------------------------------
+using RbKernel = void (*)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
+                          int64_t, int);
 struct Variant {
     const char* name;
-    dim3 (*grid)(const gs_level*);
-    int wy;
-    void (*kern)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t, int64_t);
+    int ry, wy, zc;
+    bool oneD;
+    RbKernel kern;
 };
-#define GS_V(RY, W, ZC, D, TAG) \
-    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, rb_grid<RY, W, ZC>, W, k_rb<GS_LINEAR, 0, false, RY, W, ZC, D>}
-#define GS_VX(RY, W, ZC, NT, X, TAG)                                                                   \
-    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, X ? rb_grid1d<RY, W, ZC> : rb_grid<RY, W, ZC>, W,          \
-     k_rb<GS_LINEAR, 0, false, RY, W, ZC, true, NT, X>}
-#define GS_VV(RY, W, ZC, TAG) \
-    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, rb_grid<RY, W, ZC>, W, k_rb<GS_LINEAR, 0, false, RY, W, ZC, true, true, false, true>}
+#define GS_VX(RY, W, ZC, NT, X, NTV, TAG) \
+    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, RY, W, ZC, X, k_rb<GS_LINEAR, 0, false, RY, W, true, NT, X, NTV>}
 const Variant kVariants[] = {
-    {"zmarch v1 64x4 zc32", zm_grid, ZM_TY, k_zmarch<GS_LINEAR, 0, false>},
-    GS_V(4, 4, 32, true, "dpp"),   GS_V(8, 2, 32, true, "dpp"), GS_V(4, 4, 32, false, "shfl"),
-    GS_VX(8, 2, 32, true, false, "dpp nt"), GS_VX(8, 1, 32, true, false, "dpp nt"),
-    GS_VX(8, 4, 32, true, false, "dpp nt"), GS_VX(8, 2, 64, true, false, "dpp nt"),
-    GS_VX(8, 2, 16, true, false, "dpp nt"), GS_VX(1, 4, 32, true, false, "dpp nt"),
-    GS_VX(2, 4, 32, true, false, "dpp nt"), GS_VX(4, 4, 32, true, false, "dpp nt"),
-    GS_VX(4, 2, 32, true, false, "dpp nt"), GS_VX(6, 2, 32, true, false, "dpp nt"),
-    GS_VX(1, 8, 32, true, false, "dpp nt"), GS_VX(2, 2, 32, true, false, "dpp nt"),
-    GS_VV(8, 2, 32, "dpp nt ntv"), GS_VV(4, 4, 32, "dpp nt ntv"), GS_VV(1, 4, 32, "dpp nt ntv"),
-    GS_VX(8, 2, 32, true, true, "dpp nt xcd"),
+    GS_VX(8, 2, 32, true, false, false, "dpp nt (production shape)"),
+    GS_VX(8, 2, 32, false, false, false, "dpp"),
+    GS_VX(4, 4, 32, true, false, false, "dpp nt"),
+    GS_VX(8, 1, 32, true, false, false, "dpp nt"),
+    GS_VX(8, 2, 16, true, false, false, "dpp nt"),
+    GS_VX(8, 2, 8, true, false, false, "dpp nt"),
+    GS_VX(8, 2, 64, true, false, false, "dpp nt"),
+    GS_VX(6, 2, 32, true, false, false, "dpp nt"),
+    GS_VX(1, 4, 32, true, false, false, "dpp nt"),
+    GS_VX(2, 4, 32, true, false, false, "dpp nt"),
+    GS_VX(8, 2, 32, true, false, true, "dpp nt ntv"),
+    GS_VX(8, 2, 32, true, true, false, "dpp nt xcd"),
 };
-#undef GS_VV
-#undef GS_V
 #undef GS_VX
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -798,7 +776,7 @@ int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L)
 {
     if (!S || !L) return 0;
     if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 1;
-    const dim3 g = canonical_order(S) ? rb_grid<RB_RY, RB_W, RB_ZC>(L) : gn_grid(L);
+    const dim3 g = pass_plan(S, L).grid;
     return (int64_t)g.x * g.y * g.z;
 }
 
@@ -856,7 +834,7 @@ int gs_prolong_add(const double* coarse_v, const double* coarse_sub, const gs_le
     const int64_t clo = (fl->z0 + 1) / 2 - cl->z0, chi = (fl->z0 + fl->nz) / 2 + 1 - cl->z0;
     if ((fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 || clo < 0 || chi > cl->nz + 1)
         return GS_EINVAL;
-    const dim3 g((unsigned)((fl->nx + 63) / 64), (unsigned)((fl->ny + 3) / 4), (unsigned)fl->nz), b(64, 4);
+    const dim3 g((unsigned)((fl->nx + 127) / 128), (unsigned)((fl->ny + 3) / 4), (unsigned)fl->nz), b(64, 4);
     if (coarse_sub)
         hipLaunchKernelGGL(k_prolong_add<true>, g, b, 0, st, coarse_v, coarse_sub, fine_v, (int)fl->nx, (int)fl->ny,
                            (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz, (int)fl->z0, (int)cl->z0);
@@ -905,7 +883,7 @@ const char* gs_strerror(int code)
 
 const char* gs_build_info(void)
 {
-    return "gpusolve_hip v3: rb(ry8 w2 zc32 dpp nt) + generic; fp-contract=off";
+    return "gpusolve_hip v4: rb(ry8 w2 zc<=32 dpp nt) large levels, 1-pt/thread small levels; fp-contract=off";
 }
 
 int gs_debug_num_variants(void) { return kNumVariants; }
@@ -924,8 +902,8 @@ int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, 
     if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
     const Variant& V = kVariants[variant];
     const Coef k = make_coef(S, L, omega, 0.0);
-    hipLaunchKernelGGL(V.kern, V.grid(L), dim3(WAVE, V.wy), 0, st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx,
-                       (int)L->ny, (int)L->nz, L->ldy, L->ldz);
+    hipLaunchKernelGGL(V.kern, rb_grid(L, V.ry, V.wy, V.zc, V.oneD), dim3(WAVE, V.wy), 0, st, k, v_in, f, nullptr,
+                       v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, V.zc);
     return launch_status();
 }
 

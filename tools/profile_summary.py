@@ -64,7 +64,8 @@ def main():
         write_bytes = write_kb * 1024
         n = bench["config"]["grid"][0] if bench else 512
         alg = 24.0 * n ** 3
-        d = {"n": n, "kernel": kname.split("(")[0], "launches_averaged": min(nf, nw),
+        d = {"n": n, "kernel": kname.replace("(anonymous namespace)::", "").split("(")[0],
+             "launches_averaged": min(nf, nw),
              "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
              "read_bytes_per_launch": read_bytes, "write_bytes_per_launch": write_bytes,
              "hbm_bytes_per_launch": read_bytes + write_bytes, "algorithmic_bytes_per_launch": alg,
