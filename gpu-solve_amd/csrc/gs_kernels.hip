@@ -598,6 +598,189 @@ bool bad_level(const gs_level* L)
 }
 
 // Dispatch a stencil pass over (mode, kind) to the fast or the generic kernel.
+// ---------------------------------------------------------------------------------------------
+// Two fused Jacobi sweeps (temporal blocking): out = S(S(v)) reading v and f once and writing once
+// (24 B per two lattice updates instead of 48). Wavefront along z: at step z the block computes
+// sweep 1 at plane z — rows y0-1..y0+RY, i.e. one recomputed halo row per side — and sweep 2 at
+// plane z-1 for rows y0..y0+RY-1. A block spans the whole x-row: WX waves of 128 columns whose
+// outside columns (of v, and of the sweep-1 values) come from the neighbour waves through LDS, so
+// nothing is recomputed along x. Where a sweep-1 point is a level boundary (x or y index 0 / n+1,
+// z index 0 / nz+1 unless zlo / zhi says that side is an internal Z-slab boundary whose two ghost
+// planes are current) its value is the boundary value itself, exactly as a stored sweep would leave
+// it. Per point the arithmetic is the single sweep's, so the result is bit-identical to two
+// gs_jacobi_sweep calls.
+template <int MODE, int RY, int WXMAX, bool NT>
+__global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __restrict__ v,
+                                                      const double* __restrict__ f, const double* __restrict__ w,
+                                                      double* __restrict__ out, int nx, int ny, int nz, int64_t ldy,
+                                                      int64_t ldz, int ZC, int zlo, int zhi)
+{
+    constexpr int NV = RY + 2;  // sweep-1 rows (j = 1..RY+2 <-> y0-1..y0+RY)
+    constexpr int NE = NV + RY; // LDS edge values per wave side: v rows + sweep-1 rows
+    __shared__ double edge[2][WXMAX][2][NE];
+    const int lane = threadIdx.x;
+    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int WX = blockDim.y;
+    const int x0 = 1 + wx * (2 * WAVE);
+    const int x = x0 + 2 * lane;
+    const int xl = min(x, nx + 1);
+    const bool bx0 = x > nx, bx1 = x + 1 > nx;            // boundary / beyond columns
+    const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
+    const int y0 = 1 + blockIdx.x * RY;
+    const int zb = 1 + blockIdx.y * ZC;
+    const int ze = min(zb + ZC - 1, nz);
+
+    int64_t roff[RY + 4]; // rows y0-2 .. y0+RY+1
+    bool rowc[RY + 4];    // row is a computable interior row
+#pragma unroll
+    for (int j = 0; j < RY + 4; j++) {
+        const int y = y0 - 2 + j;
+        roff[j] = (int64_t)min(max(y, 0), ny + 1) * ldy;
+        rowc[j] = y >= 1 && y <= ny;
+    }
+    auto planeok = [&](int z) { return (z >= 1 && z <= nz) || (z == 0 && zlo) || (z == nz + 1 && zhi); };
+    auto at = [&](const double* base, int j, int z) { return base + xl + roff[j] + (int64_t)z * ldz; };
+
+    double2 Vp[NV], Vc[RY + 4], Vn[NV], Fc[NV], Wc[NV];
+    double2 V1p[RY], V1c[NV], Fprev[RY], Wprev[RY];
+#pragma unroll
+    for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int j = 0; j < RY; j++) V1p[j] = make_double2(0.0, 0.0);
+    {
+        const int z = zb - 1;
+#pragma unroll
+        for (int j = 1; j <= NV; j++) {
+            Vp[j - 1] = ld2(at(v, j, z - 1));
+            Vn[j - 1] = ld2(at(v, j, z + 1));
+            Fc[j - 1] = ld2s<NT>(at(f, j, z));
+            if (MODE == GS_NEWTON) Wc[j - 1] = ld2(at(w, j, z));
+        }
+#pragma unroll
+        for (int j = 0; j < RY + 4; j++) Vc[j] = ld2(at(v, j, z));
+    }
+    int parity = 0;
+    for (int z = zb - 1; z <= ze + 1; z++) {
+        // ---- issue every load of plane z+1 (v rows of z+2, the two extra halo rows, f, w) ----
+        double2 Vnn[NV], Fn[NV], Wn[NV], H0, H1;
+        const bool more = z <= ze;
+        if (more) {
+#pragma unroll
+            for (int j = 1; j <= NV; j++) {
+                Vnn[j - 1] = ld2(at(v, j, z + 2));
+                Fn[j - 1] = ld2s<NT>(at(f, j, z + 1));
+                if (MODE == GS_NEWTON) Wn[j - 1] = ld2(at(w, j, z + 1));
+            }
+            H0 = ld2(at(v, 0, z + 1));
+            H1 = ld2(at(v, RY + 3, z + 1));
+        }
+        // ---- exchange the columns just outside each wave: v(z) rows 1..NV, sweep-1(z-1) rows 2..RY+1 ----
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 1; j <= NV; j++) edge[parity][wx][0][j - 1] = Vc[j].x;
+#pragma unroll
+            for (int j = 2; j <= RY + 1; j++) edge[parity][wx][0][NV + j - 2] = V1c[j - 1].x;
+        }
+        if (lane == WAVE - 1) {
+#pragma unroll
+            for (int j = 1; j <= NV; j++) edge[parity][wx][1][j - 1] = Vc[j].y;
+#pragma unroll
+            for (int j = 2; j <= RY + 1; j++) edge[parity][wx][1][NV + j - 2] = V1c[j - 1].y;
+        }
+        __syncthreads();
+        double CL[NE], CR[NE];
+#pragma unroll
+        for (int i = 0; i < NE; i++) {
+            CL[i] = wx > 0 ? edge[parity][wx - 1][1][i] : 0.0;
+            CR[i] = wx + 1 < WX ? edge[parity][wx + 1][0][i] : 0.0;
+        }
+        parity ^= 1;
+
+        // ---- sweep 1 at plane z ----
+        double2 V1n[NV];
+        const bool pz = planeok(z);
+#pragma unroll
+        for (int j = 1; j <= NV; j++) {
+            const double2 c = Vc[j], ym = Vc[j - 1], yp = Vc[j + 1], zm = Vp[j - 1], zp = Vn[j - 1];
+            const double xm0 = lane_from_left<true>(c.y, CL[j - 1]);
+            const double xp1 = lane_from_right<true>(c.x, CR[j - 1]);
+            const double wx0 = (MODE == GS_NEWTON) ? Wc[j - 1].x : 0.0, wx1 = (MODE == GS_NEWTON) ? Wc[j - 1].y : 0.0;
+            const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
+            const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
+            const double n0 = jacobi_update<MODE>(k, c.x, Fc[j - 1].x - a0, wx0);
+            const double n1 = jacobi_update<MODE>(k, c.y, Fc[j - 1].y - a1, wx1);
+            const bool keep = !pz || !rowc[j];
+            V1n[j - 1] = make_double2((keep || bx0) ? c.x : n0, (keep || bx1) ? c.y : n1);
+        }
+        // ---- sweep 2 at plane z-1 ----
+        if (z - 1 >= zb) {
+            const int64_t zo = (int64_t)(z - 1) * ldz;
+#pragma unroll
+            for (int j = 2; j <= RY + 1; j++) {
+                const double2 c = V1c[j - 1], ym = V1c[j - 2], yp = V1c[j], zm = V1p[j - 2], zp = V1n[j - 1];
+                const double xm0 = lane_from_left<true>(c.y, CL[NV + j - 2]);
+                const double xp1 = lane_from_right<true>(c.x, CR[NV + j - 2]);
+                const double wx0 = (MODE == GS_NEWTON) ? Wprev[j - 2].x : 0.0;
+                const double wx1 = (MODE == GS_NEWTON) ? Wprev[j - 2].y : 0.0;
+                const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
+                const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
+                const double o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 2].x - a0, wx0);
+                const double o1 = jacobi_update<MODE>(k, c.y, Fprev[j - 2].y - a1, wx1);
+                if (y0 - 2 + j <= ny) {
+                    double* q = out + x + roff[j] + zo;
+                    if (okx1) st2s<NT>(q, o0, o1);
+                    else if (okx0) *q = o0;
+                }
+            }
+        }
+        // ---- rotate ----
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < RY; j++) {
+                V1p[j] = V1c[j + 1];
+                Fprev[j] = Fc[j + 1];
+                if (MODE == GS_NEWTON) Wprev[j] = Wc[j + 1];
+            }
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                V1c[j] = V1n[j];
+                Vp[j] = Vc[j + 1];
+            }
+            Vc[0] = H0;
+            Vc[RY + 3] = H1;
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                Vc[j + 1] = Vn[j];
+                Vn[j] = Vnn[j];
+                Fc[j] = Fn[j];
+                if (MODE == GS_NEWTON) Wc[j] = Wn[j];
+            }
+        }
+    }
+}
+
+// Two shapes: rows of <= 512 points run 4 output rows per wave in blocks of <= 4 waves (up to 512
+// VGPRs per lane, no spills); rows of <= 1024 points run 2 output rows per wave in 8-wave blocks.
+constexpr int TB_RY_A = 4, TB_WX_A = 4, TB_RY_B = 2, TB_WX_B = 8;
+
+// Geometry rule of the fused pair: the whole x-row in one block and enough work for >= 512 blocks of
+// 4-plane chunks; the z-chunk is then chosen for >= 1024 blocks (4..32 planes).
+// Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU).
+int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block)
+{
+    if (!S || !L || !canonical_order(S) || L->nx < 1 || L->nx > 2 * WAVE * TB_WX_B || L->ny < 1 || L->nz < 1)
+        return 0;
+    const int ry = L->nx <= 2 * WAVE * TB_WX_A ? TB_RY_A : TB_RY_B;
+    const int64_t tiles = (L->ny + ry - 1) / ry;
+    const int fills = tiles * ((L->nz + 3) / 4) >= 512 ? 2 : 1;
+    int64_t c = tiles * L->nz / 1024;
+    c = c < 4 ? 4 : (c > 32 ? 32 : c);
+    *zc = (int)c;
+    *grid = dim3((unsigned)tiles, (unsigned)((L->nz + c - 1) / c));
+    *block = dim3(WAVE, (unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)));
+    return fills;
+}
+
 // Production shape of the register-blocked kernel (chosen by tools/kbench.py on MI355X,
 // profiles/r01a_kbench.json): 8 rows x 128 columns per wave, 2 waves per block, non-temporal f /
 // output streams. The z-chunk is chosen per launch so the grid keeps >= 2048 blocks (at most 32
@@ -742,8 +925,10 @@ int gs_field_layout(int64_t nx, int64_t ny, int64_t nz, int64_t* ldy, int64_t* l
     const int64_t py = ((nx + 2 + 15) / 16) * 16;
     *ldy = py;
     *ldz = py * (ny + 2);
-    *origin_offset = 15;
-    *alloc_elems = *ldz * (nz + 2) + 32;
+    // one extra plane below plane 0 and above plane nz+1 (Z-slab ghost depth 2 for the fused
+    // two-sweep kernel), plus slack for the clamped pair loads at the last row
+    *origin_offset = 15 + *ldz;
+    *alloc_elems = *ldz * (nz + 4) + 32;
     return 0;
 }
 
@@ -770,6 +955,38 @@ int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, doubl
     if (partials && L && (L->nx == 0 || L->ny == 0 || L->nz == 0))
         return (int)hipMemsetAsync(partials, 0, sizeof(double), st);
     return launch_pass<0, false>(S, L, mode, omega, gamma, v_in, f, w, v_out, partials, st);
+}
+
+int gs_jacobi_sweep2_supported(const gs_stencil* S, const gs_level* L)
+{
+    int zc;
+    dim3 g, b;
+    return (!bad_level(L) && valid_stencil(S)) ? tb2_plan(S, L, &zc, &g, &b) : 0;
+}
+
+int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                     const double* v_in, double* v_out, const double* f, const double* w, int zlo, int zhi,
+                     hipStream_t st)
+{
+    int zc;
+    dim3 g, b;
+    if (!S || bad_level(L) || !valid_stencil(S) || !v_in || !v_out || !f || v_in == v_out ||
+        (mode == GS_NEWTON && !w) || mode < GS_LINEAR || mode > GS_NEWTON || !tb2_plan(S, L, &zc, &g, &b))
+        return GS_EINVAL;
+    const Coef k = make_coef(S, L, omega, gamma);
+    const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
+#define GS_TB(M, RY, WX) hipLaunchKernelGGL((k_tb2<M, RY, WX, true>), g, b, 0, st, k, v_in, f, w, v_out, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
+    if (b.y <= (unsigned)TB_WX_A) {
+        if (mode == GS_LINEAR) GS_TB(GS_LINEAR, TB_RY_A, TB_WX_A);
+        else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_A, TB_WX_A);
+        else GS_TB(GS_NEWTON, TB_RY_A, TB_WX_A);
+    } else {
+        if (mode == GS_LINEAR) GS_TB(GS_LINEAR, TB_RY_B, TB_WX_B);
+        else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_B, TB_WX_B);
+        else GS_TB(GS_NEWTON, TB_RY_B, TB_WX_B);
+    }
+#undef GS_TB
+    return launch_status();
 }
 
 int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L)

@@ -20,6 +20,8 @@ class DevField:
         self.span = self.ldz * (nz + 2)
         # [z][y][x] view of the padded region (x extends to ldy; columns >= nx+2 are pitch padding)
         self.zyx = self.buf[origin: origin + self.span].view(nz + 2, ny + 2, self.ldy)
+        # the same including the second ghost planes z = -1 and z = nz+2
+        self.zyx_ext = self.buf[origin - self.ldz: origin + self.span + self.ldz].view(nz + 4, ny + 2, self.ldy)
 
     def level(self, h: float, z0: int = 0) -> gs_level:
         return gs_level(self.nx, self.ny, self.nz, self.ldy, self.ldz, z0, h)
@@ -33,6 +35,14 @@ class DevField:
         a = np.asarray(arr, dtype=np.float64)
         assert a.shape == (self.nx + 2, self.ny + 2, self.nz + 2), a.shape
         self.zyx[:, :, : self.nx + 2] = torch.from_numpy(np.ascontiguousarray(a.transpose(2, 1, 0))).to(self.buf.device)
+        return self
+
+    def from_xyz_ext(self, arr: np.ndarray):
+        """Set planes z = -1 .. nz+2 from an array shaped (nx+2, ny+2, nz+4)."""
+        a = np.asarray(arr, dtype=np.float64)
+        assert a.shape == (self.nx + 2, self.ny + 2, self.nz + 4), a.shape
+        self.zyx_ext[:, :, : self.nx + 2] = torch.from_numpy(np.ascontiguousarray(a.transpose(2, 1, 0))).to(
+            self.buf.device)
         return self
 
     def zero(self):

@@ -22,7 +22,9 @@
  *    (x,y,z), 0 <= x <= nx+1 etc., lives at ptr[x + y*ldy + z*ldz]  (x unit-stride, z slowest;
  *    the reference's (x,y,z) semantics, not its z-fastest storage). `ptr` is the address of
  *    padded element (0,0,0). gs_field_layout() gives the pitches and an allocation recipe that
- *    makes every interior x=1 element 128-byte aligned (speed only; any pitch >= nx+2 is correct).
+ *    makes every interior x=1 element 128-byte aligned (speed only; any pitch >= nx+2 is correct)
+ *    and provides planes z = -1 and z = nz+2 (the second ghost plane of a Z-slab, read only by the
+ *    fused two-sweep launcher gs_jacobi_sweep2 when a slab side is an internal boundary).
  *  - Stencil: 7 (value, offset) pairs in config order, offsets in {-1,0,1}. The canonical order
  *    (centre, +x, -x, +y, -y, +z, -z) of every reference config runs the LDS/register-tiled fast
  *    kernels; any other order or shape runs a generic kernel. Sums are evaluated in config order.
@@ -79,6 +81,17 @@ int gs_jacobi_sweep(const gs_stencil* S, const gs_level* L, int mode, double ome
 int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                          const double* v_in, double* v_out, const double* f, const double* w, double* partials,
                          hipStream_t stream);
+
+/* Two fused sweeps, v_out = S(S(v_in)), reading v_in / f once (temporal blocking; bit-identical to
+ * two gs_jacobi_sweep calls). gs_jacobi_sweep2_supported(S, L): 0 impossible (stencil not in
+ * canonical order, nx > 1024), 1 possible, 2 possible and large enough to fill the GPU (the driver
+ * uses it only then). zlo / zhi: the plane below local plane 1
+ * (resp. above plane nz) is an internal Z-slab boundary whose two ghost planes (0 and -1, resp.
+ * nz+1 and nz+2) of v_in are current; 0 = a level boundary. */
+int gs_jacobi_sweep2_supported(const gs_stencil* S, const gs_level* L);
+int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                     const double* v_in, double* v_out, const double* f, const double* w, int zlo, int zhi,
+                     hipStream_t stream);
 
 /* r = f - A(v) on the interior. r may be NULL (norm only). partials may be NULL (no norm);
  * otherwise it receives gs_residual_num_partials(S, L) per-block sums of r^2 in a fixed order. */

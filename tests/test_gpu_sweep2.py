@@ -1,0 +1,113 @@
+"""The fused two-sweep kernel (gs_jacobi_sweep2, temporal blocking) against two single fused
+sweeps (gs_jacobi_sweep) — bit for bit in every mode — on shapes that exercise every tile edge:
+single-wave and multi-wave rows (LDS edge exchange), both wave shapes (rows <= 512 and <= 1024),
+ragged y / z tiles, and Z-slabs with internal boundaries on one or both sides (two ghost planes)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import gpusolve as gsv  # noqa: E402
+from gpusolve.devfield import DevField  # noqa: E402
+
+
+def k():
+    assert torch.cuda.is_available()
+    return gsv.kernels()
+
+
+def st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ok(rc):
+    assert rc == 0, k().gs_strerror(rc).decode()
+
+
+S = None
+
+
+def stencil():
+    global S
+    if S is None:
+        S = gsv.Stencil().to_abi()
+    return S
+
+
+def rand_full(rng, nx, ny, nz, scale=1.0, extra=0):
+    a = np.zeros((nx + 2, ny + 2, nz + 2 + 2 * extra))
+    a[1:nx + 1, 1:ny + 1, 1 + extra: nz + 1 + extra] = rng.uniform(-scale, scale, (nx, ny, nz))
+    return a
+
+
+def two_sweeps(v0, f0, w0, mode, h):
+    nx, ny, nz = (s - 2 for s in v0.shape)
+    v, f, w, alt = DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0), \
+        DevField(nx, ny, nz).from_xyz(w0), DevField(nx, ny, nz)
+    L = v.level(h)
+    for _ in range(2):
+        ok(k().gs_jacobi_sweep(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, alt.ptr, f.ptr, w.ptr, st()))
+        v, alt = alt, v
+    return v.to_xyz()
+
+
+SHAPES = [(1, 1, 1), (2, 5, 3), (5, 4, 33), (127, 9, 17), (128, 8, 8), (129, 13, 40), (257, 6, 10), (500, 7, 9),
+          (512, 4, 5), (513, 5, 6), (1024, 3, 4), (64, 64, 64), (200, 33, 70)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_sweep2_equals_two_sweeps(shape, mode):
+    rng = np.random.default_rng(abs(hash((shape, mode))) % 2**32)
+    nx, ny, nz = shape
+    h = 1.0 / (ny + 1)
+    v0, f0, w0 = rand_full(rng, *shape), rand_full(rng, *shape, 100.0), rand_full(rng, *shape)
+    ref = two_sweeps(v0, f0, w0, mode, h)
+    v, f, w, out = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
+                    DevField(nx, ny, nz).from_xyz(w0), DevField(nx, ny, nz))
+    L = v.level(h)
+    assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(L)) >= 1
+    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, out.ptr, f.ptr, w.ptr, 0, 0, st()))
+    np.testing.assert_array_equal(out.to_xyz(), ref)
+
+
+@pytest.mark.parametrize("lo,hi", [(1, 9), (5, 14), (12, 22), (3, 3), (10, 11)])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_sweep2_on_slab_with_two_ghost_planes(lo, hi, mode):
+    rng = np.random.default_rng(lo * 100 + hi)
+    nx, ny, NZ = 130, 11, 22
+    h = 1.0 / (ny + 1)
+    v0, f0, w0 = rand_full(rng, nx, ny, NZ), rand_full(rng, nx, ny, NZ, 100.0), rand_full(rng, nx, ny, NZ)
+    ref = two_sweeps(v0, f0, w0, mode, h)
+    nzl = hi - lo + 1
+
+    def slab(a):  # global planes lo-2 .. hi+2 (clamped to the allocation: planes outside are zero)
+        out = np.zeros((nx + 2, ny + 2, nzl + 4))
+        for k_ in range(nzl + 4):
+            g = lo - 2 + k_
+            if 0 <= g <= NZ + 1:
+                out[:, :, k_] = a[:, :, g]
+        return out
+
+    v, f, w, out = (DevField(nx, ny, nzl).from_xyz_ext(slab(v0)), DevField(nx, ny, nzl).from_xyz_ext(slab(f0)),
+                    DevField(nx, ny, nzl).from_xyz_ext(slab(w0)), DevField(nx, ny, nzl))
+    L = v.level(h, lo - 1)
+    zlo, zhi = int(lo > 1), int(hi < NZ)
+    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, out.ptr, f.ptr, w.ptr, zlo, zhi,
+                            st()))
+    got = out.to_xyz()
+    np.testing.assert_array_equal(got[:, :, 1:nzl + 1], ref[:, :, lo:hi + 1])
+
+
+def test_sweep2_rejects_unsupported():
+    v = DevField(1030, 3, 4)
+    L = v.level(0.25)
+    assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(L)) == 0
+    rc = k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, DevField(1030, 3, 4).ptr, v.ptr,
+                              None, 0, 0, st())
+    assert rc == gsv._abi.GS_EINVAL
+    big = DevField(512, 512, 64)
+    assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(big.level(1 / 513))) == 2
