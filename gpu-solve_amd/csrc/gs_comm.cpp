@@ -71,17 +71,18 @@ public:
     int rank() const override { return r_; }
     int size() const override { return n_; }
 
-    void halo(double* field, int64_t ldz, int64_t nzl, hipStream_t s) override
+    void halo(double* field, int64_t ldz, int64_t nzl, int depth, hipStream_t s) override
     {
         if (n_ == 1) return;
+        const size_t cnt = (size_t)(depth * ldz);
         ncclOk(ncclGroupStart(), "ncclGroupStart");
         if (r_ > 0) {
-            ncclOk(ncclSend(field + ldz, (size_t)ldz, ncclDouble, r_ - 1, c_, s), "ncclSend");
-            ncclOk(ncclRecv(field, (size_t)ldz, ncclDouble, r_ - 1, c_, s), "ncclRecv");
+            ncclOk(ncclSend(field + ldz, cnt, ncclDouble, r_ - 1, c_, s), "ncclSend");
+            ncclOk(ncclRecv(field + (1 - depth) * ldz, cnt, ncclDouble, r_ - 1, c_, s), "ncclRecv");
         }
         if (r_ + 1 < n_) {
-            ncclOk(ncclSend(field + nzl * ldz, (size_t)ldz, ncclDouble, r_ + 1, c_, s), "ncclSend");
-            ncclOk(ncclRecv(field + (nzl + 1) * ldz, (size_t)ldz, ncclDouble, r_ + 1, c_, s), "ncclRecv");
+            ncclOk(ncclSend(field + (nzl - depth + 1) * ldz, cnt, ncclDouble, r_ + 1, c_, s), "ncclSend");
+            ncclOk(ncclRecv(field + (nzl + 1) * ldz, cnt, ncclDouble, r_ + 1, c_, s), "ncclRecv");
         }
         ncclOk(ncclGroupEnd(), "ncclGroupEnd");
     }
@@ -174,16 +175,18 @@ public:
     int rank() const override { return r_; }
     int size() const override { return h_->n_; }
 
-    void halo(double* field, int64_t ldz, int64_t nzl, hipStream_t s) override
+    void halo(double* field, int64_t ldz, int64_t nzl, int depth, hipStream_t s) override
     {
         publish(field, ldz, nzl, s);
-        const size_t bytes = sizeof(double) * (size_t)ldz;
-        if (r_ > 0) {
+        const size_t bytes = sizeof(double) * (size_t)(depth * ldz);
+        if (r_ > 0) { // rank-1's planes nzl'-depth+1 .. nzl' -> my planes 1-depth .. 0
             auto& nb = h_->slots_[r_ - 1];
             hipOk(hipStreamWaitEvent(s, nb.produced, 0), "hipStreamWaitEvent");
-            hipOk(hipMemcpyAsync(field, nb.p + nb.b * ldz, bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+            hipOk(hipMemcpyAsync(field + (1 - depth) * ldz, nb.p + (nb.b - depth + 1) * ldz, bytes,
+                                 hipMemcpyDeviceToDevice, s),
+                  "hipMemcpyAsync");
         }
-        if (r_ + 1 < size()) {
+        if (r_ + 1 < size()) { // rank+1's planes 1 .. depth -> my planes nzl+1 .. nzl+depth
             auto& nb = h_->slots_[r_ + 1];
             hipOk(hipStreamWaitEvent(s, nb.produced, 0), "hipStreamWaitEvent");
             hipOk(hipMemcpyAsync(field + (nzl + 1) * ldz, nb.p + ldz, bytes, hipMemcpyDeviceToDevice, s),

@@ -24,9 +24,10 @@ public:
     virtual int rank() const = 0;
     virtual int size() const = 0;
     // field: padded plane p of this rank's slab at field + p*ldz, local interior planes 1..nzl.
-    // Sends plane 1 to rank-1 and plane nzl to rank+1; receives rank-1's top plane into plane 0 and
-    // rank+1's bottom plane into plane nzl+1. Asynchronous on s.
-    virtual void halo(double* field, int64_t ldz, int64_t nzl, hipStream_t s) = 0;
+    // depth 1: sends plane 1 to rank-1 and plane nzl to rank+1; receives rank-1's top plane into
+    // plane 0 and rank+1's bottom plane into plane nzl+1. depth 2 (nzl >= 2): the two outermost
+    // planes each way, into planes -1..0 and nzl+1..nzl+2. Asynchronous on s.
+    virtual void halo(double* field, int64_t ldz, int64_t nzl, int depth, hipStream_t s) = 0;
     // out[r] <- rank r's *in, on every rank (out holds size() doubles). Asynchronous on s.
     virtual void allgather1(const double* in, double* out, hipStream_t s) = 0;
     // field: a full-size level on every rank; rank r has computed planes [lo[r], hi[r]]; afterwards

@@ -126,6 +126,12 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s);
         L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), L.lo - 1, L.h};
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
+        L.minPlanes = nz;
+        if (L.distributed)
+            for (int q = 0; q < nranks(); q++) L.minPlanes = std::min(L.minPlanes, L.ranksHi[q] - L.ranksLo[q] + 1);
+        static const bool noPairs = std::getenv("GS_NO_FUSED_SWEEPS") != nullptr;
+        L.fusedPairs = !noPairs && gs_jacobi_sweep2_supported(&stencilAbi, &L.geom) == 2 &&
+                       (!L.distributed || L.minPlanes >= 2);
     }
     if (mode == NEWTON) newtonF = DeviceField(levels_[0].geom.nx, levels_[0].geom.ny, levels_[0].geom.nz, s);
     // the overlapped sweep splits a level into 3 launches, each with its own partials region
@@ -140,6 +146,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
     // a slab evaluates it at its global plane indices (geom.z0)
     check(gs_rhs_init(&levels_[0].geom, levels_[0].f.data(), (int)mode, 1.0 / (gridDim[1] + 1), gamma, s),
           "gs_rhs_init");
+    halo(levels_[0], levels_[0].f, s); // the fused pair's first sweep reads f on a ghost plane
     check((int)hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
@@ -162,9 +169,9 @@ double HipGridData::readNorm()
     return *hNorm_;
 }
 
-void HipGridData::halo(LevelData& L, DeviceField& fld, hipStream_t s)
+void HipGridData::halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth)
 {
-    if (L.distributed && nranks() > 1) comm_->halo(fld.data(), fld.ldz(), L.geom.nz, s);
+    if (L.distributed && nranks() > 1) comm_->halo(fld.data(), fld.ldz(), L.geom.nz, depth, s);
 }
 
 void HipGridData::gather(LevelData& L, DeviceField& fld)
@@ -210,6 +217,23 @@ int64_t sweepPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64
     return partials ? gs_residual_num_partials(&g.stencilAbi, &sub) : 0;
 }
 
+// two fused sweeps over local planes [z1, z2]: reads L.v (two ghost planes deep where a side is an
+// internal boundary), writes L.vAlt
+void pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_t z2, hipStream_t s)
+{
+    if (z2 < z1) return;
+    gs_level sub = L.geom;
+    sub.nz = z2 - z1 + 1;
+    sub.z0 += z1 - 1;
+    const int64_t off = (z1 - 1) * L.geom.ldz;
+    const bool dist = L.distributed && g.nranks() > 1;
+    const int zlo = z1 > 1 || (dist && g.rank() > 0);
+    const int zhi = z2 < L.geom.nz || (dist && g.rank() + 1 < g.nranks());
+    check(gs_jacobi_sweep2(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.v.data() + off, L.vAlt.data() + off,
+                           L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr, zlo, zhi, s),
+          "gs_jacobi_sweep2");
+}
+
 bool transitionLevel(HipGridData& g, std::size_t l)
 {
     return l > 0 && g.nranks() > 1 && !g.getLevel(l).distributed && g.getLevel(l - 1).distributed;
@@ -231,7 +255,7 @@ void restrictTo(HipGridData& g, const DeviceField& src, std::size_t l, DeviceFie
         if (b) g.gather(C, *b);
     } else if (needGhosts) {
         g.halo(C, a, s);
-        if (b) g.halo(C, *b, s);
+        if (b) g.halo(C, *b, s, g.vDepth(C)); // b is the coarse iterate (FAS)
     }
 }
 
@@ -299,32 +323,42 @@ double HipSolver::compResidual(HipGridData& grid, std::size_t l, bool storeR, bo
     return finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L.geom));
 }
 
-// k fused sweeps (src/cpu/CpuSolver.cpp:141-180): each reads v, writes vAlt, then the two swap.
-// On a Z-slab the two boundary planes are computed first; their halo exchange then runs on the
-// comm stream while the interior planes are swept on the compute stream.
+// k sweeps (src/cpu/CpuSolver.cpp:141-180). Each reads v and writes vAlt, then the two swap. Where
+// the level allows, sweeps run in fused pairs (gs_jacobi_sweep2: one read of v and f, one write, for
+// two sweeps), an odd one as a single sweep. On a Z-slab the outermost planes (one per side for a
+// sweep, two for a pair) are computed first; their ghost exchange then runs on the comm stream while
+// the interior planes are computed on the compute stream.
 void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
 {
     auto& L = grid.getLevel(l);
     const hipStream_t s = grid.stream();
     const bool dist = L.distributed && grid.nranks() > 1;
     const int64_t nz = L.geom.nz;
-    for (std::size_t i = 0; i < sweeps; i++) {
+    const int depth = grid.vDepth(L);
+    while (sweeps > 0) {
+        const bool pair = L.fusedPairs && sweeps >= 2;
+        const int64_t b = pair ? 2 : depth; // outermost planes whose ghost copies the neighbours need
+        auto run = [&](int64_t z1, int64_t z2) {
+            if (pair) pairPlanes(grid, L, z1, z2, s);
+            else sweepPlanes(grid, L, z1, z2, s);
+        };
         if (!dist) {
-            sweepPlanes(grid, L, 1, nz, s);
-        } else if (grid.overlapHalo && nz >= 3) {
-            sweepPlanes(grid, L, 1, 1, s);
-            sweepPlanes(grid, L, nz, nz, s);
+            run(1, nz);
+        } else if (grid.overlapHalo && nz >= 2 * b + 1) {
+            run(1, b);
+            run(nz - b + 1, nz);
             check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
             check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
-            grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, grid.commStream());
+            grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, grid.commStream());
             check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
-            sweepPlanes(grid, L, 2, nz - 1, s);
+            run(b + 1, nz - b);
             check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
         } else {
-            sweepPlanes(grid, L, 1, nz, s);
-            grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, s);
+            run(1, nz);
+            grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, s);
         }
         L.v.swap(L.vAlt);
+        sweeps -= pair ? 2 : 1;
     }
 }
 
@@ -335,20 +369,21 @@ double HipSolver::speculativeSweep(HipGridData& grid)
     const int64_t nz = L.geom.nz;
     double* P = grid.partials();
     int64_t n = 0;
+    const int depth = grid.vDepth(L);
     if (!(L.distributed && grid.nranks() > 1)) {
         n = sweepPlanes(grid, L, 1, nz, s, P);
-    } else if (grid.overlapHalo && nz >= 3) {
-        n += sweepPlanes(grid, L, 1, 1, s, P + n);
-        n += sweepPlanes(grid, L, nz, nz, s, P + n);
+    } else if (grid.overlapHalo && nz >= 2 * depth + 1) {
+        n += sweepPlanes(grid, L, 1, depth, s, P + n);
+        n += sweepPlanes(grid, L, nz - depth + 1, nz, s, P + n);
         check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
         check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
-        grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, grid.commStream());
+        grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, grid.commStream());
         check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
-        n += sweepPlanes(grid, L, 2, nz - 1, s, P + n);
+        n += sweepPlanes(grid, L, depth + 1, nz - depth, s, P + n);
         check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
     } else {
         n = sweepPlanes(grid, L, 1, nz, s, P);
-        grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, s);
+        grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, s);
     }
     return finishNorm(grid, n);
 }
@@ -376,7 +411,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, bool* pending)
         auto& L = grid.getLevel(i);
         auto& C = grid.getLevel(i + 1);
         compResidual(grid, i, true, false);
-        restrictTo(grid, L.r, i, C.f, nullptr, false); // f^2h = R r^h (read point-wise only: no ghosts)
+        restrictTo(grid, L.r, i, C.f, nullptr, true); // f^2h = R r^h (ghosts: the fused pair reads them)
         if (grid.mode != GridParams::NONLINEAR) {
             C.v.zero(s);
         } else {
@@ -384,6 +419,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, bool* pending)
             restrictTo(grid, L.v, i, C.restV, &C.v, true);
             check(gs_apply_op_add(&grid.stencilAbi, &C.geom, grid.gamma, C.restV.data(), C.f.data(), s),
                   "gs_apply_op_add");
+            grid.halo(C, C.f, s);
         }
     }
     jacobi(grid, nl - 1, grid.preSmoothing + grid.postSmoothing); // coarsest "solve"
@@ -394,7 +430,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, bool* pending)
         check(gs_prolong_add(C.v.data(), grid.mode == GridParams::NONLINEAR ? C.restV.data() : nullptr, &C.geom,
                              F.v.data(), &F.geom, s),
               "gs_prolong_add");
-        grid.halo(F, F.v, s);
+        grid.halo(F, F.v, s, grid.vDepth(F));
         jacobi(grid, i - 1, grid.postSmoothing);
     }
     if (pending && speculationEnabled(grid)) {
@@ -441,6 +477,7 @@ double NewtonSolver::compF(HipGridData& grid)
     check(gs_newton_F(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), grid.newtonF.data(), L0.f.data(),
                       grid.partials(), grid.stream()),
           "gs_newton_F");
+    grid.halo(L0, L0.f, grid.stream());
     return HipSolver::finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L0.geom));
 }
 

@@ -69,7 +69,9 @@ public:
         double h = 0.0;
         gs_level geom{};     // kernel-side geometry of the stored array (slab or full level)
         bool distributed = false;
+        bool fusedPairs = false; // smoothing runs as fused sweep pairs (gs_jacobi_sweep2)
         int64_t lo = 1, hi = 0; // this rank's owned global planes (== 1..nz when not distributed)
+        int64_t minPlanes = 0;  // fewest planes any rank owns on this level
         std::vector<int64_t> ranksLo, ranksHi; // every rank's owned planes (gather of replicated levels)
     };
 
@@ -96,8 +98,10 @@ public:
     double* dRankSums() const { return dRankSums_; }
     double readNorm(); // async D2H of dNorm + stream sync: the one host sync per V-cycle
 
-    // ghost planes of a distributed level's field (no-op otherwise)
-    void halo(LevelData& L, DeviceField& fld, hipStream_t s);
+    // ghost planes of a distributed level's field (no-op otherwise); depth 2 where possible for
+    // iterate fields (the fused pair reads two ghost planes of v)
+    void halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth = 1);
+    int vDepth(const LevelData& L) const { return L.minPlanes >= 2 ? 2 : 1; }
     // replicated level fed from a distributed parent: assemble every rank's owned planes
     void gather(LevelData& L, DeviceField& fld);
     // geometry + pointer offset of the planes this rank computes on level L
