@@ -2,20 +2,23 @@
 """bench.py — BASELINE.json's metric on MI355X:
    "MLUPS (Jacobi smoother) + V-cycle wall-time, 512^3 fp64; achieved HBM GB/s %peak".
 
-A step = one fused damped-Jacobi sweep (residual + update, 7-point stencil, fp64, LINEAR mode) over
-level 0 of the 512^3 grid of BASELINE config #3, i.e. one pass of the hot path over 512^3 lattice
-updates; value = lattice updates of all ranks / max-over-ranks wall time (MLUPS). Inputs are
-resident in HBM before the timed region. The V-cycle wall time (512^3, 2+2, including the 8-byte
-norm readback) is measured after the timed region and reported under "vcycle".
+A step = one damped-Jacobi sweep (residual + update, 7-point stencil, fp64, LINEAR mode) over level 0
+of the 512^3 grid of BASELINE config #3 (512^3 lattice updates). The K timed sweeps run exactly as
+the solver runs its 2+2 smoothing: in fused pairs (gs_jacobi_sweep2, temporal blocking: one read of
+v and f and one write per pair), an odd last sweep alone. value = lattice updates of all ranks /
+max-over-ranks wall time (MLUPS). Inputs are resident in HBM before the timed region. The one-sweep
+kernel is also timed on its own ("single_sweep_kernel"), and the V-cycle wall time (512^3, 2+2,
+including the 8-byte norm readback) is measured after the timed region ("vcycle").
 
 Multi-GPU (torchrun, one process per GPU): the grid is Z-slab partitioned over RCCL (xGMI), ghost
 planes exchanged every sweep on a second stream while the interior planes are swept; weak scaling
 with 512^3 lattice points per rank: N=2 -> 1024x512x512, N=4 -> 1024x1024x512, N=8 -> 1024^3
 (BASELINE config #5); other N -> 512x512x(512N).
 
-Roofline: the smoother is HBM-bound (0.5 flop/B); algorithmic bytes = 24 B per lattice update
-(read v, read f, write v_new) x 512^3 per launch / average launch duration measured
-with HIP events on the solver's stream; peak = 8000 GB/s (MI355X HBM3E, MI355X_MICROARCH.md).
+Roofline: the smoother is HBM-bound (0.5 flop/B per sweep); algorithmic bytes per launch = 24 B
+per lattice point (read v, read f, write the result) x 512^3, for a single sweep
+and for a fused pair alike / the average launch duration measured with HIP events on the solver's
+stream; peak = 8000 GB/s (MI355X HBM3E, MI355X_MICROARCH.md).
 cpu_baseline: the reference's own CpuSolver::jacobi (oracle/_ref/ref_probe, compiled from
 /root/reference/src/cpu) on this host's cores, a bounded sample of the same workload.
 """
@@ -121,6 +124,39 @@ def make_grid(params, rank, world):
     return grid
 
 
+def single_sweep_timing(grid, dims, k):
+    """The one-sweep kernel alone (gs_jacobi_sweep on the grid's level-0 fields), for reference."""
+    import ctypes as C
+    from gpusolve.devfield import DevField
+    kl, drv = gsv.kernels(), gsv.driver()
+    L = grid.getLevel(0).geom
+    S = grid.params.stencil.to_abi()
+    v = drv.gs_grid_field(grid.handle, 0, 0)
+    f = drv.gs_grid_field(grid.handle, 0, 3)
+    tmp = DevField(L.nx, L.ny, L.nz)
+    st = grid.stream()
+    stream = torch.cuda.ExternalStream(st)
+    a_, b_ = v, tmp.ptr
+    for _ in range(2):
+        kl.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, a_, b_, f, None, st)
+        a_, b_ = b_, a_
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(k):
+        kl.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, a_, b_, f, None, st)
+        a_, b_ = b_, a_
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if k % 2:  # leave the iterate in the grid's own buffer
+        kl.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, a_, b_, f, None, st)
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / k
+    pts = float(L.nx) * L.ny * L.nz
+    gbps = BYTES_PER_LUP * pts / (ms * 1e-3) / 1e9
+    return {"kernel": "k_rb (one sweep per launch)", "ms": round(ms, 4), "mlups": round(pts / ms / 1e3, 1),
+            "achieved_GBps": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,30 +179,36 @@ def main():
     drv = gsv.driver()
     stream = torch.cuda.ExternalStream(grid.stream())
 
-    def sweep():
-        rc = drv.gs_grid_jacobi(grid.handle, 0, 1)
+    def sweeps(k):
+        """k level-0 Jacobi sweeps through the driver (fused pairs where the level allows)."""
+        rc = drv.gs_grid_jacobi(grid.handle, 0, k)
         if rc:
             raise gsv.GpuSolveError(drv.gs_last_error().decode())
 
-    for _ in range(a.warmup):
-        sweep()
+    fused = drv.gs_grid_level_fused(grid.handle, 0) == 1
+    sweeps(a.warmup)
     grid.sync()
     barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(a.steps):
-        sweep()
+    sweeps(a.steps)
     ev1.record(stream)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / a.steps  # average launch duration on the solver's stream
+    # passes over the level: a fused pair reads v and f once and writes once, like a single sweep
+    passes = (a.steps // 2 + a.steps % 2) if fused else a.steps
+    kernel_ms = ev0.elapsed_time(ev1) / passes  # average pass duration on the solver's stream
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
+
+    single = None
+    if world == 1:
+        single = single_sweep_timing(grid, dims, a.steps)
 
     lups_per_rank = float(dims[0]) * dims[1] * dims[2] / world
     total_lups = lups_per_rank * a.steps * world
@@ -219,7 +261,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_GBPS, 4),
                          "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
+                         "kernel": ("k_tb2: two fused sweeps per launch (24 B per point per launch)" if fused
+                                    else "k_rb: one sweep per launch (24 B per point per launch)"),
                          "algorithmic_bytes_per_launch": BYTES_PER_LUP * lups_per_rank},
+            "single_sweep_kernel": single,
             "vcycle": vc,
             "cpu_baseline": cpu,
             "kernel_build": gsv.build_info(),

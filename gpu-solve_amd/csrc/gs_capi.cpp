@@ -191,6 +191,12 @@ int gs_grid_residual_norm(void* grid, int level, double* norm)
 
 int gs_grid_num_levels(void* grid) { return (int)G(grid).numLevels(); }
 
+int gs_grid_level_fused(void* grid, int level)
+{
+    if (level < 0 || level >= (int)G(grid).numLevels()) return 0;
+    return G(grid).getLevel(level).fusedPairs ? 1 : 0;
+}
+
 int gs_grid_level(void* grid, int level, gs_level* out)
 {
     if (level < 0 || level >= (int)G(grid).numLevels() || !out) return 1;

@@ -81,6 +81,7 @@ DRIVER_API = {
     "gs_grid_jacobi": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "gs_grid_residual_norm": (C.c_int, [C.c_void_p, C.c_int, dptr]),
     "gs_grid_num_levels": (C.c_int, [C.c_void_p]),
+    "gs_grid_level_fused": (C.c_int, [C.c_void_p, C.c_int]),
     "gs_grid_level": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(gs_level)]),
     "gs_grid_field": (C.c_void_p, [C.c_void_p, C.c_int, C.c_int]),
     "gs_grid_stream": (C.c_void_p, [C.c_void_p]),

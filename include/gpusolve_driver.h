@@ -51,6 +51,8 @@ int gs_grid_vcycle(void* grid, double* residual);
 int gs_grid_jacobi(void* grid, int level, int sweeps);
 int gs_grid_residual_norm(void* grid, int level, double* norm);
 int gs_grid_num_levels(void* grid);
+/* 1 if the level's smoothing runs as fused sweep pairs (gs_jacobi_sweep2), else 0. */
+int gs_grid_level_fused(void* grid, int level);
 int gs_grid_level(void* grid, int level, gs_level* out);
 /* field: 0 v (current iterate), 1 restV, 2 newtonV, 3 f, 4 r, 5 newtonF (level 0). NULL if absent. */
 double* gs_grid_field(void* grid, int level, int field);

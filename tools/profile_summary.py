@@ -22,7 +22,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def sweep_kernel(name):
-    return "k_rb<0, 0, false" in name or "k_zmarch<0, 0, false" in name
+    """The level-0 smoother of bench.py: the fused pair (k_tb2) or, without it, the one-sweep k_rb."""
+    return "k_tb2<0," in name
+
+
+def single_kernel(name):
+    return "k_rb<0, 0, false" in name
 
 
 def main():
@@ -46,7 +51,10 @@ def main():
         fn = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(fn):
             continue
-        rows = [r for r in csv.DictReader(open(fn)) if sweep_kernel(r["Kernel_Name"]) and r["Counter_Name"] == counter]
+        allrows = list(csv.DictReader(open(fn)))
+        rows = [r for r in allrows if sweep_kernel(r["Kernel_Name"]) and r["Counter_Name"] == counter]
+        if not rows:
+            rows = [r for r in allrows if single_kernel(r["Kernel_Name"]) and r["Counter_Name"] == counter]
         if not rows:
             continue
         big = max(int(r["Grid_Size"]) for r in rows)
