@@ -281,11 +281,8 @@ int gs_grid_time_vcycles(void* grid, int cycles, double* ms, double* last_residu
     return guarded([&] {
         auto& g = G(grid);
         // the solve loop's steady state: speculative closing norms (HipSolver::solve)
-        bool pending = false;
-        if (gs::HipSolver::speculationEnabled(g)) {
-            gs::HipSolver::speculativeSweep(g);
-            pending = true;
-        }
+        int pending = 0;
+        if (gs::HipSolver::speculationEnabled(g)) gs::HipSolver::speculativeSweep(g, &pending);
         gs::check((int)hipStreamSynchronize(g.stream()), "hipStreamSynchronize");
         const auto t0 = std::chrono::steady_clock::now();
         double r = 0;

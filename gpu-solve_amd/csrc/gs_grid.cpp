@@ -126,6 +126,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s);
         L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), L.lo - 1, L.h};
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
+        maxParts = std::max(maxParts, gs_jacobi_sweep2_num_partials(&stencilAbi, &L.geom));
         L.minPlanes = nz;
         if (L.distributed)
             for (int q = 0; q < nranks(); q++) L.minPlanes = std::min(L.minPlanes, L.ranksHi[q] - L.ranksLo[q] + 1);
@@ -218,10 +219,12 @@ int64_t sweepPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64
 }
 
 // two fused sweeps over local planes [z1, z2]: reads L.v (two ghost planes deep where a side is an
-// internal boundary), writes L.vAlt
-void pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_t z2, hipStream_t s)
+// internal boundary), writes L.vAlt; with partials, also the per-block r^2 sums of the input's
+// residual. Returns the partial count written.
+int64_t pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_t z2, hipStream_t s,
+                   double* partials = nullptr)
 {
-    if (z2 < z1) return;
+    if (z2 < z1) return 0;
     gs_level sub = L.geom;
     sub.nz = z2 - z1 + 1;
     sub.z0 += z1 - 1;
@@ -229,9 +232,11 @@ void pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_t z
     const bool dist = L.distributed && g.nranks() > 1;
     const int zlo = z1 > 1 || (dist && g.rank() > 0);
     const int zhi = z2 < L.geom.nz || (dist && g.rank() + 1 < g.nranks());
-    check(gs_jacobi_sweep2(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.v.data() + off, L.vAlt.data() + off,
-                           L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr, zlo, zhi, s),
+    check(gs_jacobi_sweep2_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.v.data() + off,
+                                L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
+                                zlo, zhi, partials, s),
           "gs_jacobi_sweep2");
+    return partials ? gs_jacobi_sweep2_num_partials(&g.stencilAbi, &sub) : 0;
 }
 
 bool transitionLevel(HipGridData& g, std::size_t l)
@@ -275,9 +280,8 @@ void HipSolver::solve(HipGridData& grid)
 {
     const bool print = grid.printProgress && grid.rank() == 0;
     const bool spec = speculationEnabled(grid);
-    bool pending = false;
-    const double initialResidual = spec ? speculativeSweep(grid) : compResidual(grid, 0, false, true);
-    pending = spec;
+    int pending = 0;
+    const double initialResidual = spec ? speculativeSweep(grid, &pending) : compResidual(grid, 0, false, true);
     if (history) history->push_back(initialResidual);
     if (print) std::cout << "Inital residual: " << initialResidual << '\n';
 
@@ -362,29 +366,38 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
     }
 }
 
-double HipSolver::speculativeSweep(HipGridData& grid)
+// The first pre-smoothing step of the next cycle, run into vAlt (v untouched) with the norm of the
+// residual of v: a fused pair when level 0 smooths in pairs and pre-smoothing has two sweeps, else
+// one sweep. *sweeps = how many sweeps vAlt holds.
+double HipSolver::speculativeSweep(HipGridData& grid, int* sweeps)
 {
     auto& L = grid.getLevel(0);
     const hipStream_t s = grid.stream();
     const int64_t nz = L.geom.nz;
     double* P = grid.partials();
     int64_t n = 0;
+    const bool pair = L.fusedPairs && grid.preSmoothing >= 2;
     const int depth = grid.vDepth(L);
+    const int64_t b = pair ? 2 : depth;
+    auto run = [&](int64_t z1, int64_t z2) {
+        n += pair ? pairPlanes(grid, L, z1, z2, s, P + n) : sweepPlanes(grid, L, z1, z2, s, P + n);
+    };
     if (!(L.distributed && grid.nranks() > 1)) {
-        n = sweepPlanes(grid, L, 1, nz, s, P);
-    } else if (grid.overlapHalo && nz >= 2 * depth + 1) {
-        n += sweepPlanes(grid, L, 1, depth, s, P + n);
-        n += sweepPlanes(grid, L, nz - depth + 1, nz, s, P + n);
+        run(1, nz);
+    } else if (grid.overlapHalo && nz >= 2 * b + 1) {
+        run(1, b);
+        run(nz - b + 1, nz);
         check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
         check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
         grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, grid.commStream());
         check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
-        n += sweepPlanes(grid, L, depth + 1, nz - depth, s, P + n);
+        run(b + 1, nz - b);
         check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
     } else {
-        n = sweepPlanes(grid, L, 1, nz, s, P);
+        run(1, nz);
         grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, s);
     }
+    if (sweeps) *sweeps = pair ? 2 : 1;
     return finishNorm(grid, n);
 }
 
@@ -396,16 +409,16 @@ void HipSolver::restrict(HipGridData& grid, const DeviceField& src, std::size_t 
 double HipSolver::vcycle(HipGridData& grid) { return vcycleSpeculative(grid, nullptr); }
 
 // src/cpu/CpuSolver.cpp:85-139
-double HipSolver::vcycleSpeculative(HipGridData& grid, bool* pending)
+double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
 {
     const std::size_t nl = grid.numLevels();
     const hipStream_t s = grid.stream();
     for (std::size_t i = 0; i + 1 < nl; i++) {
         std::size_t pre = grid.preSmoothing;
-        if (i == 0 && pending && *pending && pre > 0) {
-            grid.getLevel(0).v.swap(grid.getLevel(0).vAlt); // adopt the speculative first sweep
-            *pending = false;
-            pre--;
+        if (i == 0 && pending && *pending > 0 && pre >= (std::size_t)*pending) {
+            grid.getLevel(0).v.swap(grid.getLevel(0).vAlt); // adopt the speculative first sweep(s)
+            pre -= (std::size_t)*pending;
+            *pending = 0;
         }
         jacobi(grid, i, pre);
         auto& L = grid.getLevel(i);
@@ -433,10 +446,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, bool* pending)
         grid.halo(F, F.v, s, grid.vDepth(F));
         jacobi(grid, i - 1, grid.postSmoothing);
     }
-    if (pending && speculationEnabled(grid)) {
-        *pending = true;
-        return speculativeSweep(grid);
-    }
+    if (pending && speculationEnabled(grid)) return speculativeSweep(grid, pending);
     return compResidual(grid, 0, false, true);
 }
 

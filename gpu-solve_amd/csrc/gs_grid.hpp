@@ -129,10 +129,12 @@ public:
     static double compResidual(HipGridData& grid, std::size_t level, bool storeR, bool norm);
     static double vcycle(HipGridData& grid);
     // The solve loop's V-cycle: with speculation on, a cycle's closing norm comes out of the first
-    // pre-smoothing sweep of the next cycle (same residual, computed by the sweep anyway), run
-    // into vAlt without swapping; *pending says vAlt holds it and the next cycle adopts it.
-    static double vcycleSpeculative(HipGridData& grid, bool* pending);
-    static double speculativeSweep(HipGridData& grid); // level-0 sweep v -> vAlt (no swap) + norm of f - A v
+    // pre-smoothing step of the next cycle (same residual, computed by that step anyway: one sweep
+    // or a fused pair), run into vAlt without swapping; *pending = how many sweeps vAlt holds (0:
+    // none), and the next cycle adopts them.
+    static double vcycleSpeculative(HipGridData& grid, int* pending);
+    // level-0 sweep or pair v -> vAlt (no swap) + norm of f - A v; *sweeps = sweeps run
+    static double speculativeSweep(HipGridData& grid, int* sweeps);
     static bool speculationEnabled(const HipGridData& grid);
     static void jacobi(HipGridData& grid, std::size_t level, std::size_t sweeps);
     static double finishNorm(HipGridData& grid, int64_t nparts);

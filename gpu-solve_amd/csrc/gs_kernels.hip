@@ -111,9 +111,9 @@ __device__ __forceinline__ double wave_sum(double x)
     return x;
 }
 
-// Block-wide fixed-order sum; result valid in thread 0. nwaves <= 16.
+// Block-wide fixed-order sum of nw <= NWAVES waves (default: all); result valid in thread 0.
 template <int NWAVES>
-__device__ __forceinline__ double block_sum(double x, double* lds)
+__device__ __forceinline__ double block_sum(double x, double* lds, int nw = NWAVES)
 {
     const int tid = threadIdx.x + threadIdx.y * blockDim.x;
     x = wave_sum(x);
@@ -122,7 +122,8 @@ __device__ __forceinline__ double block_sum(double x, double* lds)
     double t = 0.0;
     if (tid == 0) {
 #pragma unroll
-        for (int i = 0; i < NWAVES; i++) t += lds[i];
+        for (int i = 0; i < NWAVES; i++)
+            if (i < nw) t += lds[i];
     }
     return t;
 }
@@ -238,88 +239,88 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
 #pragma unroll
     for (int r = 0; r < RY + 2; r++) roff[r] = (int64_t)min(y0 - 1 + r, ny + 1) * ldy;
 
-    double2 P[RY], C[RY + 2], N[RY], F[RY], Wc[RY];
-    double CL[RY], CR[RY];
+    // Planes z-1 (P) and z (C) of the wave's rows live in registers. Everything of plane z+1 (its
+    // halo rows, f, w, tile edges) and the v rows of plane z+2 is loaded into slot ph of a two-slot
+    // ring while plane z is computed from the other slot, and only moved out after it was consumed:
+    // a load's destination is never copied before its first use, so its wait lands one full plane
+    // of arithmetic after the issue (the loop is unrolled by two to make the slot index static).
+    double2 P[RY], C[RY], NL[2][RY], FL[2][RY], WL[2][RY], HL[2][2];
+    double EL[2][RY], ER[2][RY];
     double sumsq = 0.0;
+    // slot s <- plane z1's halo rows, f, w, edges and plane z2's v rows (plane offsets)
+    auto load_slot = [&](const int s, const int64_t z1, const int64_t z2) {
+#pragma unroll
+        for (int r = 0; r < RY; r++) {
+            NL[s][r] = ld2s<NTV>(v + xl + roff[r + 1] + z2);
+            if (KIND != 2 || ADD) FL[s][r] = ld2s<NT>(fin + xl + roff[r + 1] + z1);
+            if (MODE == GS_NEWTON) WL[s][r] = ld2(w + xl + roff[r + 1] + z1);
+            EL[s][r] = v[xle + roff[r + 1] + z1];
+            ER[s][r] = v[xre + roff[r + 1] + z1];
+        }
+        HL[s][0] = ld2(v + xl + roff[0] + z1);
+        HL[s][1] = ld2(v + xl + roff[RY + 1] + z1);
+    };
     if (zb <= ze) {
         const int64_t zo = (int64_t)zb * ldz;
 #pragma unroll
         for (int r = 0; r < RY; r++) {
             P[r] = ld2(v + xl + roff[r + 1] + zo - ldz);
-            N[r] = ld2(v + xl + roff[r + 1] + zo + ldz);
-            if (KIND != 2 || ADD) F[r] = ld2s<NT>(fin + xl + roff[r + 1] + zo);
-            if (MODE == GS_NEWTON) Wc[r] = ld2(w + xl + roff[r + 1] + zo);
-            CL[r] = v[xle + roff[r + 1] + zo];
-            CR[r] = v[xre + roff[r + 1] + zo];
+            C[r] = ld2(v + xl + roff[r + 1] + zo);
         }
-#pragma unroll
-        for (int r = 0; r < RY + 2; r++) C[r] = ld2(v + xl + roff[r] + zo);
+        load_slot(1, zo, zo + ldz);
     }
-    for (int z = zb; z <= ze; z++) {
-        const int64_t zo = (int64_t)z * ldz;
-        // ---- issue every load of plane z+1 (and the v rows of plane z+2) ----
-        double2 NN[RY], H0, H1, FN[RY], WN[RY];
-        double ELn[RY], ERn[RY];
-        const bool more = z < ze;
-        if (more) {
-            const int64_t z1 = zo + ldz;
+    // Both halves always run (an odd chunk ends with one step whose results are discarded), and
+    // the loads of every step are unconditional (plane indices clamped into the padded range), so
+    // the slots keep fixed registers around the loop.
+    for (int z0 = zb; z0 <= ze; z0 += 2) {
+#pragma unroll
+        for (int ph = 0; ph < 2; ph++) {
+            const int z = z0 + ph;
+            const bool real = z <= ze;
+            const int cs = ph ^ 1; // slot holding plane z
+            const int64_t zo = (int64_t)z * ldz;
+            load_slot(ph, (int64_t)min(z + 1, nz + 1) * ldz, (int64_t)min(z + 2, nz + 1) * ldz);
 #pragma unroll
             for (int r = 0; r < RY; r++) {
-                NN[r] = ld2s<NTV>(v + xl + roff[r + 1] + z1 + ldz);
-                if (KIND != 2 || ADD) FN[r] = ld2s<NT>(fin + xl + roff[r + 1] + z1);
-                if (MODE == GS_NEWTON) WN[r] = ld2(w + xl + roff[r + 1] + z1);
-                ELn[r] = v[xle + roff[r + 1] + z1];
-                ERn[r] = v[xre + roff[r + 1] + z1];
+                const double2 c = C[r], ym = r == 0 ? HL[cs][0] : C[r - 1], yp = r == RY - 1 ? HL[cs][1] : C[r + 1];
+                const double2 zm = P[r], zp = NL[cs][r];
+                const double xm0 = lane_from_left<DPP>(c.y, EL[cs][r]);
+                const double xp1 = lane_from_right<DPP>(c.x, ER[cs][r]);
+                const double wx = (MODE == GS_NEWTON) ? WL[cs][r].x : 0.0;
+                const double wy = (MODE == GS_NEWTON) ? WL[cs][r].y : 0.0;
+                const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
+                const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
+                double r0 = 0.0, r1 = 0.0; // residual of the input iterate
+                if (KIND != 2 || ADD) {
+                    r0 = FL[cs][r].x - a0;
+                    r1 = FL[cs][r].y - a1;
+                }
+                double o0, o1;
+                if (KIND == 0) {
+                    o0 = jacobi_update<MODE>(k, c.x, r0, wx);
+                    o1 = jacobi_update<MODE>(k, c.y, r1, wy);
+                } else if (KIND == 1) {
+                    o0 = r0;
+                    o1 = r1;
+                } else {
+                    o0 = ADD ? FL[cs][r].x + a0 : a0;
+                    o1 = ADD ? FL[cs][r].y + a1 : a1;
+                }
+                const bool rowok = real && y0 + r <= ny;
+                if (KIND != 2 && partials) {
+                    if (rowok && okx0) sumsq += r0 * r0;
+                    if (rowok && okx1) sumsq += r1 * r1;
+                }
+                if (rowok && (KIND != 1 || out)) {
+                    double* q = out + x + roff[r + 1] + zo;
+                    if (okx1) st2s<NT>(q, o0, o1);
+                    else if (okx0) *q = o0;
+                }
             }
-            H0 = ld2(v + xl + roff[0] + z1);
-            H1 = ld2(v + xl + roff[RY + 1] + z1);
-        }
-        // ---- plane z ----
-#pragma unroll
-        for (int r = 0; r < RY; r++) {
-            const double2 c = C[r + 1], ym = C[r], yp = C[r + 2], zm = P[r], zp = N[r];
-            const double xm0 = lane_from_left<DPP>(c.y, CL[r]);
-            const double xp1 = lane_from_right<DPP>(c.x, CR[r]);
-            const double wx = (MODE == GS_NEWTON) ? Wc[r].x : 0.0, wy = (MODE == GS_NEWTON) ? Wc[r].y : 0.0;
-            const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
-            const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
-            const double r0 = F[r].x - a0, r1 = F[r].y - a1; // residual of the input iterate
-            double o0, o1;
-            if (KIND == 0) {
-                o0 = jacobi_update<MODE>(k, c.x, r0, wx);
-                o1 = jacobi_update<MODE>(k, c.y, r1, wy);
-            } else if (KIND == 1) {
-                o0 = r0;
-                o1 = r1;
-            } else {
-                o0 = ADD ? F[r].x + a0 : a0;
-                o1 = ADD ? F[r].y + a1 : a1;
-            }
-            const bool rowok = y0 + r <= ny;
-            if (KIND != 2 && partials) {
-                if (rowok && okx0) sumsq += r0 * r0;
-                if (rowok && okx1) sumsq += r1 * r1;
-            }
-            if (rowok && (KIND != 1 || out)) {
-                double* q = out + x + roff[r + 1] + zo;
-                if (okx1) st2s<NT>(q, o0, o1);
-                else if (okx0) *q = o0;
-            }
-        }
-        // ---- rotate the plane window ----
-        if (more) {
-#pragma unroll
-            for (int r = 0; r < RY; r++) P[r] = C[r + 1];
-            C[0] = H0;
-            C[RY + 1] = H1;
 #pragma unroll
             for (int r = 0; r < RY; r++) {
-                C[r + 1] = N[r];
-                N[r] = NN[r];
-                if (KIND != 2 || ADD) F[r] = FN[r];
-                if (MODE == GS_NEWTON) Wc[r] = WN[r];
-                CL[r] = ELn[r];
-                CR[r] = ERn[r];
+                P[r] = C[r];
+                C[r] = NL[cs][r];
             }
         }
     }
@@ -612,9 +613,12 @@ bool bad_level(const gs_level* L)
 template <int MODE, int RY, int WXMAX, bool NT>
 __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __restrict__ v,
                                                       const double* __restrict__ f, const double* __restrict__ w,
-                                                      double* __restrict__ out, int nx, int ny, int nz, int64_t ldy,
-                                                      int64_t ldz, int ZC, int zlo, int zhi)
+                                                      double* __restrict__ out, double* __restrict__ partials, int nx,
+                                                      int ny, int nz, int64_t ldy, int64_t ldz, int ZC, int zlo,
+                                                      int zhi)
 {
+    __shared__ double red[WXMAX];
+    double sumsq = 0.0; // r^2 of sweep 1's residual over the block's own points (partials != NULL)
     constexpr int NV = RY + 2;  // sweep-1 rows (j = 1..RY+2 <-> y0-1..y0+RY)
     constexpr int NE = NV + RY; // LDS edge values per wave side: v rows + sweep-1 rows
     __shared__ double edge[2][WXMAX][2][NE];
@@ -626,8 +630,13 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
     const int xl = min(x, nx + 1);
     const bool bx0 = x > nx, bx1 = x + 1 > nx;            // boundary / beyond columns
     const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
-    const int y0 = 1 + blockIdx.x * RY;
-    const int zb = 1 + blockIdx.y * ZC;
+    // XCD-aware order (cdna_hip_programming.md T1): hardware block b runs on XCD b % 8, so logical
+    // tiles are dealt out in contiguous runs per XCD, y-tile fastest: the blocks an XCD runs at one
+    // time are y-neighbours marching the same planes, and the halo rows one of them re-reads were
+    // just fetched into that XCD's L2 by its neighbour.
+    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+    const int y0 = 1 + (int)(tile % gridDim.x) * RY;
+    const int zb = 1 + (int)(tile / gridDim.x) * ZC;
     const int ze = min(zb + ZC - 1, nz);
 
     int64_t roff[RY + 4]; // rows y0-2 .. y0+RY+1
@@ -641,121 +650,128 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
     auto planeok = [&](int z) { return (z >= 1 && z <= nz) || (z == 0 && zlo) || (z == nz + 1 && zhi); };
     auto at = [&](const double* base, int j, int z) { return base + xl + roff[j] + (int64_t)z * ldz; };
 
-    double2 Vp[NV], Vc[RY + 4], Vn[NV], Fc[NV], Wc[NV];
+    // Register window (rows j = 1..NV of the v planes; rows 0 and RY+3 only as halo pairs): Vp, Vc =
+    // v at planes z-1, z; V1p, V1c = sweep-1 values at planes z-2, z-1; Fprev, Wprev = f, w at z-1.
+    // What step z loads (v rows of plane z+2, f / w rows and the halo rows of plane z+1) goes into
+    // slot ph of a two-slot ring and is consumed from there one step later before being moved on,
+    // so every wait lands a full step of arithmetic after its load (loop unrolled by two).
+    double2 Vp[NV], Vc[NV], VL[2][NV], FL[2][NV], WL[2][NV], HL[2][2];
     double2 V1p[RY], V1c[NV], Fprev[RY], Wprev[RY];
 #pragma unroll
     for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
 #pragma unroll
     for (int j = 0; j < RY; j++) V1p[j] = make_double2(0.0, 0.0);
-    {
-        const int z = zb - 1;
+    // slot s <- plane z's f, w, halo rows and plane zv's v rows
+    auto load_slot = [&](const int s, const int z, const int zv) {
 #pragma unroll
         for (int j = 1; j <= NV; j++) {
-            Vp[j - 1] = ld2(at(v, j, z - 1));
-            Vn[j - 1] = ld2(at(v, j, z + 1));
-            Fc[j - 1] = ld2s<NT>(at(f, j, z));
-            if (MODE == GS_NEWTON) Wc[j - 1] = ld2(at(w, j, z));
+            VL[s][j - 1] = ld2(at(v, j, zv));
+            FL[s][j - 1] = ld2s<NT>(at(f, j, z));
+            if (MODE == GS_NEWTON) WL[s][j - 1] = ld2(at(w, j, z));
         }
+        HL[s][0] = ld2(at(v, 0, z));
+        HL[s][1] = ld2(at(v, RY + 3, z));
+    };
 #pragma unroll
-        for (int j = 0; j < RY + 4; j++) Vc[j] = ld2(at(v, j, z));
+    for (int j = 1; j <= NV; j++) {
+        Vp[j - 1] = ld2(at(v, j, zb - 2));
+        Vc[j - 1] = ld2(at(v, j, zb - 1));
     }
-    int parity = 0;
-    for (int z = zb - 1; z <= ze + 1; z++) {
-        // ---- issue every load of plane z+1 (v rows of z+2, the two extra halo rows, f, w) ----
-        double2 Vnn[NV], Fn[NV], Wn[NV], H0, H1;
-        const bool more = z <= ze;
-        if (more) {
+    load_slot(1, zb - 1, zb);
+    // Both halves always run (an odd step count ends with one step whose results are discarded) and
+    // every load is unconditional (plane indices clamped into the padded range), so the slots keep
+    // fixed registers around the loop.
+    for (int z0 = zb - 1; z0 <= ze + 1; z0 += 2) {
+#pragma unroll
+        for (int ph = 0; ph < 2; ph++) {
+            const int z = z0 + ph;
+            const int cs = ph ^ 1; // slot holding plane z (and v of plane z+1)
+            load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
+            // ---- exchange the columns just outside each wave: v(z) rows 1..NV, sweep-1(z-1) rows 2..RY+1 ----
+            if (lane == 0) {
+#pragma unroll
+                for (int j = 1; j <= NV; j++) edge[ph][wx][0][j - 1] = Vc[j - 1].x;
+#pragma unroll
+                for (int j = 2; j <= RY + 1; j++) edge[ph][wx][0][NV + j - 2] = V1c[j - 1].x;
+            }
+            if (lane == WAVE - 1) {
+#pragma unroll
+                for (int j = 1; j <= NV; j++) edge[ph][wx][1][j - 1] = Vc[j - 1].y;
+#pragma unroll
+                for (int j = 2; j <= RY + 1; j++) edge[ph][wx][1][NV + j - 2] = V1c[j - 1].y;
+            }
+            // LDS-only barrier: the outstanding prefetch must stay in flight across it
+            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            double CL[NE], CR[NE];
+#pragma unroll
+            for (int i = 0; i < NE; i++) {
+                CL[i] = wx > 0 ? edge[ph][wx - 1][1][i] : 0.0;
+                CR[i] = wx + 1 < WX ? edge[ph][wx + 1][0][i] : 0.0;
+            }
+
+            // ---- sweep 1 at plane z ----
+            double2 V1n[NV];
+            const bool pz = planeok(z);
 #pragma unroll
             for (int j = 1; j <= NV; j++) {
-                Vnn[j - 1] = ld2(at(v, j, z + 2));
-                Fn[j - 1] = ld2s<NT>(at(f, j, z + 1));
-                if (MODE == GS_NEWTON) Wn[j - 1] = ld2(at(w, j, z + 1));
-            }
-            H0 = ld2(at(v, 0, z + 1));
-            H1 = ld2(at(v, RY + 3, z + 1));
-        }
-        // ---- exchange the columns just outside each wave: v(z) rows 1..NV, sweep-1(z-1) rows 2..RY+1 ----
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 1; j <= NV; j++) edge[parity][wx][0][j - 1] = Vc[j].x;
-#pragma unroll
-            for (int j = 2; j <= RY + 1; j++) edge[parity][wx][0][NV + j - 2] = V1c[j - 1].x;
-        }
-        if (lane == WAVE - 1) {
-#pragma unroll
-            for (int j = 1; j <= NV; j++) edge[parity][wx][1][j - 1] = Vc[j].y;
-#pragma unroll
-            for (int j = 2; j <= RY + 1; j++) edge[parity][wx][1][NV + j - 2] = V1c[j - 1].y;
-        }
-        __syncthreads();
-        double CL[NE], CR[NE];
-#pragma unroll
-        for (int i = 0; i < NE; i++) {
-            CL[i] = wx > 0 ? edge[parity][wx - 1][1][i] : 0.0;
-            CR[i] = wx + 1 < WX ? edge[parity][wx + 1][0][i] : 0.0;
-        }
-        parity ^= 1;
-
-        // ---- sweep 1 at plane z ----
-        double2 V1n[NV];
-        const bool pz = planeok(z);
-#pragma unroll
-        for (int j = 1; j <= NV; j++) {
-            const double2 c = Vc[j], ym = Vc[j - 1], yp = Vc[j + 1], zm = Vp[j - 1], zp = Vn[j - 1];
-            const double xm0 = lane_from_left<true>(c.y, CL[j - 1]);
-            const double xp1 = lane_from_right<true>(c.x, CR[j - 1]);
-            const double wx0 = (MODE == GS_NEWTON) ? Wc[j - 1].x : 0.0, wx1 = (MODE == GS_NEWTON) ? Wc[j - 1].y : 0.0;
-            const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
-            const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
-            const double n0 = jacobi_update<MODE>(k, c.x, Fc[j - 1].x - a0, wx0);
-            const double n1 = jacobi_update<MODE>(k, c.y, Fc[j - 1].y - a1, wx1);
-            const bool keep = !pz || !rowc[j];
-            V1n[j - 1] = make_double2((keep || bx0) ? c.x : n0, (keep || bx1) ? c.y : n1);
-        }
-        // ---- sweep 2 at plane z-1 ----
-        if (z - 1 >= zb) {
-            const int64_t zo = (int64_t)(z - 1) * ldz;
-#pragma unroll
-            for (int j = 2; j <= RY + 1; j++) {
-                const double2 c = V1c[j - 1], ym = V1c[j - 2], yp = V1c[j], zm = V1p[j - 2], zp = V1n[j - 1];
-                const double xm0 = lane_from_left<true>(c.y, CL[NV + j - 2]);
-                const double xp1 = lane_from_right<true>(c.x, CR[NV + j - 2]);
-                const double wx0 = (MODE == GS_NEWTON) ? Wprev[j - 2].x : 0.0;
-                const double wx1 = (MODE == GS_NEWTON) ? Wprev[j - 2].y : 0.0;
+                const double2 c = Vc[j - 1], zm = Vp[j - 1], zp = VL[cs][j - 1];
+                const double2 ym = j == 1 ? HL[cs][0] : Vc[j - 2], yp = j == NV ? HL[cs][1] : Vc[j];
+                const double xm0 = lane_from_left<true>(c.y, CL[j - 1]);
+                const double xp1 = lane_from_right<true>(c.x, CR[j - 1]);
+                const double wx0 = (MODE == GS_NEWTON) ? WL[cs][j - 1].x : 0.0;
+                const double wx1 = (MODE == GS_NEWTON) ? WL[cs][j - 1].y : 0.0;
                 const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
                 const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
-                const double o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 2].x - a0, wx0);
-                const double o1 = jacobi_update<MODE>(k, c.y, Fprev[j - 2].y - a1, wx1);
-                if (y0 - 2 + j <= ny) {
-                    double* q = out + x + roff[j] + zo;
-                    if (okx1) st2s<NT>(q, o0, o1);
-                    else if (okx0) *q = o0;
+                const double r0 = FL[cs][j - 1].x - a0, r1 = FL[cs][j - 1].y - a1;
+                const double n0 = jacobi_update<MODE>(k, c.x, r0, wx0);
+                const double n1 = jacobi_update<MODE>(k, c.y, r1, wx1);
+                if (partials && j >= 2 && j <= RY + 1 && z >= zb && z <= ze && rowc[j]) {
+                    if (okx0) sumsq += r0 * r0;
+                    if (okx1) sumsq += r1 * r1;
+                }
+                const bool keep = !pz || !rowc[j];
+                V1n[j - 1] = make_double2((keep || bx0) ? c.x : n0, (keep || bx1) ? c.y : n1);
+            }
+            // ---- sweep 2 at plane z-1 ----
+            if (z - 1 >= zb && z - 1 <= ze) {
+                const int64_t zo = (int64_t)(z - 1) * ldz;
+#pragma unroll
+                for (int j = 2; j <= RY + 1; j++) {
+                    const double2 c = V1c[j - 1], ym = V1c[j - 2], yp = V1c[j], zm = V1p[j - 2], zp = V1n[j - 1];
+                    const double xm0 = lane_from_left<true>(c.y, CL[NV + j - 2]);
+                    const double xp1 = lane_from_right<true>(c.x, CR[NV + j - 2]);
+                    const double wx0 = (MODE == GS_NEWTON) ? Wprev[j - 2].x : 0.0;
+                    const double wx1 = (MODE == GS_NEWTON) ? Wprev[j - 2].y : 0.0;
+                    const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
+                    const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
+                    const double o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 2].x - a0, wx0);
+                    const double o1 = jacobi_update<MODE>(k, c.y, Fprev[j - 2].y - a1, wx1);
+                    if (y0 - 2 + j <= ny) {
+                        double* q = out + x + roff[j] + zo;
+                        if (okx1) st2s<NT>(q, o0, o1);
+                        else if (okx0) *q = o0;
+                    }
                 }
             }
-        }
-        // ---- rotate ----
-        if (more) {
+            // ---- rotate (only registers whose loads were consumed above) ----
 #pragma unroll
             for (int j = 0; j < RY; j++) {
                 V1p[j] = V1c[j + 1];
-                Fprev[j] = Fc[j + 1];
-                if (MODE == GS_NEWTON) Wprev[j] = Wc[j + 1];
+                Fprev[j] = FL[cs][j + 1];
+                if (MODE == GS_NEWTON) Wprev[j] = WL[cs][j + 1];
             }
 #pragma unroll
             for (int j = 0; j < NV; j++) {
                 V1c[j] = V1n[j];
-                Vp[j] = Vc[j + 1];
-            }
-            Vc[0] = H0;
-            Vc[RY + 3] = H1;
-#pragma unroll
-            for (int j = 0; j < NV; j++) {
-                Vc[j + 1] = Vn[j];
-                Vn[j] = Vnn[j];
-                Fc[j] = Fn[j];
-                if (MODE == GS_NEWTON) Wc[j] = Wn[j];
+                Vp[j] = Vc[j];
+                Vc[j] = VL[cs][j];
             }
         }
+    }
+    if (partials) {
+        const double t = block_sum<WXMAX>(sumsq, red, WX);
+        if (threadIdx.x == 0 && threadIdx.y == 0) partials[tile] = t;
     }
 }
 
@@ -968,6 +984,21 @@ int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double om
                      const double* v_in, double* v_out, const double* f, const double* w, int zlo, int zhi,
                      hipStream_t st)
 {
+    return gs_jacobi_sweep2_norm(S, L, mode, omega, gamma, v_in, v_out, f, w, zlo, zhi, nullptr, st);
+}
+
+int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L)
+{
+    int zc;
+    dim3 g, b;
+    if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b)) return 0;
+    return (int64_t)g.x * g.y;
+}
+
+int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                          const double* v_in, double* v_out, const double* f, const double* w, int zlo, int zhi,
+                          double* partials, hipStream_t st)
+{
     int zc;
     dim3 g, b;
     if (!S || bad_level(L) || !valid_stencil(S) || !v_in || !v_out || !f || v_in == v_out ||
@@ -975,7 +1006,7 @@ int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double om
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
-#define GS_TB(M, RY, WX) hipLaunchKernelGGL((k_tb2<M, RY, WX, true>), g, b, 0, st, k, v_in, f, w, v_out, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
+#define GS_TB(M, RY, WX) hipLaunchKernelGGL((k_tb2<M, RY, WX, true>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
     if (b.y <= (unsigned)TB_WX_A) {
         if (mode == GS_LINEAR) GS_TB(GS_LINEAR, TB_RY_A, TB_WX_A);
         else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_A, TB_WX_A);

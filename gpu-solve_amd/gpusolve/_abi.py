@@ -44,6 +44,10 @@ KERNEL_API = {
     "gs_jacobi_sweep2_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),
     "gs_jacobi_sweep2": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double, C.c_double,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "gs_jacobi_sweep2_norm": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double,
+                                        C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                        C.c_int, C.c_void_p, C.c_void_p]),
+    "gs_jacobi_sweep2_num_partials": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),
     "gs_residual": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double, C.c_void_p,
                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_residual_num_partials": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),

@@ -111,3 +111,30 @@ def test_sweep2_rejects_unsupported():
     assert rc == gsv._abi.GS_EINVAL
     big = DevField(512, 512, 64)
     assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(big.level(1 / 513))) == 2
+
+
+@pytest.mark.parametrize("shape", [(5, 4, 33), (129, 13, 40), (512, 4, 5), (300, 9, 7), (1024, 3, 4), (64, 64, 64)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_sweep2_norm_partials(shape, mode):
+    """gs_jacobi_sweep2_norm: same output as the plain pair, and its partials sum to ||f - A v_in||^2."""
+    rng = np.random.default_rng(sum(shape) * 7 + mode)
+    nx, ny, nz = shape
+    h = 1.0 / (ny + 1)
+    v0, f0, w0 = rand_full(rng, *shape), rand_full(rng, *shape, 100.0), rand_full(rng, *shape)
+    v, f, w, out, out2 = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
+                          DevField(nx, ny, nz).from_xyz(w0), DevField(nx, ny, nz), DevField(nx, ny, nz))
+    L = v.level(h)
+    n = k().gs_jacobi_sweep2_num_partials(C.byref(stencil()), C.byref(L))
+    assert n >= 1
+    parts = torch.full((n,), float("nan"), dtype=torch.float64, device="cuda")
+    ok(k().gs_jacobi_sweep2_norm(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, out.ptr, f.ptr, w.ptr, 0, 0,
+                                 parts.data_ptr(), st()))
+    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, out2.ptr, f.ptr, w.ptr, 0, 0, st()))
+    np.testing.assert_array_equal(out.to_xyz(), out2.to_xyz())
+    nr = k().gs_residual_num_partials(C.byref(stencil()), C.byref(L))
+    rparts = torch.zeros((nr,), dtype=torch.float64, device="cuda")
+    ok(k().gs_residual(C.byref(stencil()), C.byref(L), mode, 1.0, v.ptr, f.ptr, w.ptr, None, rparts.data_ptr(), st()))
+    torch.cuda.synchronize()
+    got, want = parts.sum().item(), rparts.sum().item()
+    assert np.isfinite(got)
+    assert abs(got - want) <= 1e-12 * abs(want)
