@@ -157,6 +157,29 @@ def single_sweep_timing(grid, dims, k):
             "achieved_GBps": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)}
 
 
+def triad_ceiling(n):
+    """This GPU's achievable rate for the smoother's byte pattern (2 streamed reads + 1 streamed write,
+    24 B per element) on arrays of the level's size: boxes differ by up to ~25%, so the kernel's
+    fraction of it is reported next to the fraction of the 8 TB/s datasheet peak."""
+    kl = gsv.kernels()
+    A = torch.rand(n, dtype=torch.float64, device="cuda")
+    B = torch.rand(n, dtype=torch.float64, device="cuda")
+    O = torch.empty(n, dtype=torch.float64, device="cuda")
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        kl.gs_debug_stream_triad(O.data_ptr(), A.data_ptr(), B.data_ptr(), n, st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(10):
+        kl.gs_debug_stream_triad(O.data_ptr(), A.data_ptr(), B.data_ptr(), n, st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    del A, B, O
+    return {"kernel": "triad out = a + 0.8 b (24 B per element)", "elements": n, "ms": round(ms, 4),
+            "gbps": round(24.0 * n / (ms * 1e-3) / 1e9, 1)}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -206,9 +229,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
 
-    single = None
+    single = ceiling = None
     if world == 1:
         single = single_sweep_timing(grid, dims, a.steps)
+        ceiling = triad_ceiling(int(dims[0]) * dims[1] * dims[2])
 
     lups_per_rank = float(dims[0]) * dims[1] * dims[2] / world
     total_lups = lups_per_rank * a.steps * world
@@ -260,11 +284,13 @@ def main():
                        "parallelism": f"zslab{world}-rccl" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_GBPS, 4),
+                         "frac_of_measured_ceiling": round(achieved / ceiling["gbps"], 4) if ceiling else None,
                          "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
                          "kernel": ("k_tb2: two fused sweeps per launch (24 B per point per launch)" if fused
                                     else "k_rb: one sweep per launch (24 B per point per launch)"),
                          "algorithmic_bytes_per_launch": BYTES_PER_LUP * lups_per_rank},
             "single_sweep_kernel": single,
+            "measured_ceiling": ceiling,
             "vcycle": vc,
             "cpu_baseline": cpu,
             "kernel_build": gsv.build_info(),

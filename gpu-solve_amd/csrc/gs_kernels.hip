@@ -29,6 +29,7 @@ struct Coef {
     double gamma;
     double alpha;  // h*h / s0          (CpuSolver.cpp:145)
     double preFac; // s0 / (h*h)        (CpuSolver.cpp:144)
+    int fastdiv;   // 2^-120 <= hh <= 1: div_hh may take its 3-operation path
     int64_t off[7]; // generic kernel: linear element offsets of the 7 entries
 };
 
@@ -62,11 +63,39 @@ Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamm
     k.gamma = gamma;
     k.alpha = k.hh / S->s[0];
     k.preFac = S->s[0] / k.hh;
+    k.fastdiv = k.hh >= 0x1p-120 && k.hh <= 1.0;
     return k;
 }
 
 // ---------------------------------------------------------------------------------------------
 // Point formulas (reference evaluation order; built with -ffp-contract=off).
+
+// s / hh, bit-identical to the compiler's IEEE division, in 3 FP64 operations instead of ~11.
+// The gfx950 division sequence is: D = div_scale(hh), y = rcp(D) refined by two Newton steps,
+// N = div_scale(s), q = N*y, r = fma(-D, q, N), q' = div_fmas(r, y, q), div_fixup(q', hh, s). When
+// neither operand is scaled (s and hh normal, s != 0, exponent(s) - exponent(hh) < 768, the quotient
+// normal and exponent(s) > 53) div_scale returns its operand, div_fmas is a plain fma and div_fixup
+// returns q' — and y depends on hh alone, so it is loop-invariant. The fast path is taken for
+// 2^-899 <= |s| < 2^601 with the host guaranteeing 2^-120 <= hh <= 1 (Coef::fastdiv); anything
+// else (zero, denormals, inf/nan, extreme magnitudes) takes the ordinary division.
+__device__ __forceinline__ double hh_recip(double hh)
+{
+    const double y0 = __builtin_amdgcn_rcp(hh);
+    const double y1 = __builtin_fma(y0, __builtin_fma(-hh, y0, 1.0), y0);
+    return __builtin_fma(y1, __builtin_fma(-hh, y1, 1.0), y1);
+}
+
+__device__ __forceinline__ double div_hh(const Coef& k, double s)
+{
+    const unsigned e = ((unsigned)__double2hiint(s) >> 20) & 0x7ffu; // biased exponent
+    if (k.fastdiv && e - 124u < 1500u) {                              // 124 <= e <= 1623
+        const double y = hh_recip(k.hh);
+        const double q = s * y;
+        const double r = __builtin_fma(-k.hh, q, s);
+        return __builtin_fma(r, y, q);
+    }
+    return s / k.hh;
+}
 
 // stencil sum in config order, then /h^2 and the non-linear term  — CpuSolver.cpp:56-76
 template <int MODE>
@@ -81,7 +110,7 @@ __device__ __forceinline__ double op_value(const Coef& k, double c, double xp, d
     s += k.s[4] * ym;
     s += k.s[5] * zp;
     s += k.s[6] * zm;
-    s /= k.hh;
+    s = div_hh(k, s);
     if (MODE == GS_NEWTON) {
         const double ew = exp(w);
         s += k.gamma * (1 + w) * c * ew;
@@ -357,7 +386,7 @@ __global__ __launch_bounds__(256) void k_generic(Coef k, const double* __restric
         double s = 0.0;
 #pragma unroll
         for (int i = 0; i < 7; i++) s += k.s[i] * v[p + k.off[i]];
-        s /= k.hh;
+        s = div_hh(k, s);
         const double c = v[p];
         const double wv = (MODE == GS_NEWTON) ? w[p] : 0.0;
         if (MODE == GS_NEWTON) {
@@ -621,10 +650,16 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
     double sumsq = 0.0; // r^2 of sweep 1's residual over the block's own points (partials != NULL)
     constexpr int NV = RY + 2;  // sweep-1 rows (j = 1..RY+2 <-> y0-1..y0+RY)
     constexpr int NE = NV + RY; // LDS edge values per wave side: v rows + sweep-1 rows
-    __shared__ double edge[2][WXMAX][2][NE];
+    // edge[parity][1 + wave][side][value]; slots 0 and WX+1 are virtual waves holding the x-boundary
+    // columns, which this kernel takes to be zero (the reference's homogeneous Dirichlet boundary:
+    // v's boundary cells are never written)
+    __shared__ double edge[2][WXMAX + 2][2][NE];
     const int lane = threadIdx.x;
     const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int WX = blockDim.y;
+    for (int i = threadIdx.x + threadIdx.y * WAVE; i < 2 * (WXMAX + 2) * 2 * NE; i += WAVE * WX)
+        (&edge[0][0][0][0])[i] = 0.0;
+    __syncthreads();
     const int x0 = 1 + wx * (2 * WAVE);
     const int x = x0 + 2 * lane;
     const int xl = min(x, nx + 1);
@@ -690,15 +725,15 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
             // ---- exchange the columns just outside each wave: v(z) rows 1..NV, sweep-1(z-1) rows 2..RY+1 ----
             if (lane == 0) {
 #pragma unroll
-                for (int j = 1; j <= NV; j++) edge[ph][wx][0][j - 1] = Vc[j - 1].x;
+                for (int j = 1; j <= NV; j++) edge[ph][wx + 1][0][j - 1] = Vc[j - 1].x;
 #pragma unroll
-                for (int j = 2; j <= RY + 1; j++) edge[ph][wx][0][NV + j - 2] = V1c[j - 1].x;
+                for (int j = 2; j <= RY + 1; j++) edge[ph][wx + 1][0][NV + j - 2] = V1c[j - 1].x;
             }
             if (lane == WAVE - 1) {
 #pragma unroll
-                for (int j = 1; j <= NV; j++) edge[ph][wx][1][j - 1] = Vc[j - 1].y;
+                for (int j = 1; j <= NV; j++) edge[ph][wx + 1][1][j - 1] = Vc[j - 1].y;
 #pragma unroll
-                for (int j = 2; j <= RY + 1; j++) edge[ph][wx][1][NV + j - 2] = V1c[j - 1].y;
+                for (int j = 2; j <= RY + 1; j++) edge[ph][wx + 1][1][NV + j - 2] = V1c[j - 1].y;
             }
             // LDS-only barrier: the outstanding prefetch must stay in flight across it
             __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
@@ -706,8 +741,8 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
             double CL[NE], CR[NE];
 #pragma unroll
             for (int i = 0; i < NE; i++) {
-                CL[i] = wx > 0 ? edge[ph][wx - 1][1][i] : 0.0;
-                CR[i] = wx + 1 < WX ? edge[ph][wx + 1][0][i] : 0.0;
+                CL[i] = edge[ph][wx][1][i];     // wave wx-1 (slot 0: the zero x = 0 boundary)
+                CR[i] = edge[ph][wx + 2][0][i]; // wave wx+1 (slot WX+1: the zero x = nx+1 boundary)
             }
 
             // ---- sweep 1 at plane z ----
@@ -775,9 +810,11 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
     }
 }
 
-// Two shapes: rows of <= 512 points run 4 output rows per wave in blocks of <= 4 waves (up to 512
-// VGPRs per lane, no spills); rows of <= 1024 points run 2 output rows per wave in 8-wave blocks.
-constexpr int TB_RY_A = 4, TB_WX_A = 4, TB_RY_B = 2, TB_WX_B = 8;
+// Two shapes, both 2 output rows per wave (measured on MI355X with tools/kbench.py --pairs: at 2
+// rows a wave needs ~216 VGPRs, so two waves share a SIMD and hide each other's latency, which
+// beats the lower halo overhead of 3-6 rows at one wave per SIMD by 20-25%): rows of <= 512
+// points in blocks of <= 4 waves, rows of <= 1024 points in blocks of <= 8 waves.
+constexpr int TB_RY_A = 2, TB_WX_A = 4, TB_RY_B = 2, TB_WX_B = 8;
 
 // Geometry rule of the fused pair: the whole x-row in one block and enough work for >= 512 blocks of
 // 4-plane chunks; the z-chunk is then chosen for >= 1024 blocks (4..32 planes).
@@ -916,6 +953,16 @@ __global__ __launch_bounds__(256) void k_bw(double* __restrict__ out, const doub
         }
     }
     if (KIND == 0 && acc == -1.2345e300) *sink = acc; // keeps the loads alive
+}
+
+// div_hh against the plain division (tests: bitwise equality over all magnitudes)
+__global__ __launch_bounds__(256) void k_div_check(const double* __restrict__ a, int64_t n, Coef k,
+                                                   double* __restrict__ fast, double* __restrict__ ref)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fast[i] = div_hh(k, a[i]);
+    ref[i] = a[i] / k.hh;
 }
 
 __global__ __launch_bounds__(256) void k_triad(double* __restrict__ out, const double* __restrict__ a,
@@ -1155,6 +1202,47 @@ int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, 
     return launch_status();
 }
 
+// Fused-pair shapes for tools/kbench.py --pairs (LINEAR): output rows per wave x max waves per
+// block (the launch bound, hence the VGPR budget: 4 waves -> 512, 8 waves -> 256 per lane).
+struct PairVariant {
+    const char* name;
+    int ry, wxmax;
+    void (*kern)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
+                 int64_t, int, int, int);
+};
+#define GS_PV(RY, WX) {"tb2 ry" #RY " wx" #WX, RY, WX, k_tb2<GS_LINEAR, RY, WX, true>}
+const PairVariant kPairVariants[] = {GS_PV(4, 4), GS_PV(2, 8), GS_PV(3, 8), GS_PV(2, 4), GS_PV(3, 4), GS_PV(6, 4),
+                                     GS_PV(4, 8)};
+#undef GS_PV
+constexpr int kNumPairVariants = (int)(sizeof(kPairVariants) / sizeof(kPairVariants[0]));
+
+int gs_debug_num_pair_variants(void) { return kNumPairVariants; }
+const char* gs_debug_pair_variant_name(int variant)
+{
+    return (variant >= 0 && variant < kNumPairVariants) ? kPairVariants[variant].name : "";
+}
+
+int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
+                          double* v_out, const double* f, int zc, hipStream_t st)
+{
+    if (variant < 0 || variant >= kNumPairVariants || !S || bad_level(L) || !canonical_order(S) || !v_in ||
+        !v_out || !f || v_in == v_out || zc < 0)
+        return GS_EINVAL;
+    const PairVariant& V = kPairVariants[variant];
+    const int64_t wx = (L->nx + 2 * WAVE - 1) / (2 * WAVE);
+    if (L->nx < 1 || L->ny < 1 || L->nz < 1 || wx > V.wxmax) return GS_EINVAL;
+    const int64_t tiles = (L->ny + V.ry - 1) / V.ry;
+    if (zc == 0) {
+        int64_t c = tiles * L->nz / 1024;
+        zc = (int)(c < 4 ? 4 : (c > 32 ? 32 : c));
+    }
+    const Coef k = make_coef(S, L, omega, 0.0);
+    hipLaunchKernelGGL(V.kern, dim3((unsigned)tiles, (unsigned)((L->nz + zc - 1) / zc)), dim3(WAVE, (unsigned)wx), 0,
+                       st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc,
+                       0, 0);
+    return launch_status();
+}
+
 int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
                 double* sink, hipStream_t st)
 {
@@ -1167,6 +1255,17 @@ int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const dou
         {{k_bw<3, 1, false>, k_bw<3, 1, true>}, {k_bw<3, 4, false>, k_bw<3, 4, true>}},
     };
     hipLaunchKernelGGL(tab[kind][unroll > 1][nt != 0], dim3(blocks), dim3(256), 0, st, out, a, b, n / 2, sink);
+    return launch_status();
+}
+
+int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, double* ref, hipStream_t st)
+{
+    if (!a || !fast || !ref || n < 0) return GS_EINVAL;
+    if (n == 0) return 0;
+    Coef k{};
+    k.hh = hh;
+    k.fastdiv = hh >= 0x1p-120 && hh <= 1.0;
+    hipLaunchKernelGGL(k_div_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, n, k, fast, ref);
     return launch_status();
 }
 

@@ -87,7 +87,8 @@ int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, doubl
  * canonical order, nx > 1024), 1 possible, 2 possible and large enough to fill the GPU (the driver
  * uses it only then). zlo / zhi: the plane below local plane 1
  * (resp. above plane nz) is an internal Z-slab boundary whose two ghost planes (0 and -1, resp.
- * nz+1 and nz+2) of v_in are current; 0 = a level boundary. */
+ * nz+1 and nz+2) of v_in are current; 0 = a level boundary. The x-boundary columns (x = 0 and
+ * nx+1) of v_in must be zero, as the reference's are (homogeneous Dirichlet, never written). */
 int gs_jacobi_sweep2_supported(const gs_stencil* S, const gs_level* L);
 int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                      const double* v_in, double* v_out, const double* f, const double* w, int zlo, int zhi,
@@ -147,6 +148,13 @@ int gs_debug_num_variants(void);
 const char* gs_debug_variant_name(int variant);
 int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
                            double* v_out, const double* f, hipStream_t stream);
+/* fast[i] = the kernels' a[i] / hh (3-operation path where it applies), ref[i] = plain division. */
+int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, double* ref, hipStream_t stream);
+/* Fused-pair shape variants (LINEAR, level boundaries on both z sides; zc = 0: default chunk). */
+int gs_debug_num_pair_variants(void);
+const char* gs_debug_pair_variant_name(int variant);
+int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
+                          double* v_out, const double* f, int zc, hipStream_t stream);
 int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t n, hipStream_t stream);
 /* Streaming ceilings: kind 0 read a, 1 write out, 2 copy, 3 triad; unroll 1 or 4 dwordx4 per thread,
  * nt = non-temporal, `blocks` workgroups of 256 threads (grid-stride). */

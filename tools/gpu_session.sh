@@ -15,7 +15,7 @@ timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>
 tail -2 "$OUT/pytest_gpu.log"
 
 step kbench
-timeout -k 10 400 python tools/kbench.py --bw --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 || { tail -20 "$OUT/kbench.log"; exit 1; }
+timeout -k 10 500 python tools/kbench.py --bw --pairs --zc 0 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 || { tail -20 "$OUT/kbench.log"; exit 1; }
 
 step bench
 timeout -k 10 600 python bench.py --steps "$STEPS" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }

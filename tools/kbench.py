@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--variants", type=str, default="")
     ap.add_argument("--out", type=str, default="")
     ap.add_argument("--bw", action="store_true", help="also sweep the streaming-ceiling kernels")
+    ap.add_argument("--pairs", action="store_true", help="also time the fused-pair shape variants")
+    ap.add_argument("--zc", type=str, default="0", help="fused-pair z-chunks to try (comma list, 0 = auto)")
     a = ap.parse_args()
     k = gsv.kernels()
     nx = a.n
@@ -95,6 +97,50 @@ def main():
         d["gbps"] = round(24 * lups / med / 1e6, 1)
         d["pct_peak"] = round(100 * 24 * lups / med / 1e6 / PEAK, 1)
         del d["ms"]
+
+    if a.pairs:
+        # reference: two production single sweeps of the current v
+        ref1, ref2 = DevField(nx, ny, nz), DevField(nx, ny, nz)
+        assert k.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, v.ptr, ref1.ptr, f.ptr, None, st) == 0
+        assert k.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, ref1.ptr, ref2.ptr, f.ptr, None, st) == 0
+        torch.cuda.synchronize()
+        pv = {}
+        cases = [("production", -1, 0)] + [(k.gs_debug_pair_variant_name(i).decode() + f" zc{zc}", i, int(zc))
+                                            for i in range(k.gs_debug_num_pair_variants())
+                                            for zc in a.zc.split(",")]
+
+        def launch(i, zc, src, dst):
+            if i < 0:
+                return k.gs_jacobi_sweep2(C.byref(S), C.byref(L), 0, 0.8, 1.0, src.ptr, dst.ptr, f.ptr, None, 0, 0, st)
+            return k.gs_debug_pair_variant(i, C.byref(S), C.byref(L), 0.8, src.ptr, dst.ptr, f.ptr, zc, st)
+        for name, i, zc in cases:
+            alt.buf.zero_()
+            rc = launch(i, zc, v, alt)
+            if rc != 0:
+                continue
+            torch.cuda.synchronize()
+            pv[name] = {"bitwise_equal_to_two_sweeps": bool(torch.equal(alt.zyx[:, :, :nx + 2],
+                                                                         ref2.zyx[:, :, :nx + 2])), "ms": []}
+        for r in range(a.rounds):
+            for name, i, zc in cases:
+                if name not in pv:
+                    continue
+                a_, b_ = v, alt
+                launch(i, zc, a_, b_)
+                ev[0].record()
+                for _ in range(a.sweeps):
+                    launch(i, zc, a_, b_)
+                    a_, b_ = b_, a_
+                ev[1].record()
+                torch.cuda.synchronize()
+                pv[name]["ms"].append(ev[0].elapsed_time(ev[1]) / a.sweeps)
+        for name, d in pv.items():
+            med = statistics.median(d["ms"])
+            d["median_ms_per_pair"] = round(med, 4)
+            d["gbps_24B"] = round(24 * lups / med / 1e6, 1)
+            d["glups"] = round(2 * lups / med / 1e6, 1)
+            del d["ms"]
+        result["pairs"] = pv
 
     # achievable ceiling for the same byte pattern (2 streamed reads + 1 streamed write)
     n = (v.span // 2) * 2

@@ -28,7 +28,9 @@ def main():
         names = {}
         for r in csv.DictReader(open(fn)):
             key = (r["Dispatch_Id"], r["Counter_Name"])
-            per[key] += float(r["Counter_Value"])
+            x = float(r["Counter_Value"])
+            # GRBM_* are chip-wide clocks repeated per XCD: take one copy; everything else adds up
+            per[key] = max(per[key], x) if r["Counter_Name"].startswith("GRBM") else per[key] + x
             names[r["Dispatch_Id"]] = short(r["Kernel_Name"])
         for (d, c), v in per.items():
             vals[names[d]][c].append(v)
