@@ -639,7 +639,7 @@ bool bad_level(const gs_level* L)
 // planes are current) its value is the boundary value itself, exactly as a stored sweep would leave
 // it. Per point the arithmetic is the single sweep's, so the result is bit-identical to two
 // gs_jacobi_sweep calls.
-template <int MODE, int RY, int WXMAX, bool NT>
+template <int MODE, int RY, int WXMAX, bool NT, bool NTF = NT>
 __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __restrict__ v,
                                                       const double* __restrict__ f, const double* __restrict__ w,
                                                       double* __restrict__ out, double* __restrict__ partials, int nx,
@@ -701,7 +701,7 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
 #pragma unroll
         for (int j = 1; j <= NV; j++) {
             VL[s][j - 1] = ld2(at(v, j, zv));
-            FL[s][j - 1] = ld2s<NT>(at(f, j, z));
+            FL[s][j - 1] = ld2s<NTF>(at(f, j, z));
             if (MODE == GS_NEWTON) WL[s][j - 1] = ld2(at(w, j, z));
         }
         HL[s][0] = ld2(at(v, 0, z));
@@ -839,7 +839,7 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
 // output streams. The z-chunk is chosen per launch so the grid keeps >= 2048 blocks (at most 32
 // planes, at least 4); a level too small for that many 4-plane chunks runs the one-point-per-thread
 // kernel instead (coarse levels are latency-bound: parallelism beats register blocking there).
-constexpr int RB_RY = 8, RB_W = 2, RB_ZCMAX = 32, RB_ZCMIN = 4;
+constexpr int RB_RY = 2, RB_W = 4, RB_ZCMAX = 32, RB_ZCMIN = 4;
 constexpr bool RB_NT = true;
 
 struct PassPlan {
@@ -908,18 +908,18 @@ struct Variant {
 #define GS_VX(RY, W, ZC, NT, X, NTV, TAG) \
     {"rb ry" #RY " w" #W " zc" #ZC " " TAG, RY, W, ZC, X, k_rb<GS_LINEAR, 0, false, RY, W, true, NT, X, NTV>}
 const Variant kVariants[] = {
-    GS_VX(8, 2, 32, true, false, false, "dpp nt (production shape)"),
-    GS_VX(8, 2, 32, false, false, false, "dpp"),
+    GS_VX(2, 4, 32, true, false, false, "dpp nt (production shape)"),
+    GS_VX(2, 4, 32, false, false, false, "dpp"),
+    GS_VX(2, 4, 32, true, true, false, "dpp nt xcd"),
+    GS_VX(2, 4, 32, true, false, true, "dpp nt ntv"),
+    GS_VX(2, 4, 16, true, false, false, "dpp nt"),
+    GS_VX(2, 4, 64, true, false, false, "dpp nt"),
+    GS_VX(2, 8, 32, true, false, false, "dpp nt"),
+    GS_VX(2, 2, 32, true, false, false, "dpp nt"),
+    GS_VX(1, 8, 32, true, false, false, "dpp nt"),
     GS_VX(4, 4, 32, true, false, false, "dpp nt"),
-    GS_VX(8, 1, 32, true, false, false, "dpp nt"),
-    GS_VX(8, 2, 16, true, false, false, "dpp nt"),
-    GS_VX(8, 2, 8, true, false, false, "dpp nt"),
-    GS_VX(8, 2, 64, true, false, false, "dpp nt"),
-    GS_VX(6, 2, 32, true, false, false, "dpp nt"),
-    GS_VX(1, 4, 32, true, false, false, "dpp nt"),
-    GS_VX(2, 4, 32, true, false, false, "dpp nt"),
-    GS_VX(8, 2, 32, true, false, true, "dpp nt ntv"),
-    GS_VX(8, 2, 32, true, true, false, "dpp nt xcd"),
+    GS_VX(4, 2, 32, true, false, false, "dpp nt"),
+    GS_VX(8, 2, 32, true, false, false, "dpp nt"),
 };
 #undef GS_VX
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
@@ -1211,8 +1211,9 @@ struct PairVariant {
                  int64_t, int, int, int);
 };
 #define GS_PV(RY, WX) {"tb2 ry" #RY " wx" #WX, RY, WX, k_tb2<GS_LINEAR, RY, WX, true>}
-const PairVariant kPairVariants[] = {GS_PV(4, 4), GS_PV(2, 8), GS_PV(3, 8), GS_PV(2, 4), GS_PV(3, 4), GS_PV(6, 4),
-                                     GS_PV(4, 8)};
+#define GS_PVF(RY, WX) {"tb2 ry" #RY " wx" #WX " f-cached", RY, WX, k_tb2<GS_LINEAR, RY, WX, true, false>}
+const PairVariant kPairVariants[] = {GS_PV(2, 4), GS_PVF(2, 4), GS_PV(2, 8), GS_PVF(2, 8), GS_PV(4, 4), GS_PV(3, 8)};
+#undef GS_PVF
 #undef GS_PV
 constexpr int kNumPairVariants = (int)(sizeof(kPairVariants) / sizeof(kPairVariants[0]));
 
