@@ -44,10 +44,10 @@ BYTES_PER_LUP = 24.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=200, help="untimed sweeps first (also brings the GPU clocks up)")
     ap.add_argument("--size", type=int, default=512, help="per-rank cube edge (BASELINE config #3: 512)")
-    ap.add_argument("--vcycles", type=int, default=5, help="timed V-cycles after one warm-up cycle (0: skip)")
+    ap.add_argument("--vcycles", type=int, default=20, help="timed V-cycles after one warm-up cycle (0: skip)")
     ap.add_argument("--cpu-sweeps", type=int, default=6, help="cpu_baseline sample size (0: skip)")
     ap.add_argument("--cpu-vcycles", type=int, default=1, help="cpu_baseline V-cycles (0: skip)")
     return ap.parse_args()

@@ -211,7 +211,7 @@ int64_t sweepPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64
     sub.nz = z2 - z1 + 1;
     sub.z0 += z1 - 1;
     const int64_t off = (z1 - 1) * L.geom.ldz;
-    check(gs_jacobi_sweep_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.v.data() + off,
+    check(gs_jacobi_sweep_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.vZero ? nullptr : L.v.data() + off,
                                L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
                                partials, s),
           "gs_jacobi_sweep");
@@ -232,7 +232,7 @@ int64_t pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_
     const bool dist = L.distributed && g.nranks() > 1;
     const int zlo = z1 > 1 || (dist && g.rank() > 0);
     const int zhi = z2 < L.geom.nz || (dist && g.rank() + 1 < g.nranks());
-    check(gs_jacobi_sweep2_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.v.data() + off,
+    check(gs_jacobi_sweep2_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.vZero ? nullptr : L.v.data() + off,
                                 L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
                                 zlo, zhi, partials, s),
           "gs_jacobi_sweep2");
@@ -316,6 +316,7 @@ double HipSolver::finishNorm(HipGridData& grid, int64_t nparts)
 // the norm only when a caller reads it (level 0).
 double HipSolver::compResidual(HipGridData& grid, std::size_t l, bool storeR, bool norm)
 {
+    materialize(grid, l);
     auto& L = grid.getLevel(l);
     const hipStream_t s = grid.stream();
     check(gs_residual(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(), L.f.data(),
@@ -362,8 +363,18 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
             grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, s);
         }
         L.v.swap(L.vAlt);
+        L.vZero = false;
         sweeps -= pair ? 2 : 1;
     }
+}
+
+// v = 0 made real (the zero-iterate sweeps had no chance to replace it)
+void HipSolver::materialize(HipGridData& grid, std::size_t l)
+{
+    auto& L = grid.getLevel(l);
+    if (!L.vZero) return;
+    L.v.zero(grid.stream());
+    L.vZero = false;
 }
 
 // The first pre-smoothing step of the next cycle, run into vAlt (v untouched) with the norm of the
@@ -426,7 +437,10 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
         compResidual(grid, i, true, false);
         restrictTo(grid, L.r, i, C.f, nullptr, true); // f^2h = R r^h (ghosts: the fused pair reads them)
         if (grid.mode != GridParams::NONLINEAR) {
-            C.v.zero(s);
+            // v^2h = 0 (CpuSolver.cpp:114-116): not stored; the first sweep on the level reads no v
+            static const bool noZeroGuess = std::getenv("GS_NO_ZERO_GUESS") != nullptr;
+            if (noZeroGuess) C.v.zero(s);
+            else C.vZero = true;
         } else {
             // FAS: restV = v^2h = R v^h, then f^2h += A^2h(restV)  (CpuSolver.cpp:104-113)
             restrictTo(grid, L.v, i, C.restV, &C.v, true);
@@ -439,6 +453,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
     for (std::size_t i = nl - 1; i > 0; i--) {
         auto& C = grid.getLevel(i);
         auto& F = grid.getLevel(i - 1);
+        materialize(grid, i); // only if the level had no sweep at all
         // v^h += P (v^2h [- restV^2h])   (CpuSolver.cpp:121-132, interpolate + v += e fused)
         check(gs_prolong_add(C.v.data(), grid.mode == GridParams::NONLINEAR ? C.restV.data() : nullptr, &C.geom,
                              F.v.data(), &F.geom, s),

@@ -70,6 +70,7 @@ public:
         gs_level geom{};     // kernel-side geometry of the stored array (slab or full level)
         bool distributed = false;
         bool fusedPairs = false; // smoothing runs as fused sweep pairs (gs_jacobi_sweep2)
+        bool vZero = false;      // v is identically zero but not stored: the next sweep reads no v
         int64_t lo = 1, hi = 0; // this rank's owned global planes (== 1..nz when not distributed)
         int64_t minPlanes = 0;  // fewest planes any rank owns on this level
         std::vector<int64_t> ranksLo, ranksHi; // every rank's owned planes (gather of replicated levels)
@@ -137,6 +138,7 @@ public:
     static double speculativeSweep(HipGridData& grid, int* sweeps);
     static bool speculationEnabled(const HipGridData& grid);
     static void jacobi(HipGridData& grid, std::size_t level, std::size_t sweeps);
+    static void materialize(HipGridData& grid, std::size_t level); // store a pending v = 0
     static double finishNorm(HipGridData& grid, int64_t nparts);
 
     // solve() records its residual history here when non-null (initial, then one per V-cycle)

@@ -227,6 +227,21 @@ __device__ __forceinline__ void st2s(double* __restrict__ p, double a, double b)
     }
 }
 
+// Loads of the iterate; ZV: the iterate is identically zero (a coarse level's first sweep after
+// the reference's v = 0) and is not read at all. Multiplying the literal zeros keeps the arithmetic,
+// and so every bit of the result, that of loaded zeros (no fast-math folding).
+template <bool ZV, bool NT = false>
+__device__ __forceinline__ double2 ldv2(const double* __restrict__ p)
+{
+    if (ZV) return make_double2(0.0, 0.0);
+    return ld2s<NT>(p);
+}
+template <bool ZV>
+__device__ __forceinline__ double ldv1(const double* __restrict__ p)
+{
+    return ZV ? 0.0 : *p;
+}
+
 // Bijective XCD-aware tile order (cdna_hip_programming.md T1): hardware block b runs on XCD b % 8;
 // give each XCD a contiguous run of tiles so y-neighbour tiles share an L2 while they run.
 __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb)
@@ -235,7 +250,8 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb)
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
-template <int MODE, int KIND, bool ADD, int RY, int W, bool DPP, bool NT = false, bool XCD = false, bool NTV = false>
+template <int MODE, int KIND, bool ADD, int RY, int W, bool DPP, bool NT = false, bool XCD = false, bool NTV = false,
+          bool ZV = false>
 __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict__ v, const double* __restrict__ f,
                                                  const double* __restrict__ w, double* __restrict__ out,
                                                  double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
@@ -280,21 +296,21 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
     auto load_slot = [&](const int s, const int64_t z1, const int64_t z2) {
 #pragma unroll
         for (int r = 0; r < RY; r++) {
-            NL[s][r] = ld2s<NTV>(v + xl + roff[r + 1] + z2);
+            NL[s][r] = ldv2<ZV, NTV>(v + xl + roff[r + 1] + z2);
             if (KIND != 2 || ADD) FL[s][r] = ld2s<NT>(fin + xl + roff[r + 1] + z1);
             if (MODE == GS_NEWTON) WL[s][r] = ld2(w + xl + roff[r + 1] + z1);
-            EL[s][r] = v[xle + roff[r + 1] + z1];
-            ER[s][r] = v[xre + roff[r + 1] + z1];
+            EL[s][r] = ldv1<ZV>(v + xle + roff[r + 1] + z1);
+            ER[s][r] = ldv1<ZV>(v + xre + roff[r + 1] + z1);
         }
-        HL[s][0] = ld2(v + xl + roff[0] + z1);
-        HL[s][1] = ld2(v + xl + roff[RY + 1] + z1);
+        HL[s][0] = ldv2<ZV>(v + xl + roff[0] + z1);
+        HL[s][1] = ldv2<ZV>(v + xl + roff[RY + 1] + z1);
     };
     if (zb <= ze) {
         const int64_t zo = (int64_t)zb * ldz;
 #pragma unroll
         for (int r = 0; r < RY; r++) {
-            P[r] = ld2(v + xl + roff[r + 1] + zo - ldz);
-            C[r] = ld2(v + xl + roff[r + 1] + zo);
+            P[r] = ldv2<ZV>(v + xl + roff[r + 1] + zo - ldz);
+            C[r] = ldv2<ZV>(v + xl + roff[r + 1] + zo);
         }
         load_slot(1, zo, zo + ldz);
     }
@@ -385,9 +401,9 @@ __global__ __launch_bounds__(256) void k_generic(Coef k, const double* __restric
         const int64_t p = x + y * ldy + (int64_t)z * ldz;
         double s = 0.0;
 #pragma unroll
-        for (int i = 0; i < 7; i++) s += k.s[i] * v[p + k.off[i]];
+        for (int i = 0; i < 7; i++) s += k.s[i] * (v ? v[p + k.off[i]] : 0.0);
         s = div_hh(k, s);
-        const double c = v[p];
+        const double c = v ? v[p] : 0.0;
         const double wv = (MODE == GS_NEWTON) ? w[p] : 0.0;
         if (MODE == GS_NEWTON) {
             const double ew = exp(wv);
@@ -639,7 +655,7 @@ bool bad_level(const gs_level* L)
 // planes are current) its value is the boundary value itself, exactly as a stored sweep would leave
 // it. Per point the arithmetic is the single sweep's, so the result is bit-identical to two
 // gs_jacobi_sweep calls.
-template <int MODE, int RY, int WXMAX, bool NT, bool NTF = NT>
+template <int MODE, int RY, int WXMAX, bool NT, bool NTF = NT, bool ZV = false>
 __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __restrict__ v,
                                                       const double* __restrict__ f, const double* __restrict__ w,
                                                       double* __restrict__ out, double* __restrict__ partials, int nx,
@@ -700,17 +716,17 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
     auto load_slot = [&](const int s, const int z, const int zv) {
 #pragma unroll
         for (int j = 1; j <= NV; j++) {
-            VL[s][j - 1] = ld2(at(v, j, zv));
+            VL[s][j - 1] = ldv2<ZV>(at(v, j, zv));
             FL[s][j - 1] = ld2s<NTF>(at(f, j, z));
             if (MODE == GS_NEWTON) WL[s][j - 1] = ld2(at(w, j, z));
         }
-        HL[s][0] = ld2(at(v, 0, z));
-        HL[s][1] = ld2(at(v, RY + 3, z));
+        HL[s][0] = ldv2<ZV>(at(v, 0, z));
+        HL[s][1] = ldv2<ZV>(at(v, RY + 3, z));
     };
 #pragma unroll
     for (int j = 1; j <= NV; j++) {
-        Vp[j - 1] = ld2(at(v, j, zb - 2));
-        Vc[j - 1] = ld2(at(v, j, zb - 1));
+        Vp[j - 1] = ldv2<ZV>(at(v, j, zb - 2));
+        Vc[j - 1] = ldv2<ZV>(at(v, j, zb - 1));
     }
     load_slot(1, zb - 1, zb);
     // Both halves always run (an odd step count ends with one step whose results are discarded) and
@@ -872,7 +888,9 @@ template <int KIND, bool ADD>
 int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma, const double* v,
                 const double* f, const double* w, double* out, double* partials, hipStream_t st)
 {
-    if (!S || bad_level(L) || !valid_stencil(S) || !v) return GS_EINVAL;
+    // v == NULL: the zero iterate (sweeps only, not in NONLINEAR mode, whose coarse iterates are
+    // restrictions, never zero)
+    if (!S || bad_level(L) || !valid_stencil(S) || (!v && (KIND != 0 || mode == GS_NONLINEAR))) return GS_EINVAL;
     if (mode < GS_LINEAR || mode > GS_NEWTON) return GS_EINVAL;
     if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
     const Coef k = make_coef(S, L, omega, gamma);
@@ -880,10 +898,15 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
     const PassPlan plan = pass_plan(S, L);
     if (plan.rb) {
         const dim3 g = plan.grid, b(WAVE, RB_W);
-#define GS_RB(M) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, true, RB_NT>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz, plan.zc)
-        if (mode == GS_LINEAR) GS_RB(GS_LINEAR);
-        else if (mode == GS_NONLINEAR) GS_RB(GS_NONLINEAR);
-        else GS_RB(GS_NEWTON);
+#define GS_RB(M, Z) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, true, RB_NT, false, false, Z>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz, plan.zc)
+        if (!v) {
+            if constexpr (KIND == 0 && !ADD) {
+                if (mode == GS_LINEAR) GS_RB(GS_LINEAR, true);
+                else GS_RB(GS_NEWTON, true);
+            }
+        } else if (mode == GS_LINEAR) GS_RB(GS_LINEAR, false);
+        else if (mode == GS_NONLINEAR) GS_RB(GS_NONLINEAR, false);
+        else GS_RB(GS_NEWTON, false);
 #undef GS_RB
     } else {
         const dim3 g = plan.grid, b(GN_BX, GN_BY);
@@ -1048,20 +1071,27 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
 {
     int zc;
     dim3 g, b;
-    if (!S || bad_level(L) || !valid_stencil(S) || !v_in || !v_out || !f || v_in == v_out ||
+    if (!S || bad_level(L) || !valid_stencil(S) || !v_out || !f || v_in == v_out || (!v_in && mode == GS_NONLINEAR) ||
         (mode == GS_NEWTON && !w) || mode < GS_LINEAR || mode > GS_NEWTON || !tb2_plan(S, L, &zc, &g, &b))
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
-#define GS_TB(M, RY, WX) hipLaunchKernelGGL((k_tb2<M, RY, WX, true>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
+#define GS_TB(M, RY, WX, Z) hipLaunchKernelGGL((k_tb2<M, RY, WX, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
+    const bool zv = !v_in;
     if (b.y <= (unsigned)TB_WX_A) {
-        if (mode == GS_LINEAR) GS_TB(GS_LINEAR, TB_RY_A, TB_WX_A);
-        else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_A, TB_WX_A);
-        else GS_TB(GS_NEWTON, TB_RY_A, TB_WX_A);
+        if (mode == GS_LINEAR) {
+            if (zv) GS_TB(GS_LINEAR, TB_RY_A, TB_WX_A, true);
+            else GS_TB(GS_LINEAR, TB_RY_A, TB_WX_A, false);
+        } else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_A, TB_WX_A, false);
+        else if (zv) GS_TB(GS_NEWTON, TB_RY_A, TB_WX_A, true);
+        else GS_TB(GS_NEWTON, TB_RY_A, TB_WX_A, false);
     } else {
-        if (mode == GS_LINEAR) GS_TB(GS_LINEAR, TB_RY_B, TB_WX_B);
-        else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_B, TB_WX_B);
-        else GS_TB(GS_NEWTON, TB_RY_B, TB_WX_B);
+        if (mode == GS_LINEAR) {
+            if (zv) GS_TB(GS_LINEAR, TB_RY_B, TB_WX_B, true);
+            else GS_TB(GS_LINEAR, TB_RY_B, TB_WX_B, false);
+        } else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_B, TB_WX_B, false);
+        else if (zv) GS_TB(GS_NEWTON, TB_RY_B, TB_WX_B, true);
+        else GS_TB(GS_NEWTON, TB_RY_B, TB_WX_B, false);
     }
 #undef GS_TB
     return launch_status();

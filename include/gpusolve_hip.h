@@ -72,7 +72,9 @@ int gs_field_layout(int64_t nx, int64_t ny, int64_t nz, int64_t* ldy, int64_t* l
 int gs_rhs_init(const gs_level* L, double* f, int mode, double h0, double gamma, hipStream_t stream);
 
 /* One damped-Jacobi sweep, residual and update fused: v_out = v_in + omega * D^-1 (f - A v_in).
- * w = newtonV of this level (mode NEWTON), ignored otherwise. v_in and v_out must differ. */
+ * w = newtonV of this level (mode NEWTON), ignored otherwise. v_in and v_out must differ.
+ * v_in = NULL: the zero iterate, not read (modes LINEAR / NEWTON; the coarse-level first sweep after
+ * the reference's v = 0, CpuSolver.cpp:114-116) — bit-identical to passing a zeroed field. */
 int gs_jacobi_sweep(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                     const double* v_in, double* v_out, const double* f, const double* w, hipStream_t stream);
 
@@ -83,7 +85,7 @@ int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, doubl
                          hipStream_t stream);
 
 /* Two fused sweeps, v_out = S(S(v_in)), reading v_in / f once (temporal blocking; bit-identical to
- * two gs_jacobi_sweep calls). gs_jacobi_sweep2_supported(S, L): 0 impossible (stencil not in
+ * two gs_jacobi_sweep calls; v_in = NULL: the zero iterate, as for gs_jacobi_sweep). gs_jacobi_sweep2_supported(S, L): 0 impossible (stencil not in
  * canonical order, nx > 1024), 1 possible, 2 possible and large enough to fill the GPU (the driver
  * uses it only then). zlo / zhi: the plane below local plane 1
  * (resp. above plane nz) is an internal Z-slab boundary whose two ghost planes (0 and -1, resp.

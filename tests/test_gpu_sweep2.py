@@ -138,3 +138,45 @@ def test_sweep2_norm_partials(shape, mode):
     got, want = parts.sum().item(), rparts.sum().item()
     assert np.isfinite(got)
     assert abs(got - want) <= 1e-12 * abs(want)
+
+
+@pytest.mark.parametrize("shape", [(5, 4, 33), (129, 13, 40), (512, 6, 5), (64, 64, 64)])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_zero_iterate_sweeps(shape, mode):
+    """v_in = NULL (the coarse levels' v = 0 after restriction) is bit-identical to a zeroed v_in,
+    for the single sweep (with its norm partials) and for the fused pair."""
+    rng = np.random.default_rng(sum(shape) + 11 * mode)
+    nx, ny, nz = shape
+    h = 1.0 / (ny + 1)
+    f0, w0 = rand_full(rng, *shape, 100.0), rand_full(rng, *shape)
+    zero, f, w = DevField(nx, ny, nz), DevField(nx, ny, nz).from_xyz(f0), DevField(nx, ny, nz).from_xyz(w0)
+    a, b = DevField(nx, ny, nz, fill=7.0), DevField(nx, ny, nz, fill=7.0)
+    a.from_xyz(np.zeros((nx + 2, ny + 2, nz + 2)))
+    b.from_xyz(np.zeros((nx + 2, ny + 2, nz + 2)))
+    L = zero.level(h)
+    n = k().gs_residual_num_partials(C.byref(stencil()), C.byref(L))
+    pa = torch.zeros((n,), dtype=torch.float64, device="cuda")
+    pb = torch.zeros((n,), dtype=torch.float64, device="cuda")
+    ok(k().gs_jacobi_sweep_norm(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, zero.ptr, a.ptr, f.ptr, w.ptr,
+                                pa.data_ptr(), st()))
+    ok(k().gs_jacobi_sweep_norm(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, None, b.ptr, f.ptr, w.ptr,
+                                pb.data_ptr(), st()))
+    np.testing.assert_array_equal(a.to_xyz(), b.to_xyz())
+    assert torch.equal(pa, pb)
+    if k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(L)) >= 1:
+        a.from_xyz(np.zeros((nx + 2, ny + 2, nz + 2)))
+        b.from_xyz(np.zeros((nx + 2, ny + 2, nz + 2)))
+        ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, zero.ptr, a.ptr, f.ptr, w.ptr, 0, 0,
+                                st()))
+        ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, None, b.ptr, f.ptr, w.ptr, 0, 0,
+                                st()))
+        np.testing.assert_array_equal(a.to_xyz(), b.to_xyz())
+
+
+def test_zero_iterate_rejected_in_fas_mode():
+    nx = ny = nz = 16
+    f, out = DevField(nx, ny, nz), DevField(nx, ny, nz)
+    L = f.level(1.0 / 17)
+    assert k().gs_jacobi_sweep(C.byref(stencil()), C.byref(L), 1, 0.8, 1.0, None, out.ptr, f.ptr, None, st()) != 0
+    assert k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 1, 0.8, 1.0, None, out.ptr, f.ptr, None, 0, 0,
+                                st()) != 0
