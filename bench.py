@@ -249,6 +249,9 @@ def main():
     value = total_lups / elapsed / 1e6
     achieved = BYTES_PER_LUP * lups_per_rank / (kernel_ms * 1e-3) / 1e9
     traffic, pmc = pmc_traffic(n)
+    import ctypes as C
+    pair_kernel = gsv.kernels().gs_jacobi_sweep2_kernel(C.byref(grid.params.stencil.to_abi()),
+                                                        C.byref(grid.getLevel(0).geom), 0).decode()
 
     vc = None
     if a.vcycles > 0:
@@ -296,8 +299,8 @@ def main():
                          "frac": round(achieved / PEAK_GBPS, 4),
                          "frac_of_measured_ceiling": round(achieved / ceiling["gbps"], 4) if ceiling else None,
                          "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
-                         "kernel": ("k_tb2: two fused sweeps per launch (24 B per point per launch)" if fused
-                                    else "k_rb: one sweep per launch (24 B per point per launch)"),
+                         "kernel": (pair_kernel + ": two fused sweeps per launch (24 B per point per launch)"
+                                    if fused else "k_rb: one sweep per launch (24 B per point per launch)"),
                          "algorithmic_bytes_per_launch": BYTES_PER_LUP * lups_per_rank},
             "single_sweep_kernel": single,
             "measured_ceiling": ceiling,

@@ -126,7 +126,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s);
         L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), L.lo - 1, L.h};
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
-        maxParts = std::max(maxParts, gs_jacobi_sweep2_num_partials(&stencilAbi, &L.geom));
+        maxParts = std::max(maxParts, gs_jacobi_sweep2_num_partials(&stencilAbi, &L.geom, (int)mode));
         L.minPlanes = nz;
         if (L.distributed)
             for (int q = 0; q < nranks(); q++) L.minPlanes = std::min(L.minPlanes, L.ranksHi[q] - L.ranksLo[q] + 1);
@@ -236,7 +236,7 @@ int64_t pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_
                                 L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
                                 zlo, zhi, partials, s),
           "gs_jacobi_sweep2");
-    return partials ? gs_jacobi_sweep2_num_partials(&g.stencilAbi, &sub) : 0;
+    return partials ? gs_jacobi_sweep2_num_partials(&g.stencilAbi, &sub, (int)g.mode) : 0;
 }
 
 bool transitionLevel(HipGridData& g, std::size_t l)

@@ -20,6 +20,16 @@ namespace {
 
 constexpr int WAVE = 64;
 
+// compile-time / run-time booleans for code specialised per wave (BoolC) or selected per use (RtBool)
+template <bool B>
+struct BoolC {
+    __device__ static constexpr bool get() { return B; }
+};
+struct RtBool {
+    bool b;
+    __device__ bool get() const { return b; }
+};
+
 // ---------------------------------------------------------------------------------------------
 // Stencil coefficients by value (they land in SGPRs).
 struct Coef {
@@ -95,6 +105,78 @@ __device__ __forceinline__ double div_hh(const Coef& k, double s)
         return __builtin_fma(r, y, q);
     }
     return s / k.hh;
+}
+
+// The same division for N values at once: the operand-range test of every value is combined first
+// and ONE branch picks the 3-operation path for all N (or the IEEE division for all N when any value
+// is outside the range), so a sweep over several rows has one exec branch instead of one per point
+// and the scheduler can interleave the rows' arithmetic.
+__device__ __forceinline__ bool div_hh_fast_ok(double s)
+{
+    const unsigned e = ((unsigned)__double2hiint(s) >> 20) & 0x7ffu;
+    return e - 124u < 1500u;
+}
+template <int N>
+__device__ __forceinline__ void div_hh_n(const Coef& k, double (&s)[N])
+{
+    bool ok = k.fastdiv;
+#pragma unroll
+    for (int i = 0; i < N; i++) ok &= div_hh_fast_ok(s[i]);
+    if (ok) {
+        const double y = hh_recip(k.hh);
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+            const double q = s[i] * y;
+            const double r = __builtin_fma(-k.hh, q, s[i]);
+            s[i] = __builtin_fma(r, y, q);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; i++) s[i] = s[i] / k.hh;
+    }
+}
+
+// one row's two points: batched, except in NEWTON mode whose kernels run at the VGPR limit (the batch
+// keeps both sums live across the branch)
+template <int MODE>
+__device__ __forceinline__ void div_hh_row(const Coef& k, double (&q)[2])
+{
+    if (MODE == GS_NEWTON) {
+        q[0] = div_hh(k, q[0]);
+        q[1] = div_hh(k, q[1]);
+    } else {
+        div_hh_n(k, q);
+    }
+}
+
+// stencil sum in config order (before the division by h^2) — CpuSolver.cpp:56-62
+__device__ __forceinline__ double stencil_sum(const Coef& k, double c, double xp, double xm, double yp, double ym,
+                                              double zp, double zm)
+{
+    double s = 0.0;
+    s += k.s[0] * c;
+    s += k.s[1] * xp;
+    s += k.s[2] * xm;
+    s += k.s[3] * yp;
+    s += k.s[4] * ym;
+    s += k.s[5] * zp;
+    s += k.s[6] * zm;
+    return s;
+}
+
+// the non-linear term added after the division — CpuSolver.cpp:63-76
+template <int MODE>
+__device__ __forceinline__ double op_finish(const Coef& k, double q, double c, double w)
+{
+    if (MODE == GS_NEWTON) {
+        const double ew = exp(w);
+        q += k.gamma * (1 + w) * c * ew;
+    } else if (MODE == GS_NONLINEAR) {
+        const double ev = exp(c);
+        const double nl = k.gamma * c * ev;
+        q += nl;
+    }
+    return q;
 }
 
 // stencil sum in config order, then /h^2 and the non-linear term  — CpuSolver.cpp:56-76
@@ -826,27 +908,235 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
     }
 }
 
-// Two shapes, both 2 output rows per wave (measured on MI355X with tools/kbench.py --pairs: at 2
-// rows a wave needs ~216 VGPRs, so two waves share a SIMD and hide each other's latency, which
-// beats the lower halo overhead of 3-6 rows at one wave per SIMD by 20-25%): rows of <= 512
-// points in blocks of <= 4 waves, rows of <= 1024 points in blocks of <= 8 waves.
-constexpr int TB_RY_A = 2, TB_WX_A = 4, TB_RY_B = 2, TB_WX_B = 8;
+// The fused pair with two wave-rows per block ("tb2y"): the block is WX waves along x (the whole row)
+// times 2 waves along y; the y-wave 0 owns output rows y0..y0+RY-1, the y-wave 1 rows
+// y0+RY..y0+2RY-1. Between the two, the rows they need of each other (v of plane z and sweep-1 of
+// plane z-1 at the shared edge) pass through LDS instead of being re-read and recomputed, so a block
+// of 2RY output rows recomputes only ONE sweep-1 halo row per side and reads v rows y0-2..y0+2RY+1,
+// f rows y0-1..y0+2RY: v 1 + 4/(2RY), f 1 + 2/(2RY) times the compulsory bytes before any L2 reuse
+// (k_tb2 at RY rows per wave: 1 + 4/RY and 1 + 2/RY).
+// Both y-waves run the same code on a local row index j = -1..RY+1: wave 0 maps j to y0-1+j, wave 1
+// to the mirror image y0+2RY-j, so for both j = 0 is the recomputed halo row, j = 1..RY the own rows,
+// j = RY the row published to the other wave, j = RY+1 the row received from it and j = -1 the one
+// halo row of v loaded from memory. On wave 1 local j+1 is global y-1: the two y-neighbours are
+// swapped back before the stencil sum, which keeps the reference's term order.
+template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false>
+__global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* __restrict__ v,
+                                                           const double* __restrict__ f, const double* __restrict__ w,
+                                                           double* __restrict__ out, double* __restrict__ partials,
+                                                           int nx, int ny, int nz, int64_t ldy, int64_t ldz, int ZC,
+                                                           int zlo, int zhi)
+{
+    constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
+    constexpr int NE = NV + RY; // x-edge values per wave side: v rows 0..RY, sweep-1 rows 1..RY
+    __shared__ double red[2 * WXMAX];
+    // x-edges: [parity][y-wave][1 + x-wave][side][value]; x-wave slots 0 and WX+1 are the zero
+    // x-boundary columns (the reference's homogeneous Dirichlet boundary)
+    __shared__ double edge[2][2][WXMAX + 2][2][NE];
+    // y-edge rows: [parity][y-wave][x-wave][v | sweep-1][lane]
+    __shared__ double2 yrow[2][2][WXMAX][2][WAVE];
+    const int lane = threadIdx.x;
+    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int wy = __builtin_amdgcn_readfirstlane(threadIdx.z);
+    const int WX = blockDim.y;
+    const int tid = threadIdx.x + WAVE * (threadIdx.y + WX * threadIdx.z);
+    for (int i = tid; i < 2 * 2 * (WXMAX + 2) * 2 * NE; i += WAVE * WX * 2) (&edge[0][0][0][0][0])[i] = 0.0;
+    __syncthreads();
+    const int x0 = 1 + wx * (2 * WAVE);
+    const int x = x0 + 2 * lane;
+    const int xl = min(x, nx + 1);
+    const bool bx0 = x > nx, bx1 = x + 1 > nx;
+    const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
+    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+    const int y0 = 1 + (int)(tile % gridDim.x) * (2 * RY);
+    const int zb = 1 + (int)(tile / gridDim.x) * ZC;
+    const int ze = min(zb + ZC - 1, nz);
+    const bool mir = wy != 0;
+    auto yof = [&](int j) { return mir ? y0 + 2 * RY - j : y0 - 1 + j; };
+
+    int64_t roff[RY + 2]; // local rows j = -1..RY at index j+1
+    bool rowc[RY + 2];
+#pragma unroll
+    for (int j = -1; j <= RY; j++) {
+        const int y = yof(j);
+        roff[j + 1] = (int64_t)min(max(y, 0), ny + 1) * ldy;
+        rowc[j + 1] = y >= 1 && y <= ny;
+    }
+    auto planeok = [&](int z) { return (z >= 1 && z <= nz) || (z == 0 && zlo) || (z == nz + 1 && zhi); };
+    auto at = [&](const double* base, int j, int z) { return base + xl + roff[j + 1] + (int64_t)z * ldz; };
+
+    double2 Vp[NV], Vc[NV], VL[2][NV], FL[2][NV], WL[2][NV], HL[2];
+    double2 V1p[RY], V1c[NV], Fprev[RY], Wprev[RY];
+#pragma unroll
+    for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int j = 0; j < RY; j++) V1p[j] = make_double2(0.0, 0.0);
+    auto load_slot = [&](const int s, const int z, const int zv) {
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            VL[s][j] = ldv2<ZV>(at(v, j, zv));
+            FL[s][j] = ld2s<NTF>(at(f, j, z));
+            if (MODE == GS_NEWTON) WL[s][j] = ld2(at(w, j, z));
+        }
+        HL[s] = ldv2<ZV>(at(v, -1, z));
+    };
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        Vp[j] = ldv2<ZV>(at(v, j, zb - 2));
+        Vc[j] = ldv2<ZV>(at(v, j, zb - 1));
+    }
+    load_slot(1, zb - 1, zb);
+    double sumsq = 0.0;
+    for (int z0 = zb - 1; z0 <= ze + 1; z0 += 2) {
+#pragma unroll
+        for (int ph = 0; ph < 2; ph++) {
+            const int z = z0 + ph;
+            const int cs = ph ^ 1;
+            load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
+            // ---- publish: x-edge columns (v(z) rows 0..RY, sweep-1(z-1) rows 1..RY) and the y-edge row
+            if (lane == 0) {
+#pragma unroll
+                for (int j = 0; j < NV; j++) edge[ph][wy][wx + 1][0][j] = Vc[j].x;
+#pragma unroll
+                for (int j = 1; j <= RY; j++) edge[ph][wy][wx + 1][0][NV + j - 1] = V1c[j].x;
+            }
+            if (lane == WAVE - 1) {
+#pragma unroll
+                for (int j = 0; j < NV; j++) edge[ph][wy][wx + 1][1][j] = Vc[j].y;
+#pragma unroll
+                for (int j = 1; j <= RY; j++) edge[ph][wy][wx + 1][1][NV + j - 1] = V1c[j].y;
+            }
+            yrow[ph][wy][wx][0][lane] = Vc[RY];
+            yrow[ph][wy][wx][1][lane] = V1c[RY];
+            // LDS-only barrier: the outstanding prefetch stays in flight across it
+            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            double CL[NE], CR[NE];
+#pragma unroll
+            for (int i = 0; i < NE; i++) {
+                CL[i] = edge[ph][wy][wx][1][i];
+                CR[i] = edge[ph][wy][wx + 2][0][i];
+            }
+            const double2 vY = yrow[ph][wy ^ 1][wx][0][lane]; // v(z) at local row RY+1
+            const double2 sY = yrow[ph][wy ^ 1][wx][1][lane]; // sweep-1(z-1) at local row RY+1
+
+            // ---- the two sweeps; wave 1 (mirrored rows) runs its own copy of the code, so the swap of
+            // its y-neighbours costs no selects ----
+            double2 V1n[NV];
+            const bool pz = planeok(z);
+            auto sweeps = [&](auto mirc) {
+                const bool M = mirc.get();
+                // sweep 1 at plane z, local rows 0..RY
+#pragma unroll
+                for (int j = 0; j < NV; j++) {
+                    const double2 c = Vc[j], zm = Vp[j], zp = VL[cs][j];
+                    const double2 lm = j == 0 ? HL[cs] : Vc[j - 1], lp = j == RY ? vY : Vc[j + 1];
+                    const double2 ym = M ? lp : lm, yp = M ? lm : lp;
+                    const double xm0 = lane_from_left<true>(c.y, CL[j]);
+                    const double xp1 = lane_from_right<true>(c.x, CR[j]);
+                    double q[2] = {stencil_sum(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
+                                   stencil_sum(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
+                    div_hh_row<MODE>(k, q);
+                    const double wx0 = (MODE == GS_NEWTON) ? WL[cs][j].x : 0.0;
+                    const double wx1 = (MODE == GS_NEWTON) ? WL[cs][j].y : 0.0;
+                    const double a0 = op_finish<MODE>(k, q[0], c.x, wx0);
+                    const double a1 = op_finish<MODE>(k, q[1], c.y, wx1);
+                    const double r0 = FL[cs][j].x - a0, r1 = FL[cs][j].y - a1;
+                    const double n0 = jacobi_update<MODE>(k, c.x, r0, wx0);
+                    const double n1 = jacobi_update<MODE>(k, c.y, r1, wx1);
+                    if (partials && j >= 1 && z >= zb && z <= ze && rowc[j + 1]) {
+                        if (okx0) sumsq += r0 * r0;
+                        if (okx1) sumsq += r1 * r1;
+                    }
+                    const bool keep = !pz || !rowc[j + 1];
+                    V1n[j] = make_double2((keep || bx0) ? c.x : n0, (keep || bx1) ? c.y : n1);
+                }
+                // sweep 2 at plane z-1, own rows 1..RY
+                if (z - 1 >= zb && z - 1 <= ze) {
+                    const int64_t zo = (int64_t)(z - 1) * ldz;
+#pragma unroll
+                    for (int j = 1; j <= RY; j++) {
+                        const double2 c = V1c[j], zm = V1p[j - 1], zp = V1n[j];
+                        const double2 lm = V1c[j - 1], lp = j == RY ? sY : V1c[j + 1];
+                        const double2 ym = M ? lp : lm, yp = M ? lm : lp;
+                        const double xm0 = lane_from_left<true>(c.y, CL[NV + j - 1]);
+                        const double xp1 = lane_from_right<true>(c.x, CR[NV + j - 1]);
+                        double q[2] = {stencil_sum(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
+                                       stencil_sum(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
+                        div_hh_row<MODE>(k, q);
+                        const double wx0 = (MODE == GS_NEWTON) ? Wprev[j - 1].x : 0.0;
+                        const double wx1 = (MODE == GS_NEWTON) ? Wprev[j - 1].y : 0.0;
+                        const double a0 = op_finish<MODE>(k, q[0], c.x, wx0);
+                        const double a1 = op_finish<MODE>(k, q[1], c.y, wx1);
+                        const double o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 1].x - a0, wx0);
+                        const double o1 = jacobi_update<MODE>(k, c.y, Fprev[j - 1].y - a1, wx1);
+                        if (yof(j) <= ny) {
+                            double* qo = out + x + roff[j + 1] + zo;
+                            if (okx1) st2s<NT>(qo, o0, o1);
+                            else if (okx0) *qo = o0;
+                        }
+                    }
+                }
+            };
+            if (!SPEC) sweeps(RtBool{mir});
+            else if (mir) sweeps(BoolC<true>{});
+            else sweeps(BoolC<false>{});
+            // ---- rotate ----
+#pragma unroll
+            for (int j = 1; j <= RY; j++) {
+                V1p[j - 1] = V1c[j];
+                Fprev[j - 1] = FL[cs][j];
+                if (MODE == GS_NEWTON) Wprev[j - 1] = WL[cs][j];
+            }
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                V1c[j] = V1n[j];
+                Vp[j] = Vc[j];
+                Vc[j] = VL[cs][j];
+            }
+        }
+    }
+    if (partials) {
+        // fixed-order block sum: waves in (x, y) order
+        sumsq = wave_sum(sumsq);
+        const int wid = wx + WX * wy;
+        if (lane == 0) red[wid] = sumsq;
+        __syncthreads();
+        if (tid == 0) {
+            double t = 0.0;
+            for (int i = 0; i < 2 * WX; i++) t += red[i];
+            partials[tile] = t;
+        }
+    }
+}
+
+// Shapes of the fused pair. Rows of <= 512 points: k_tb2y, 2 y-waves of TBY_RY rows each under the
+// 4 x-waves of a row (8 waves, ~218 VGPRs: two waves per SIMD; NEWTON carries the w rows too and takes
+// 2 rows per wave to stay clear of spills). Rows of <= 1024 points: k_tb2 at 2
+// rows per wave in blocks of <= 8 x-waves (measured on MI355X with tools/kbench.py --pairs: at 2 rows
+// a wave needs ~216 VGPRs, so two waves share a SIMD and hide each other's latency, which beats the
+// lower halo overhead of 3-6 rows at one wave per SIMD by 20-25%).
+constexpr int TBY_RY = 2, TBY_RY_NEWTON = 2, TBY_WX = 4, TB_RY_B = 2, TB_WX_B = 8;
 
 // Geometry rule of the fused pair: the whole x-row in one block and enough work for >= 512 blocks of
-// 4-plane chunks; the z-chunk is then chosen for >= 1024 blocks (4..32 planes).
-// Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU).
-int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block)
+// 4-plane chunks; the z-chunk is then chosen for >= 1024 blocks (4..64 planes: at 512^3, 64-plane
+// chunks measured 5-8% faster than 32 — fewer re-read chunk-boundary planes).
+// Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU); *y2: the k_tb2y shape.
+int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
+             int mode = GS_LINEAR)
 {
     if (!S || !L || !canonical_order(S) || L->nx < 1 || L->nx > 2 * WAVE * TB_WX_B || L->ny < 1 || L->nz < 1)
         return 0;
-    const int ry = L->nx <= 2 * WAVE * TB_WX_A ? TB_RY_A : TB_RY_B;
-    const int64_t tiles = (L->ny + ry - 1) / ry;
+    const bool two = L->nx <= 2 * WAVE * TBY_WX;
+    const int rows = two ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block
+    const int64_t tiles = (L->ny + rows - 1) / rows;
     const int fills = tiles * ((L->nz + 3) / 4) >= 512 ? 2 : 1;
     int64_t c = tiles * L->nz / 1024;
-    c = c < 4 ? 4 : (c > 32 ? 32 : c);
+    c = c < 4 ? 4 : (c > 64 ? 64 : c);
     *zc = (int)c;
     *grid = dim3((unsigned)tiles, (unsigned)((L->nz + c - 1) / c));
-    *block = dim3(WAVE, (unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)));
+    *block = dim3(WAVE, (unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), two ? 2 : 1);
+    if (y2) *y2 = two;
     return fills;
 }
 
@@ -1057,11 +1347,23 @@ int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double om
     return gs_jacobi_sweep2_norm(S, L, mode, omega, gamma, v_in, v_out, f, w, zlo, zhi, nullptr, st);
 }
 
-int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L)
+const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int mode)
 {
     int zc;
     dim3 g, b;
-    if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b)) return 0;
+    bool y2 = false;
+    if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode)) return "";
+    if (y2)
+        return mode == GS_NEWTON ? "k_tb2y: 4x2 waves, 2 rows per wave, LDS halo-row exchange"
+                                 : "k_tb2y: 4x2 waves, 2 rows per wave, LDS halo-row exchange, per-wave-row code";
+    return "k_tb2: <= 8 x-waves, 2 rows per wave";
+}
+
+int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L, int mode)
+{
+    int zc;
+    dim3 g, b;
+    if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b, nullptr, mode)) return 0;
     return (int64_t)g.x * g.y;
 }
 
@@ -1071,28 +1373,31 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
 {
     int zc;
     dim3 g, b;
+    bool y2 = false;
     if (!S || bad_level(L) || !valid_stencil(S) || !v_out || !f || v_in == v_out || (!v_in && mode == GS_NONLINEAR) ||
-        (mode == GS_NEWTON && !w) || mode < GS_LINEAR || mode > GS_NEWTON || !tb2_plan(S, L, &zc, &g, &b))
+        (mode == GS_NEWTON && !w) || mode < GS_LINEAR || mode > GS_NEWTON || !tb2_plan(S, L, &zc, &g, &b, &y2, mode))
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
-#define GS_TB(M, RY, WX, Z) hipLaunchKernelGGL((k_tb2<M, RY, WX, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
+#define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
+#define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, M != GS_NEWTON>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
     const bool zv = !v_in;
-    if (b.y <= (unsigned)TB_WX_A) {
+    if (y2) {
         if (mode == GS_LINEAR) {
-            if (zv) GS_TB(GS_LINEAR, TB_RY_A, TB_WX_A, true);
-            else GS_TB(GS_LINEAR, TB_RY_A, TB_WX_A, false);
-        } else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_A, TB_WX_A, false);
-        else if (zv) GS_TB(GS_NEWTON, TB_RY_A, TB_WX_A, true);
-        else GS_TB(GS_NEWTON, TB_RY_A, TB_WX_A, false);
+            if (zv) GS_TBY(GS_LINEAR, true);
+            else GS_TBY(GS_LINEAR, false);
+        } else if (mode == GS_NONLINEAR) GS_TBY(GS_NONLINEAR, false);
+        else if (zv) GS_TBY(GS_NEWTON, true);
+        else GS_TBY(GS_NEWTON, false);
     } else {
         if (mode == GS_LINEAR) {
-            if (zv) GS_TB(GS_LINEAR, TB_RY_B, TB_WX_B, true);
-            else GS_TB(GS_LINEAR, TB_RY_B, TB_WX_B, false);
-        } else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, TB_RY_B, TB_WX_B, false);
-        else if (zv) GS_TB(GS_NEWTON, TB_RY_B, TB_WX_B, true);
-        else GS_TB(GS_NEWTON, TB_RY_B, TB_WX_B, false);
+            if (zv) GS_TB(GS_LINEAR, true);
+            else GS_TB(GS_LINEAR, false);
+        } else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, false);
+        else if (zv) GS_TB(GS_NEWTON, true);
+        else GS_TB(GS_NEWTON, false);
     }
+#undef GS_TBY
 #undef GS_TB
     return launch_status();
 }
@@ -1208,7 +1513,8 @@ const char* gs_strerror(int code)
 
 const char* gs_build_info(void)
 {
-    return "gpusolve_hip v4: rb(ry8 w2 zc<=32 dpp nt) large levels, 1-pt/thread small levels; fp-contract=off";
+    return "gpusolve_hip v5: pairs k_tb2y(4x2 waves, 2 rows/wave, zc<=64) / k_tb2 (rows > 512), sweeps "
+           "k_rb(ry2 w4 zc<=32 dpp nt), 1-pt/thread small levels; fp-contract=off";
 }
 
 int gs_debug_num_variants(void) { return kNumVariants; }
@@ -1236,13 +1542,22 @@ int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, 
 // block (the launch bound, hence the VGPR budget: 4 waves -> 512, 8 waves -> 256 per lane).
 struct PairVariant {
     const char* name;
-    int ry, wxmax;
+    int ry, wxmax, wy;
     void (*kern)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
                  int64_t, int, int, int);
 };
-#define GS_PV(RY, WX) {"tb2 ry" #RY " wx" #WX, RY, WX, k_tb2<GS_LINEAR, RY, WX, true>}
-#define GS_PVF(RY, WX) {"tb2 ry" #RY " wx" #WX " f-cached", RY, WX, k_tb2<GS_LINEAR, RY, WX, true, false>}
-const PairVariant kPairVariants[] = {GS_PV(2, 4), GS_PVF(2, 4), GS_PV(2, 8), GS_PVF(2, 8), GS_PV(4, 4), GS_PV(3, 8)};
+#define GS_PV(RY, WX) {"tb2 ry" #RY " wx" #WX, RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true>}
+#define GS_PVF(RY, WX) {"tb2 ry" #RY " wx" #WX " f-cached", RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true, false>}
+#define GS_PVY(RY, NTF, SPEC, TAG) {"tb2y ry" #RY " wx4 wy2" TAG, RY, 4, 2, k_tb2y<GS_LINEAR, RY, 4, true, NTF, false, SPEC>}
+const PairVariant kPairVariants[] = {GS_PVF(2, 4),
+                                     GS_PVF(2, 8),
+                                     GS_PV(2, 4),
+                                     GS_PVY(2, false, false, " f-cached"),
+                                     GS_PVY(3, false, false, " f-cached"),
+                                     GS_PVY(2, false, true, " f-cached spec"),
+                                     GS_PVY(3, false, true, " f-cached spec"),
+                                     GS_PVY(3, true, false, " f-nt")};
+#undef GS_PVY
 #undef GS_PVF
 #undef GS_PV
 constexpr int kNumPairVariants = (int)(sizeof(kPairVariants) / sizeof(kPairVariants[0]));
@@ -1262,13 +1577,13 @@ int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, d
     const PairVariant& V = kPairVariants[variant];
     const int64_t wx = (L->nx + 2 * WAVE - 1) / (2 * WAVE);
     if (L->nx < 1 || L->ny < 1 || L->nz < 1 || wx > V.wxmax) return GS_EINVAL;
-    const int64_t tiles = (L->ny + V.ry - 1) / V.ry;
+    const int64_t tiles = (L->ny + V.ry * V.wy - 1) / (V.ry * V.wy);
     if (zc == 0) {
         int64_t c = tiles * L->nz / 1024;
         zc = (int)(c < 4 ? 4 : (c > 32 ? 32 : c));
     }
     const Coef k = make_coef(S, L, omega, 0.0);
-    hipLaunchKernelGGL(V.kern, dim3((unsigned)tiles, (unsigned)((L->nz + zc - 1) / zc)), dim3(WAVE, (unsigned)wx), 0,
+    hipLaunchKernelGGL(V.kern, dim3((unsigned)tiles, (unsigned)((L->nz + zc - 1) / zc)), dim3(WAVE, (unsigned)wx, V.wy), 0,
                        st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc,
                        0, 0);
     return launch_status();

@@ -95,12 +95,15 @@ int gs_jacobi_sweep2_supported(const gs_stencil* S, const gs_level* L);
 int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                      const double* v_in, double* v_out, const double* f, const double* w, int zlo, int zhi,
                      hipStream_t stream);
-/* The fused pair, also writing gs_jacobi_sweep2_num_partials(S, L) per-block sums of r^2 of the
- * residual r = f - A(v_in) its first sweep computes (the compResidual norm of v_in, fixed order). */
+/* The fused pair, also writing gs_jacobi_sweep2_num_partials(S, L, mode) per-block sums of r^2 of the
+ * residual r = f - A(v_in) its first sweep computes (the compResidual norm of v_in, fixed order; the
+ * block shape, hence the count, depends on the mode). */
 int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                           const double* v_in, double* v_out, const double* f, const double* w, int zlo, int zhi,
                           double* partials, hipStream_t stream);
-int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L);
+int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L, int mode);
+/* Which fused-pair kernel (and shape) gs_jacobi_sweep2 launches for this level and mode ("" if none). */
+const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int mode);
 
 /* r = f - A(v) on the interior. r may be NULL (norm only). partials may be NULL (no norm);
  * otherwise it receives gs_residual_num_partials(S, L) per-block sums of r^2 in a fixed order. */

@@ -124,7 +124,7 @@ def test_sweep2_norm_partials(shape, mode):
     v, f, w, out, out2 = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
                           DevField(nx, ny, nz).from_xyz(w0), DevField(nx, ny, nz), DevField(nx, ny, nz))
     L = v.level(h)
-    n = k().gs_jacobi_sweep2_num_partials(C.byref(stencil()), C.byref(L))
+    n = k().gs_jacobi_sweep2_num_partials(C.byref(stencil()), C.byref(L), mode)
     assert n >= 1
     parts = torch.full((n,), float("nan"), dtype=torch.float64, device="cuda")
     ok(k().gs_jacobi_sweep2_norm(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, out.ptr, f.ptr, w.ptr, 0, 0,

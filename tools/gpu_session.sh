@@ -21,9 +21,16 @@ step bench
 timeout -k 10 600 python bench.py --steps "$STEPS" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
 
+# kernel statistics of the bench's timed smoother alone (no V-cycles: every launch of the pair kernel
+# is a level-0 launch, so its average is the bench's kernel_ms)
 step rocprof-kernel-trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python bench.py --steps "$STEPS" --cpu-sweeps 0 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail -20 "$OUT/bench_prof.err"; exit 1; }
+    python bench.py --steps "$STEPS" --cpu-sweeps 0 --vcycles 0 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail -20 "$OUT/bench_prof.err"; exit 1; }
+
+# the V-cycle's kernels (tools/vc_breakdown.py reads the trace)
+step rocprof-vcycle
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_vc" -o run --output-format csv -- \
+    python bench.py --steps 2 --warmup 2 --cpu-sweeps 0 --vcycles 10 > "$OUT/bench_vc.json" 2> "$OUT/bench_vc.err" || { tail -20 "$OUT/bench_vc.err"; exit 1; }
 
 step rocprof-pmc-fetch
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \

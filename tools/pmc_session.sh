@@ -5,6 +5,7 @@
 set -o pipefail
 TAG=${1:-pmc}
 SIZE=${2:-512}
+EXTRA=${3:-}   # extra prof_kernels.py arguments, e.g. "--which pair --pair-variants 0,3 --zc 64"
 OUT=gpurun_out/$TAG/pmc
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
@@ -18,6 +19,6 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
     i=$((i + 1))
     echo "[$(date +%T)] pass $i: $set"
     timeout -k 10 300 rocprofv3 --pmc $set -d "$OUT/p$i" -o run --output-format csv -- \
-        python tools/prof_kernels.py --size "$SIZE" --reps 3 > "$OUT/p$i.log" 2>&1 || { tail -20 "$OUT/p$i.log"; exit 1; }
+        python tools/prof_kernels.py --size "$SIZE" --reps 3 $EXTRA > "$OUT/p$i.log" 2>&1 || { tail -20 "$OUT/p$i.log"; exit 1; }
 done
 echo "[$(date +%T)] done"

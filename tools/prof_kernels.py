@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--which", default="pair,single,residual")
+    ap.add_argument("--pair-variants", default="", help="also launch these gs_debug_pair_variant ids")
+    ap.add_argument("--zc", type=int, default=0, help="z-chunk of the pair variants (0 = auto)")
     a = ap.parse_args()
     n = a.size
     kl = gsv.kernels()
@@ -36,6 +38,8 @@ def main():
             assert kl.gs_jacobi_sweep2(C.byref(S), C.byref(L), 0, 0.8, 1.0, v.ptr, v2.ptr, f.ptr, None, 0, 0, st) == 0
         if "single" in a.which:
             assert kl.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, v.ptr, v2.ptr, f.ptr, None, st) == 0
+        for i in filter(None, a.pair_variants.split(",")):
+            assert kl.gs_debug_pair_variant(int(i), C.byref(S), C.byref(L), 0.8, v.ptr, v2.ptr, f.ptr, a.zc, st) == 0
         if "residual" in a.which:
             assert kl.gs_residual(C.byref(S), C.byref(L), 0, 1.0, v.ptr, f.ptr, None, r.ptr, None, st) == 0
     torch.cuda.synchronize()

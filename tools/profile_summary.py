@@ -22,8 +22,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def sweep_kernel(name):
-    """The level-0 smoother of bench.py: the fused pair (k_tb2) or, without it, the one-sweep k_rb."""
-    return "k_tb2<0," in name
+    """The level-0 smoother of bench.py: the fused pair (k_tb2y / k_tb2) or, without it, the one-sweep k_rb."""
+    return "k_tb2y<0," in name or "k_tb2<0," in name
 
 
 def single_kernel(name):
@@ -86,6 +86,14 @@ def main():
         lines += ["", "## PMC (level-0 sweep, bench.py config)", "", "```", json.dumps(d, indent=1), "```"]
     if bench:
         lines += ["", "## bench.py line", "", "```", json.dumps(bench, indent=1), "```"]
+    vct = os.path.join(src, "prof_vc", "run_kernel_trace.csv")
+    if os.path.exists(vct):
+        import subprocess
+        out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "vc_breakdown.py"), vct, "30"],
+                             capture_output=True, text=True).stdout
+        shutil.copy(os.path.join(src, "prof_vc", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_vcycle_stats.csv"))
+        lines += ["", "## One 512^3 linear 2+2 V-cycle, kernel by kernel (rocprofv3 kernel trace, last cycle)", "",
+                  "```", out.strip(), "```"]
     kb = os.path.join(src, "kbench.json")
     if os.path.exists(kb):
         k = json.load(open(kb))
