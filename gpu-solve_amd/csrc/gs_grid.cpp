@@ -434,8 +434,17 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
         jacobi(grid, i, pre);
         auto& L = grid.getLevel(i);
         auto& C = grid.getLevel(i + 1);
-        compResidual(grid, i, true, false);
-        restrictTo(grid, L.r, i, C.f, nullptr, true); // f^2h = R r^h (ghosts: the fused pair reads them)
+        static const bool noFusedRR = std::getenv("GS_NO_FUSED_RR") != nullptr;
+        if (!noFusedRR && !(L.distributed && grid.nranks() > 1)) {
+            // f^2h = R (f^h - A v^h) in one pass: the fine residual is never stored
+            materialize(grid, i);
+            check(gs_residual_restrict(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(), L.f.data(),
+                                       L.newtonV ? L.newtonV.data() : nullptr, C.f.data(), nullptr, &C.geom, s),
+                  "gs_residual_restrict");
+        } else {
+            compResidual(grid, i, true, false);
+            restrictTo(grid, L.r, i, C.f, nullptr, true); // f^2h = R r^h (ghosts: the fused pair reads them)
+        }
         if (grid.mode != GridParams::NONLINEAR) {
             // v^2h = 0 (CpuSolver.cpp:114-116): not stored; the first sweep on the level reads no v
             static const bool noZeroGuess = std::getenv("GS_NO_ZERO_GUESS") != nullptr;

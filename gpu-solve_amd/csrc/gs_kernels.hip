@@ -563,6 +563,172 @@ __global__ __launch_bounds__(256) void k_restrict(const double* __restrict__ fin
 }
 
 // ---------------------------------------------------------------------------------------------
+// Residual fused into the full-weighting restriction: coarse f = R(f - A v) without writing the fine
+// residual to memory (CpuSolver.cpp:45-83 then :211-238; the reference stores r and re-reads it).
+// A block owns RR_TXC x RR_TYC coarse columns and marches a chunk of coarse planes. The fine region
+// its 27-point stencils touch is (2 RR_TXC + 1) x (2 RR_TYC + 1) points per plane; the v tile with its
+// one-point halo is staged in a 4-plane LDS ring (loaded once, coalesced along x), the residual of
+// that region in a 3-plane LDS ring. Per coarse plane Z: the two new v planes and the f values of the
+// next plane pair are loaded into registers while the current ones are computed (software pipeline),
+// r is evaluated on fine planes 2Z and 2Z+1 (2Z-1 is kept from the previous plane), then every
+// thread sums its coarse point's 27 terms in the reference's order. Fine points outside the interior
+// hold r = 0, as the reference's never-written boundary does. Each residual is the gs_residual
+// expression and each sum the gs_restrict one: bit-identical to the unfused pair.
+constexpr int RR_TXC = 64, RR_TYC = 4, RR_T = RR_TXC * RR_TYC;
+constexpr int RR_FX = 2 * RR_TXC + 1, RR_FY = 2 * RR_TYC + 1; // residual region per plane
+constexpr int RR_VX = RR_FX + 2, RR_VY = RR_FY + 2;           // v tile per plane (one-point halo)
+constexpr int RR_NR = (RR_FX * RR_FY + RR_T - 1) / RR_T;      // residual points per thread and plane
+constexpr int RR_NV = (RR_VX * RR_VY + RR_T - 1) / RR_T;      // v tile points per thread and plane
+
+struct StencilOffsets {
+    int lds[7]; // ox + oy * RR_VX (in-plane LDS offset)
+    int oz[7];
+};
+
+template <int MODE>
+__global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so, const double* __restrict__ v,
+                                                      const double* __restrict__ f, const double* __restrict__ w,
+                                                      double* __restrict__ ca, double* __restrict__ cb, int fnx,
+                                                      int fny, int fnz, int64_t fldy, int64_t fldz, int cnx, int cny,
+                                                      int cnz, int64_t cldy, int64_t cldz, int zoff, int ZC)
+{
+    // one LDS array addressed with integer offsets (pointers into it would become flat accesses):
+    // v ring slots 0..3 at s * RR_VP, residual ring slots 0..2 at 4 RR_VP + s * RR_RP
+    constexpr int RR_VP = RR_VY * RR_VX, RR_RP = RR_FY * RR_FX;
+    __shared__ double lds[4 * RR_VP + 3 * RR_RP];
+    const int tid = threadIdx.x;
+    const int X0 = 1 + blockIdx.x * RR_TXC, Y0 = 1 + blockIdx.y * RR_TYC;
+    const int Zb = 1 + blockIdx.z * ZC, Ze = min(Zb + ZC - 1, cnz);
+    if (Zb > Ze) return;
+    const int fx0 = 2 * X0 - 1, fy0 = 2 * Y0 - 1; // residual region origin (fine)
+
+    // this thread's v-tile points (clamped into the padded level: clamped copies are never used)
+    int64_t voff[RR_NV];
+#pragma unroll
+    for (int i = 0; i < RR_NV; i++) {
+        const int e = min(tid + i * RR_T, RR_VX * RR_VY - 1);
+        const int ly = e / RR_VX, lx = e - ly * RR_VX;
+        voff[i] = min(fx0 - 1 + lx, fnx + 1) + (int64_t)min(fy0 - 1 + ly, fny + 1) * fldy;
+    }
+    // this thread's residual points: global offset, LDS position, interior flag
+    int64_t roff[RR_NR];
+    int rpos[RR_NR];
+    bool rin[RR_NR];
+#pragma unroll
+    for (int i = 0; i < RR_NR; i++) {
+        const int e = tid + i * RR_T;
+        const int ry = min(e, RR_FX * RR_FY - 1) / RR_FX, rx = min(e, RR_FX * RR_FY - 1) - ry * RR_FX;
+        const int x = fx0 + rx, y = fy0 + ry;
+        rin[i] = e < RR_FX * RR_FY && x <= fnx && y <= fny;
+        roff[i] = min(x, fnx + 1) + (int64_t)min(y, fny + 1) * fldy;
+        rpos[i] = (ry + 1) * RR_VX + rx + 1;
+    }
+    auto zc = [&](int fz) { return (int64_t)min(max(fz, -1), fnz + 2) * fldz; };
+    auto load_v = [&](double (&dst)[RR_NV], int fz) {
+        const int64_t zo = zc(fz);
+#pragma unroll
+        for (int i = 0; i < RR_NV; i++) dst[i] = v[voff[i] + zo];
+    };
+    auto store_v = [&](const double (&src)[RR_NV], int fz) {
+        const int d = ((fz + 4) & 3) * RR_VP;
+#pragma unroll
+        for (int i = 0; i < RR_NV; i++)
+            if (tid + i * RR_T < RR_VP) lds[d + tid + i * RR_T] = src[i];
+    };
+    auto load_fw = [&](double (&F)[RR_NR], double (&W)[RR_NR], int fz) {
+        const int64_t zo = zc(fz);
+#pragma unroll
+        for (int i = 0; i < RR_NR; i++) {
+            F[i] = f[roff[i] + zo];
+            if (MODE == GS_NEWTON) W[i] = w[roff[i] + zo];
+        }
+    };
+    // r on fine plane fz from the v ring (needs planes fz-1 .. fz+1 staged)
+    auto residual_plane = [&](const double (&F)[RR_NR], const double (&W)[RR_NR], int fz) {
+        int toff[7]; // LDS offset of each stencil term relative to the point's in-plane position
+#pragma unroll
+        for (int t = 0; t < 7; t++) toff[t] = ((fz + 4 + so.oz[t]) & 3) * RR_VP + so.lds[t];
+        const int coff = ((fz + 4) & 3) * RR_VP;
+        const int dst = 4 * RR_VP + ((fz + 3) % 3) * RR_RP;
+        const bool zin = fz >= 1 && fz <= fnz;
+#pragma unroll
+        for (int i = 0; i < RR_NR; i++) {
+            if (tid + i * RR_T >= RR_FX * RR_FY) continue;
+            double r = 0.0;
+            if (zin && rin[i]) {
+                double sum = 0.0;
+#pragma unroll
+                for (int t = 0; t < 7; t++) sum += k.s[t] * lds[rpos[i] + toff[t]];
+                const double c = lds[rpos[i] + coff];
+                const double q = op_finish<MODE>(k, div_hh(k, sum), c, MODE == GS_NEWTON ? W[i] : 0.0);
+                r = F[i] - q;
+            }
+            lds[dst + tid + i * RR_T] = r;
+        }
+    };
+
+    double VA[RR_NV], VB[RR_NV], FA[RR_NR], FB[RR_NR], WA[RR_NR], WB[RR_NR];
+    // prologue: v planes P-2 .. P (P = 2 Zb + zoff) into the ring, r(P-1)
+    const int P0 = 2 * Zb + zoff;
+    load_v(VA, P0 - 2);
+    load_v(VB, P0 - 1);
+    load_fw(FA, WA, P0 - 1);
+    store_v(VA, P0 - 2);
+    store_v(VB, P0 - 1);
+    load_v(VA, P0);
+    store_v(VA, P0);
+    __syncthreads();
+    residual_plane(FA, WA, P0 - 1);
+    // staged for the first step: v(P+1), v(P+2), f(P), f(P+1)
+    load_v(VA, P0 + 1);
+    load_v(VB, P0 + 2);
+    load_fw(FA, WA, P0);
+    load_fw(FB, WB, P0 + 1);
+    __syncthreads(); // v(P+2) goes to the slot of v(P-2), which r(P-1) just read
+    const int cx = tid % RR_TXC, cy = tid / RR_TXC;
+    const int X = X0 + cx, Y = Y0 + cy;
+    for (int Z = Zb; Z <= Ze; Z++) {
+        const int P = 2 * Z + zoff;
+        store_v(VA, P + 1);
+        store_v(VB, P + 2);
+        __syncthreads();
+        double F0[RR_NR], F1[RR_NR], W0[RR_NR], W1[RR_NR];
+#pragma unroll
+        for (int i = 0; i < RR_NR; i++) {
+            F0[i] = FA[i];
+            F1[i] = FB[i];
+            W0[i] = WA[i];
+            W1[i] = WB[i];
+        }
+        if (Z < Ze) { // the next step's operands, in flight during this step's arithmetic
+            load_v(VA, P + 3);
+            load_v(VB, P + 4);
+            load_fw(FA, WA, P + 2);
+            load_fw(FB, WB, P + 3);
+        }
+        residual_plane(F0, W0, P);
+        residual_plane(F1, W1, P + 1);
+        __syncthreads();
+        if (X <= cnx && Y <= cny) {
+            double acc = 0.0;
+#pragma unroll
+            for (int a = -1; a <= 1; a++)
+#pragma unroll
+                for (int b = -1; b <= 1; b++)
+#pragma unroll
+                    for (int c = -1; c <= 1; c++) {
+                        const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) * ((2.0 - (b < 0 ? -b : b)) / 2.0) *
+                                           ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                        acc += wgt * lds[4 * RR_VP + ((P + c + 3) % 3) * RR_RP + (2 * cy + 1 + b) * RR_FX + 2 * cx + 1 + a];
+                    }
+            const int64_t q = X + Y * cldy + (int64_t)Z * cldz;
+            ca[q] = acc;
+            if (cb) cb[q] = acc;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Trilinear prolongation, closed form per fine point (the reference's inject + X, Y, Z passes,
 // CpuSolver.cpp:240-290, combined in the same X -> Y -> Z order). Fine index P-1 is never written by
 // the reference (stays 0) and coarse index Pc-1 is the zero boundary, so along each axis:
@@ -1437,6 +1603,38 @@ int gs_restrict2(const double* fine, const gs_level* fl, double* ca, double* cb,
     const dim3 g((unsigned)((cl->nx + 63) / 64), (unsigned)((cl->ny + 3) / 4), (unsigned)cl->nz), b(64, 4);
     hipLaunchKernelGGL(k_restrict, g, b, 0, st, fine, ca, cb, (int)cl->nx, (int)cl->ny, (int)cl->nz, fl->ldy, fl->ldz,
                        cl->ldy, cl->ldz, (int)zoff);
+    return launch_status();
+}
+
+int gs_residual_restrict(const gs_stencil* S, const gs_level* fl, int mode, double gamma, const double* v,
+                         const double* f, const double* w, double* ca, double* cb, const gs_level* cl, hipStream_t st)
+{
+    if (!S || !valid_stencil(S) || !v || !f || !ca || (mode == GS_NEWTON && !w) || mode < GS_LINEAR ||
+        mode > GS_NEWTON || bad_level(fl) || bad_level(cl))
+        return GS_EINVAL;
+    if (cl->nx == 0 || cl->ny == 0 || cl->nz == 0) return 0;
+    const int64_t zoff = 2 * cl->z0 - fl->z0; // fine local centre plane = 2 z + zoff
+    // the residual is evaluated on fine local planes 2z+zoff-1 .. 2z+zoff+1 of the interior only
+    // (planes 0 and nz+1 hold r = 0): they must exist, as must the coarse points' fine columns
+    if (2 * cl->nx + 1 > fl->nx + 1 || 2 * cl->ny + 1 > fl->ny + 1 || 2 + zoff - 1 < 0 ||
+        2 * cl->nz + zoff + 1 > fl->nz + 1)
+        return GS_EINVAL;
+    const Coef k = make_coef(S, fl, 0.0, gamma);
+    StencilOffsets so;
+    for (int t = 0; t < 7; t++) {
+        so.lds[t] = S->ox[t] + S->oy[t] * RR_VX;
+        so.oz[t] = S->oz[t];
+    }
+    const int64_t tiles = ((cl->nx + RR_TXC - 1) / RR_TXC) * ((cl->ny + RR_TYC - 1) / RR_TYC);
+    int64_t zc = tiles * cl->nz / 4096; // >= 4096 blocks where the level has them, 1..16 planes each
+    zc = zc < 1 ? 1 : (zc > 16 ? 16 : zc);
+    const dim3 g((unsigned)((cl->nx + RR_TXC - 1) / RR_TXC), (unsigned)((cl->ny + RR_TYC - 1) / RR_TYC),
+                 (unsigned)((cl->nz + zc - 1) / zc));
+#define GS_RR(M) hipLaunchKernelGGL(k_resrestrict<M>, g, dim3(RR_T), 0, st, k, so, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zoff, (int)zc)
+    if (mode == GS_LINEAR) GS_RR(GS_LINEAR);
+    else if (mode == GS_NONLINEAR) GS_RR(GS_NONLINEAR);
+    else GS_RR(GS_NEWTON);
+#undef GS_RR
     return launch_status();
 }
 

@@ -54,6 +54,9 @@ KERNEL_API = {
     "gs_residual_num_partials": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),
     "gs_sumsq_finish": (C.c_int, [C.c_void_p, i64, C.c_void_p, C.c_int, C.c_void_p]),
     "gs_restrict": (C.c_int, [C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.POINTER(gs_level), C.c_void_p]),
+    "gs_residual_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.POINTER(gs_level), C.c_void_p]),
     "gs_restrict2": (C.c_int, [C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.c_void_p, C.POINTER(gs_level),
                                C.c_void_p]),
     "gs_interpolate": (C.c_int, [C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.POINTER(gs_level), C.c_void_p]),

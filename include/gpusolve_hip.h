@@ -9,6 +9,8 @@
  *   gs_sumsq_finish      the sqrt(sum r^2) of compResidual     src/cpu/CpuSolver.cpp:51,77,82
  *   gs_restrict          CpuSolver::restrict                   src/cpu/CpuSolver.cpp:211-238
  *   gs_restrict2         two restrict calls of the FAS branch  src/cpu/CpuSolver.cpp:104-107
+ *   gs_residual_restrict compResidual + restrict (r never stored) src/cpu/CpuSolver.cpp:98-99
+ *   gs_jacobi_sweep2     two CpuSolver::jacobi sweeps fused    src/cpu/CpuSolver.cpp:141-180 (k=2)
  *   gs_interpolate       CpuSolver::interpolate                src/cpu/CpuSolver.cpp:240-290
  *   gs_prolong_add       interpolate + (v_c -= restV_c) + (v_f += e_f)
  *                                                              src/cpu/CpuSolver.cpp:121-132
@@ -116,6 +118,12 @@ int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L);
 int gs_sumsq_finish(const double* partials, int64_t n, double* out, int accumulate, hipStream_t stream);
 
 /* 27-point full weighting of fine onto the coarse interior. */
+/* Fused residual + full weighting: coarse = R(f - A(v)) on the coarse interior, with the fine
+ * residual never stored (bit-identical to gs_residual followed by gs_restrict2). cb may be NULL.
+ * Replaces src/cpu/CpuSolver.cpp:45-83 + :211-238 as called at CpuSolver.cpp:98-99. */
+int gs_residual_restrict(const gs_stencil* S, const gs_level* fine, int mode, double gamma, const double* v,
+                         const double* f, const double* w, double* coarse_a, double* coarse_b,
+                         const gs_level* coarse, hipStream_t stream);
 int gs_restrict(const double* fine, const gs_level* fl, double* coarse, const gs_level* cl, hipStream_t stream);
 /* Same, writing two coarse outputs (FAS restV and v). */
 int gs_restrict2(const double* fine, const gs_level* fl, double* coarse_a, double* coarse_b, const gs_level* cl,

@@ -277,3 +277,47 @@ def test_invalid_arguments_fail_loudly():
     rc = k().gs_jacobi_sweep(C.byref(S), C.byref(bad), 0, 0.8, 1.0, v.ptr, DevField(8, 8, 8).ptr, v.ptr, None,
                              stream())
     assert rc == gsv._abi.GS_EINVAL
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("fd", [(2, 2, 2), (3, 5, 7), (16, 17, 18), (129, 33, 20), (130, 8, 9), (255, 10, 33),
+                                (64, 64, 64)])
+def test_residual_restrict_fused(fd, mode):
+    """gs_residual_restrict == gs_residual + gs_restrict2 bit for bit (and == the oracle's restrict of
+    the oracle's residual, to the mode's tolerance); odd and even fine extents, partial tiles."""
+    rng = np.random.default_rng(sum(fd) * 3 + mode)
+    cd = [x // 2 for x in fd]
+    h = 1.0 / (fd[1] + 1)
+    v0, f0, w0 = rand_field(rng, *fd), rand_field(rng, *fd, 100.0), rand_field(rng, *fd)
+    S = S_abi((6, -1, -1.5, -1, -0.5, -1, -1))
+    v, f, w = dev(v0), dev(f0), dev(w0)
+    L = v.level(h)
+    r = DevField(*fd)
+    r.buf.zero_()
+    ok(k().gs_residual(C.byref(S), C.byref(L), mode, 0.7, v.ptr, f.ptr, w.ptr, r.ptr, None, stream()))
+    ca_ref, ca, cb = DevField(*cd), DevField(*cd), DevField(*cd)
+    Lc = ca.level(2 * h)
+    ok(k().gs_restrict2(r.ptr, C.byref(r.level(h)), ca_ref.ptr, None, C.byref(Lc), stream()))
+    ok(k().gs_residual_restrict(C.byref(S), C.byref(L), mode, 0.7, v.ptr, f.ptr, w.ptr, ca.ptr, cb.ptr,
+                                C.byref(Lc), stream()))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ca.to_xyz(), ca_ref.to_xyz())
+    np.testing.assert_array_equal(cb.to_xyz(), ca_ref.to_xyz())
+    rr, _ = O.residual(v0, f0, h, mode, 0.7, w=w0,
+                       stencil=O.Stencil.make((6, -1, -1.5, -1, -0.5, -1, -1), gsv.CANONICAL_OFFSETS))
+    assert_field(ca.to_xyz(), O.restrict(rr, cd), mode, f"rr {fd} m{mode}")
+
+
+def test_residual_restrict_generic_stencil():
+    rng = np.random.default_rng(11)
+    fd = (37, 11, 9)
+    cd = [x // 2 for x in fd]
+    vals = (8, -1, -1, -1, -1, -2, -2)
+    offs = [(0, 0, 0), (1, 1, 0), (-1, -1, 0), (1, -1, 1), (-1, 1, -1), (0, 1, 1), (0, -1, -1)]
+    v0, f0 = rand_field(rng, *fd), rand_field(rng, *fd, 50.0)
+    S = S_abi(vals, offs)
+    v, f, ca = dev(v0), dev(f0), DevField(*cd)
+    ok(k().gs_residual_restrict(C.byref(S), C.byref(v.level(0.1)), 0, 0.5, v.ptr, f.ptr, None, ca.ptr, None,
+                                C.byref(ca.level(0.2)), stream()))
+    rr, _ = O.residual(v0, f0, 0.1, 0, 0.5, stencil=O.Stencil.make(vals, offs))
+    np.testing.assert_array_equal(ca.to_xyz(), O.restrict(rr, cd))
