@@ -251,6 +251,56 @@ int gs_grid_upload(void* grid, int level, int field, const double* host)
     return copy_field(grid, level, field, nullptr, host);
 }
 
+// Vector3::dump (src/cpu/Vector3.cpp:56-78): with a file, the header "Px Py Pz" then one line
+// "x y z value" per padded point, x outermost and z innermost; without one (empty path or a file
+// that cannot be opened) the same lines go to stdout, header omitted. Values use the iostream
+// default format (6 significant digits, printf %g). Lines are formatted in parallel x-slabs and
+// written in order.
+int gs_dump_write(const double* host, int64_t px, int64_t py, int64_t pz, const char* path)
+{
+    return guarded([&] {
+        if (!host || px < 0 || py < 0 || pz < 0) throw gs::Error("gs_dump_write: invalid argument");
+        std::FILE* out = (path && *path) ? std::fopen(path, "w") : nullptr;
+        std::FILE* dst = out ? out : stdout;
+        if (out) std::fprintf(out, "%lld %lld %lld\n", (long long)px, (long long)py, (long long)pz);
+        const int64_t nthreads = std::max<int64_t>(1, std::min<int64_t>(px, std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()))));
+        const int64_t chunk = 8; // x-planes per task
+        for (int64_t x0 = 0; x0 < px; x0 += chunk * nthreads) {
+            std::vector<std::string> part((size_t)nthreads);
+            std::vector<std::thread> th;
+            for (int64_t t = 0; t < nthreads; t++)
+                th.emplace_back([&, t] {
+                    std::string& s = part[(size_t)t];
+                    char buf[96];
+                    for (int64_t x = x0 + t * chunk; x < std::min(px, x0 + (t + 1) * chunk); x++)
+                        for (int64_t y = 0; y < py; y++)
+                            for (int64_t z = 0; z < pz; z++) {
+                                const int n = std::snprintf(buf, sizeof buf, "%lld %lld %lld %g\n", (long long)x,
+                                                            (long long)y, (long long)z, host[x + px * (y + py * z)]);
+                                s.append(buf, (size_t)n);
+                            }
+                });
+            for (auto& t : th) t.join();
+            for (auto& s : part) std::fwrite(s.data(), 1, s.size(), dst);
+        }
+        if (out) {
+            if (std::fclose(out) != 0) throw gs::Error("gs_dump_write: write failed");
+        } else {
+            std::fflush(stdout);
+        }
+    });
+}
+
+int gs_grid_dump(void* grid, int level, int field, const char* path)
+{
+    if (level < 0 || level >= (int)G(grid).numLevels()) return guarded([] { throw gs::Error("no such level"); });
+    const gs_level& L = G(grid).getLevel(level).geom;
+    std::vector<double> host((size_t)((L.nx + 2) * (L.ny + 2) * (L.nz + 2)));
+    const int rc = gs_grid_download(grid, level, field, host.data());
+    if (rc) return rc;
+    return gs_dump_write(host.data(), L.nx + 2, L.ny + 2, L.nz + 2, path);
+}
+
 int gs_grid_sync(void* grid)
 {
     return guarded([&] { gs::check((int)hipStreamSynchronize(G(grid).stream()), "hipStreamSynchronize"); });

@@ -10,6 +10,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "gpusolve_driver.h"
+
 namespace gs {
 
 void check(int code, const char* what)
@@ -538,6 +540,21 @@ void NewtonSolver::findError(HipGridData& grid)
     auto& L0 = grid.getLevel(0);
     // whole local array, ghost planes included: both operands' ghosts are current, so the sum's are
     check(gs_axpy(L0.newtonV.data(), L0.v.data(), 1.0, L0.v.span(), grid.stream()), "gs_axpy");
+}
+
+void dumpField(HipGridData& grid, std::size_t level, const std::string& path)
+{
+    auto& L = grid.getLevel(level);
+    HipSolver::materialize(grid, level);
+    const gs_level& g = L.geom;
+    const std::size_t px = (std::size_t)g.nx + 2, py = (std::size_t)g.ny + 2, pz = (std::size_t)g.nz + 2;
+    std::vector<double> host(px * py * pz);
+    check((int)hipStreamSynchronize(grid.stream()), "hipStreamSynchronize");
+    check((int)hipMemcpy2D(host.data(), sizeof(double) * px, L.v.data(), sizeof(double) * (std::size_t)g.ldy,
+                           sizeof(double) * px, py * pz, hipMemcpyDeviceToHost),
+          "hipMemcpy2D");
+    if (gs_dump_write(host.data(), (int64_t)px, (int64_t)py, (int64_t)pz, path.c_str()) != 0)
+        throw Error(gs_last_error());
 }
 
 } // namespace gs

@@ -153,4 +153,7 @@ public:
     static thread_local std::vector<double>* history;
 };
 
+// Vector3::dump (src/cpu/Vector3.cpp:56-78) of level `level`'s iterate v (this rank's slab).
+void dumpField(HipGridData& grid, std::size_t level, const std::string& path);
+
 } // namespace gs

@@ -50,6 +50,7 @@ int main(int argc, char* argv[])
         gs::HipGridData grid(gridParams);
         if (gridParams.mode == gs::GridParams::NEWTON) gs::NewtonSolver::solve(grid);
         else gs::HipSolver::solve(grid);
+        if (argc > 2) gs::dumpField(grid, 0, argv[2]); // Vector3::dump of the solution (added, optional)
     } catch (std::exception& e) {
         std::cerr << "Exception: " << e.what() << '\n';
     }

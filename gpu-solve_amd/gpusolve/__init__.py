@@ -171,6 +171,35 @@ class HipGridData:
     def sync(self):
         _check(driver().gs_grid_sync(self.handle))
 
+    def dump(self, path: str, level: int = 0, name: str = "v"):
+        """Vector3::dump (src/cpu/Vector3.cpp:56-78) of a field: the plotter.py input format."""
+        _check(driver().gs_grid_dump(self.handle, level, FIELDS[name], path.encode()))
+
+
+def dump_write(arr_xyz: np.ndarray, path: str):
+    """Vector3::dump text of a padded host array indexed [x][y][z] (the driver's writer)."""
+    a = np.ascontiguousarray(np.asarray(arr_xyz, dtype=np.float64).transpose(2, 1, 0))
+    px, py, pz = arr_xyz.shape
+    _check(driver().gs_dump_write(a.ctypes.data_as(_abi.dptr), px, py, pz, path.encode()))
+
+
+def read_dump(path: str) -> np.ndarray:
+    """plotter.py's readFile (reference plotter.py:10-26): a dump back into an [x][y][z] array."""
+    with open(path) as f:
+        px, py, pz = (int(t) for t in f.readline().split())
+        data = np.loadtxt(f, ndmin=2)
+    out = np.zeros((px, py, pz))
+    out[data[:, 0].astype(int), data[:, 1].astype(int), data[:, 2].astype(int)] = data[:, 3]
+    return out
+
+
+def analytic_error(mesh: np.ndarray) -> float:
+    """Max |computed - u| over the mesh, u = (x-x^2)(y-y^2)(z-z^2) on linspace(0, 1, n) per axis
+    (reference plotter.py:7-8, 28-31: the exact solution of the NONLINEAR / NEWTON problems)."""
+    g = [np.linspace(0.0, 1.0, n) for n in mesh.shape]
+    X, Y, Z = np.meshgrid(*g, indexing="ij")
+    return float(np.abs(mesh - (X - X * X) * (Y - Y * Y) * (Z - Z * Z)).max())
+
 
 class HipSolver:
     @staticmethod

@@ -101,6 +101,8 @@ DRIVER_API = {
     "gs_grid_download": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
     "gs_grid_upload": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
     "gs_grid_sync": (C.c_int, [C.c_void_p]),
+    "gs_dump_write": (C.c_int, [dptr, i64, i64, i64, C.c_char_p]),
+    "gs_grid_dump": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
     "gs_grid_time_jacobi": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "gs_grid_time_vcycles": (C.c_int, [C.c_void_p, C.c_int, dptr, dptr]),
     "gs_zslab_plan": (C.c_int, [C.POINTER(i64), C.c_int, i64, C.c_int, C.POINTER(C.c_int), C.POINTER(i64),

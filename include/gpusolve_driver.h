@@ -62,6 +62,12 @@ hipStream_t gs_grid_stream(void* grid);
 int gs_grid_download(void* grid, int level, int field, double* host);
 int gs_grid_upload(void* grid, int level, int field, const double* host);
 int gs_grid_sync(void* grid);
+/* Vector3::dump (src/cpu/Vector3.cpp:56-78) of a padded field: header "Px Py Pz" then "x y z value"
+ * per point, x outermost, z innermost, values in the iostream default format (%g). path NULL or
+ * empty (or not openable): the lines go to stdout without the header, as in the reference.
+ * gs_dump_write formats a dense host array [pz][py][px] (x fastest); gs_grid_dump downloads first. */
+int gs_dump_write(const double* host, int64_t px, int64_t py, int64_t pz, const char* path);
+int gs_grid_dump(void* grid, int level, int field, const char* path);
 
 /* Times `sweeps` level-`level` Jacobi sweeps with hipEvents on the grid's stream (after `warmup`
  * untimed sweeps); *ms = elapsed milliseconds of the timed sweeps. */

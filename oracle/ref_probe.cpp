@@ -110,6 +110,7 @@ int usage()
 {
     std::cerr << "usage:\n"
                  "  ref_probe solve <config>                      (17-digit residual history)\n"
+                 "  ref_probe solve_dump <config> out.txt out.bin (Vector3::dump of level-0 v after the solve)\n"
                  "  ref_probe levels X Y Z\n"
                  "  ref_probe rhs X Y Z mode gamma out.bin\n"
                  "  ref_probe op <name> X Y Z mode level seed outdir [omega gamma k]\n"
@@ -132,6 +133,19 @@ int main(int argc, char** argv)
         CpuGridData g(p);
         if (p.mode == GridParams::NEWTON) NewtonSolver::solve(g);
         else CpuSolver::solve(g);
+        return 0;
+    }
+    if (cmd == "solve_dump" && argc >= 5) {
+        // solve quietly, then the reference's own Vector3::dump of level-0 v (text) + raw doubles
+        GridParams p;
+        if (!read_config(argv[2], p)) { std::cerr << "bad config\n"; return 1; }
+        CpuGridData g(p);
+        std::streambuf* old = std::cout.rdbuf(nullptr);
+        if (p.mode == GridParams::NEWTON) NewtonSolver::solve(g);
+        else CpuSolver::solve(g);
+        std::cout.rdbuf(old);
+        g.getLevel(0).v.dump(argv[3]);
+        dump(g.getLevel(0).v, argv[4]);
         return 0;
     }
     if (cmd == "levels" && argc >= 5) {

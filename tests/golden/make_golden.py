@@ -13,6 +13,8 @@ Outputs (all data, no reference source):
   levels.json           level dims + h for several grid shapes
   rhs.npz               level-0 f for linear / non-linear RHS on small grids
   ops.npz               per-operator fixtures (inputs + outputs, reference layout (Px,Py,Pz))
+  dumps.json / .npz     Vector3::dump text of the level-0 solution after small solves, and the same
+                        field as doubles (src/cpu/Vector3.cpp:56-78; the plotter.py input format)
 
 Usage:  python tests/golden/make_golden.py [--large]
 """
@@ -215,15 +217,41 @@ def gen_ops(path):
         json.dump(meta, f, indent=1)
 
 
+def dump_cases():
+    return {"m0_n7_3": case(7, maxiter=3), "m1_9x5x7_3": case(9, 5, 7, mode=1, maxiter=3),
+            "m2_n7_2": case(7, mode=2, maxiter=2), "m0_n15_4": case(15, maxiter=4)}
+
+
+def gen_dumps(path):
+    texts, arrs = {}, {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, c in dump_cases().items():
+            conf, txt, binf = (os.path.join(td, n) for n in ("c.conf", "v.txt", "v.bin"))
+            with open(conf, "w") as f:
+                f.write(config_text(c))
+            subprocess.run([PROBE, "solve_dump", conf, txt, binf], check=True, capture_output=True)
+            texts[name] = {"config": c, "text": open(txt).read()}
+            arrs[name] = load_field(binf, (c["X"], c["Y"], c["Z"]))
+    with open(path, "w") as f:
+        json.dump(texts, f, indent=1)
+    np.savez_compressed(path.replace(".json", ".npz"), **arrs)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--large", action="store_true", help="also the 511^3/512^3 anchors (several minutes)")
     ap.add_argument("--only-large", action="store_true")
+    ap.add_argument("--only-dumps", action="store_true")
     a = ap.parse_args()
     for exe in (PROBE, REFEXE):
         if not os.path.exists(exe):
             sys.exit(f"{exe} missing: run `make -C oracle ref` (needs /root/reference)")
+    if a.only_dumps:
+        gen_dumps(os.path.join(HERE, "dumps.json"))
+        return
     if not a.only_large:
+        print("dumps ...", flush=True)
+        gen_dumps(os.path.join(HERE, "dumps.json"))
         print("histories ...", flush=True)
         gen_histories(small_cases(), os.path.join(HERE, "histories.json"))
         print("stdout ...", flush=True)
