@@ -465,6 +465,19 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
         auto& C = grid.getLevel(i);
         auto& F = grid.getLevel(i - 1);
         materialize(grid, i); // only if the level had no sweep at all
+        static const bool noFusedPro = std::getenv("GS_NO_FUSED_PROLONG") != nullptr;
+        if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && !(F.distributed && grid.nranks() > 1) &&
+            gs_jacobi_sweep2_prolong_supported(&grid.stencilAbi, &F.geom, (int)grid.mode)) {
+            // the first two post-smoothing sweeps of v^h + P v^2h in one pass (the corrected
+            // iterate is never stored), then the remaining ones
+            materialize(grid, i - 1);
+            check(gs_jacobi_sweep2_prolong(&grid.stencilAbi, &F.geom, (int)grid.mode, grid.omega, grid.gamma,
+                                           F.v.data(), C.v.data(), nullptr, &C.geom, F.vAlt.data(), F.f.data(), s),
+                  "gs_jacobi_sweep2_prolong");
+            F.v.swap(F.vAlt);
+            jacobi(grid, i - 1, grid.postSmoothing - 2);
+            continue;
+        }
         // v^h += P (v^2h [- restV^2h])   (CpuSolver.cpp:121-132, interpolate + v += e fused)
         check(gs_prolong_add(C.v.data(), grid.mode == GridParams::NONLINEAR ? C.restV.data() : nullptr, &C.geom,
                              F.v.data(), &F.geom, s),

@@ -285,6 +285,14 @@ __device__ __forceinline__ double lane_from_right(double src, double edge)
     }
 }
 
+// a value every lane holds identically (an LDS broadcast read), moved to SGPRs
+__device__ __forceinline__ double uniform_d(double x)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ double2 ld2(const double* __restrict__ p) { return *reinterpret_cast<const double2*>(p); }
 
 typedef double dv2 __attribute__((ext_vector_type(2)));
@@ -908,7 +916,8 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
                                                       const double* __restrict__ f, const double* __restrict__ w,
                                                       double* __restrict__ out, double* __restrict__ partials, int nx,
                                                       int ny, int nz, int64_t ldy, int64_t ldz, int ZC, int zlo,
-                                                      int zhi)
+                                                      int zhi, const double*, const double*, int, int, int, int64_t,
+                                                      int64_t)
 {
     __shared__ double red[WXMAX];
     double sumsq = 0.0; // r^2 of sweep 1's residual over the block's own points (partials != NULL)
@@ -1086,13 +1095,22 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
 // j = RY the row published to the other wave, j = RY+1 the row received from it and j = -1 the one
 // halo row of v loaded from memory. On wave 1 local j+1 is global y-1: the two y-neighbours are
 // swapped back before the stencil sum, which keeps the reference's term order.
-template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false>
+// PRO = 1 / 2: the input iterate is v + P(c) / v + P(c - sub) — the prolongation and correction of
+// the V-cycle's up-leg (CpuSolver.cpp:121-132, gs_prolong_add) fused into the first post-smoothing
+// pair, so the corrected iterate is never stored. The correction is added to every v value when it
+// is consumed (the loads stay in flight as before): X-pass values of the two coarse planes under the
+// current fine planes live in registers (W0, W1) and the next coarse plane is prefetched one step
+// ahead; the z-chunk is even, so every fine plane's parity, hence its Y/Z combination, is static.
+template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0>
 __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* __restrict__ v,
                                                            const double* __restrict__ f, const double* __restrict__ w,
                                                            double* __restrict__ out, double* __restrict__ partials,
                                                            int nx, int ny, int nz, int64_t ldy, int64_t ldz, int ZC,
-                                                           int zlo, int zhi)
+                                                           int zlo, int zhi, const double* __restrict__ pc,
+                                                           const double* __restrict__ ps, int cnx, int cny, int cnz,
+                                                           int64_t cldy, int64_t cldz)
 {
+    static_assert(PRO == 0 || (SPEC && !ZV && RY % 2 == 0), "fused prolongation: per-wave code, even RY");
     constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
     constexpr int NE = NV + RY; // x-edge values per wave side: v rows 0..RY, sweep-1 rows 1..RY
     __shared__ double red[2 * WXMAX];
@@ -1151,6 +1169,76 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         Vp[j] = ldv2<ZV>(at(v, j, zb - 2));
         Vc[j] = ldv2<ZV>(at(v, j, zb - 1));
     }
+    // ---- fused prolongation (PRO): coarse rows cyb .. cyb+NCR-1 lie under the wave's fine rows ----
+    constexpr int NCR = RY / 2 + 2;
+    const int cxl = min(x >> 1, max(cnx, 0)); // the lane's coarse column (fine pair x odd, x+1 even)
+    const int cyb = mir ? ((y0 - 1) >> 1) + RY / 2 : ((y0 - 1) >> 1) - 1;
+    int64_t crow[NCR];
+#pragma unroll
+    for (int r = 0; r < NCR; r++) crow[r] = (int64_t)min(max(cyb + r, 0), cny + 1) * cldy;
+    double2 W0[NCR], W1[NCR];        // X-pass values of coarse planes K, K+1
+    double RA[NCR], RB[NCR], SA[NCR], SB[NCR]; // raw c (and sub) of plane K+2, in flight
+    auto craw = [&](int cz) {
+        const int64_t zo = (int64_t)min(max(cz, 0), cnz + 1) * cldz + cxl;
+#pragma unroll
+        for (int r = 0; r < NCR; r++) {
+            RA[r] = pc[zo + crow[r]];
+            RB[r] = pc[zo + crow[r] + 1];
+            if (PRO == 2) {
+                SA[r] = ps[zo + crow[r]];
+                SB[r] = ps[zo + crow[r] + 1];
+            }
+        }
+    };
+    // X pass of gs_prolong_add: e(x odd) = 0.5 a + 0.5 b, e(x+1 even) = b, a / b = c(cx) / c(cx+1)
+    auto xpass = [&](double2 (&X)[NCR]) {
+#pragma unroll
+        for (int r = 0; r < NCR; r++) {
+            const double a = PRO == 2 ? RA[r] - SA[r] : RA[r], b = PRO == 2 ? RB[r] - SB[r] : RB[r];
+            X[r] = make_double2(0.5 * a + 0.5 * b, b);
+        }
+    };
+    // the correction of local row j on a plane whose coarse neighbours are Wa (and Wb when the fine
+    // plane is odd), Y pass then Z pass; added where the fine point is interior
+    auto correct = [&](double2& val, int j, bool zodd, bool zin, const double2 (&Wa)[NCR], const double2 (&Wb)[NCR],
+                       auto mirc) {
+        constexpr bool M = decltype(mirc)::get();
+        const int u = M ? 2 * RY + 1 - j : j + 2; // fine row = 2 (coarse base) + u
+        const int ri = M ? (u >> 1) - RY / 2 : (u >> 1);
+        const bool yodd = u & 1;
+        auto ypass = [&](const double2 (&X)[NCR]) {
+            if (!yodd) return X[ri];
+            return make_double2(0.5 * X[ri].x + 0.5 * X[ri + 1].x, 0.5 * X[ri].y + 0.5 * X[ri + 1].y);
+        };
+        double2 e = ypass(Wa);
+        if (zodd) {
+            const double2 g = ypass(Wb);
+            e = make_double2(0.5 * e.x + 0.5 * g.x, 0.5 * e.y + 0.5 * g.y);
+        }
+        if (zin && rowc[j + 1]) {
+            if (okx0) val.x = val.x + e.x;
+            if (okx1) val.y = val.y + e.y;
+        }
+    };
+    if (PRO) {
+        const int m0 = (zb - 1) >> 1; // zb is odd: planes zb-2 = 2 m0 - 1, zb - 1 = 2 m0
+        double2 Wm[NCR];
+        craw(m0 - 1);
+        xpass(Wm);
+        craw(m0);
+        xpass(W0);
+        craw(m0 + 1);
+        xpass(W1);
+        auto pro_init = [&](auto mirc) {
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                correct(Vp[j], j, true, zb - 2 >= 1, Wm, W0, mirc);
+                correct(Vc[j], j, false, zb - 1 >= 1, W0, W0, mirc);
+            }
+        };
+        if (mir) pro_init(BoolC<true>{});
+        else pro_init(BoolC<false>{});
+    }
     load_slot(1, zb - 1, zb);
     double sumsq = 0.0;
     for (int z0 = zb - 1; z0 <= ze + 1; z0 += 2) {
@@ -1159,6 +1247,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             const int z = z0 + ph;
             const int cs = ph ^ 1;
             load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
+            if (PRO && ph == 0) craw((z >> 1) + 2); // consumed at the end of the next step
             // ---- publish: x-edge columns (v(z) rows 0..RY, sweep-1(z-1) rows 1..RY) and the y-edge row
             if (lane == 0) {
 #pragma unroll
@@ -1179,9 +1268,9 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             __builtin_amdgcn_s_barrier();
             double CL[NE], CR[NE];
 #pragma unroll
-            for (int i = 0; i < NE; i++) {
-                CL[i] = edge[ph][wy][wx][1][i];
-                CR[i] = edge[ph][wy][wx + 2][0][i];
+            for (int i = 0; i < NE; i++) { // wave-uniform: kept in SGPRs
+                CL[i] = uniform_d(edge[ph][wy][wx][1][i]);
+                CR[i] = uniform_d(edge[ph][wy][wx + 2][0][i]);
             }
             const double2 vY = yrow[ph][wy ^ 1][wx][0][lane]; // v(z) at local row RY+1
             const double2 sY = yrow[ph][wy ^ 1][wx][1][lane]; // sweep-1(z-1) at local row RY+1
@@ -1192,6 +1281,14 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             const bool pz = planeok(z);
             auto sweeps = [&](auto mirc) {
                 const bool M = mirc.get();
+                if constexpr (PRO != 0) {
+                    // the corrected iterate: plane z+1 (VL) and the halo row at plane z (HL); with z0
+                    // even, ph 0 has z even (z+1 odd: coarse K, K+1) and ph 1 has z odd
+#pragma unroll
+                    for (int j = 0; j < NV; j++)
+                        correct(VL[cs][j], j, ph == 0, z + 1 <= nz, ph == 0 ? W0 : W1, W1, mirc);
+                    correct(HL[cs], -1, ph == 1, z >= 1 && z <= nz, W0, W1, mirc);
+                }
                 // sweep 1 at plane z, local rows 0..RY
 #pragma unroll
                 for (int j = 0; j < NV; j++) {
@@ -1244,9 +1341,12 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                     }
                 }
             };
-            if (!SPEC) sweeps(RtBool{mir});
-            else if (mir) sweeps(BoolC<true>{});
-            else sweeps(BoolC<false>{});
+            if constexpr (!SPEC) {
+                sweeps(RtBool{mir});
+            } else {
+                if (mir) sweeps(BoolC<true>{});
+                else sweeps(BoolC<false>{});
+            }
             // ---- rotate ----
 #pragma unroll
             for (int j = 1; j <= RY; j++) {
@@ -1259,6 +1359,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                 V1c[j] = V1n[j];
                 Vp[j] = Vc[j];
                 Vc[j] = VL[cs][j];
+            }
+            if (PRO && ph == 1) { // next step: coarse planes K+1, K+2
+#pragma unroll
+                for (int r = 0; r < NCR; r++) W0[r] = W1[r];
+                xpass(W1);
             }
         }
     }
@@ -1299,6 +1404,7 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
     const int fills = tiles * ((L->nz + 3) / 4) >= 512 ? 2 : 1;
     int64_t c = tiles * L->nz / 1024;
     c = c < 4 ? 4 : (c > 64 ? 64 : c);
+    c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)
     *zc = (int)c;
     *grid = dim3((unsigned)tiles, (unsigned)((L->nz + c - 1) / c));
     *block = dim3(WAVE, (unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), two ? 2 : 1);
@@ -1545,8 +1651,8 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
-#define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
-#define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, M != GS_NEWTON>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0)
+#define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, M != GS_NEWTON>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
     const bool zv = !v_in;
     if (y2) {
         if (mode == GS_LINEAR) {
@@ -1565,6 +1671,36 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     }
 #undef GS_TBY
 #undef GS_TB
+    return launch_status();
+}
+
+int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, int mode)
+{
+    int zc;
+    dim3 g, b;
+    bool y2 = false;
+    // LINEAR only: the NONLINEAR (FAS) variant carries the coarse restV too and exceeds the register
+    // budget of two waves per SIMD; NEWTON runs the per-use-select code (no per-wave copies)
+    return !bad_level(L) && valid_stencil(S) && mode == GS_LINEAR && L->z0 == 0 &&
+           tb2_plan(S, L, &zc, &g, &b, &y2, mode) && y2;
+}
+
+int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                             const double* v_in, const double* coarse_v, const double* coarse_sub, const gs_level* cl,
+                             double* v_out, const double* f, hipStream_t st)
+{
+    int zc;
+    dim3 g, b;
+    bool y2 = false;
+    if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || bad_level(cl) || cl->z0 != 0 || !v_in || !coarse_v ||
+        !v_out || !f || v_in == v_out || (mode == GS_NONLINEAR) != (coarse_sub != nullptr) ||
+        (L->nx + 1) / 2 > cl->nx + 1 || (L->ny + 1) / 2 > cl->ny + 1 || (L->nz + 1) / 2 > cl->nz + 1 ||
+        !tb2_plan(S, L, &zc, &g, &b, &y2, mode))
+        return GS_EINVAL;
+    const Coef k = make_coef(S, L, omega, gamma);
+#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, false, true, P>), g, b, 0, st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, 0, 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz)
+    GS_TBP(GS_LINEAR, 1);
+#undef GS_TBP
     return launch_status();
 }
 
@@ -1742,7 +1878,7 @@ struct PairVariant {
     const char* name;
     int ry, wxmax, wy;
     void (*kern)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
-                 int64_t, int, int, int);
+                 int64_t, int, int, int, const double*, const double*, int, int, int, int64_t, int64_t);
 };
 #define GS_PV(RY, WX) {"tb2 ry" #RY " wx" #WX, RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true>}
 #define GS_PVF(RY, WX) {"tb2 ry" #RY " wx" #WX " f-cached", RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true, false>}
@@ -1783,7 +1919,7 @@ int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, d
     const Coef k = make_coef(S, L, omega, 0.0);
     hipLaunchKernelGGL(V.kern, dim3((unsigned)tiles, (unsigned)((L->nz + zc - 1) / zc)), dim3(WAVE, (unsigned)wx, V.wy), 0,
                        st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc,
-                       0, 0);
+                       0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0);
     return launch_status();
 }
 
