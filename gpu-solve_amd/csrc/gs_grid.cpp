@@ -136,6 +136,19 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         L.fusedPairs = !noPairs && gs_jacobi_sweep2_supported(&stencilAbi, &L.geom) == 2 &&
                        (!L.distributed || L.minPlanes >= 2);
     }
+    // The coarse end of the V-cycle runs as one gs_coarse_cycle launch from the first level of at
+    // most GS_COARSE_POINTS points (default 4096 = 16^3: below that each operator is launch latency,
+    // above it one workgroup is slower than the whole chip) that is not Z-slab partitioned; 0 = off.
+    coarseFrom = levels_.size();
+    {
+        const char* e = std::getenv("GS_COARSE_POINTS");
+        const int64_t thr = e ? std::atoll(e) : 4096;
+        if (thr > 0 && preSmoothing + postSmoothing < (1u << 20))
+            for (int l = nlev - 1; l >= 1; l--) {
+                if (levels_[l].distributed || pts[l] > thr || nlev - l > gs_coarse_cycle_max_levels()) break;
+                coarseFrom = (std::size_t)l;
+            }
+    }
     if (mode == NEWTON) newtonF = DeviceField(levels_[0].geom.nx, levels_[0].geom.ny, levels_[0].geom.nz, s);
     // the overlapped sweep splits a level into 3 launches, each with its own partials region
     maxParts = 2 * maxParts + 4096;
@@ -379,6 +392,31 @@ void HipSolver::materialize(HipGridData& grid, std::size_t l)
     L.vZero = false;
 }
 
+// CpuSolver.cpp:92-135 below level `from` in one launch (gs_coarse_cycle): the caller has set
+// f^from (and, FAS, restV / v); on return every level from..nl-1 holds its post-smoothed iterate.
+void HipSolver::coarseCycle(HipGridData& grid, std::size_t from)
+{
+    const std::size_t nl = grid.numLevels();
+    gs_coarse_level lv[16] = {};
+    const int n = (int)(nl - from);
+    if (n < 1 || n > 16) throw Error("coarseCycle: bad level range");
+    for (int j = 0; j < n; j++) {
+        auto& L = grid.getLevel(from + j);
+        lv[j] = gs_coarse_level{L.v.data(), L.vAlt.data(), L.f.data(), L.r ? L.r.data() : nullptr,
+                                L.restV ? L.restV.data() : nullptr, L.newtonV ? L.newtonV.data() : nullptr,
+                                L.geom, j == 0 ? (L.vZero ? 1 : 0) : (grid.mode != GridParams::NONLINEAR ? 1 : 0)};
+    }
+    check(gs_coarse_cycle(&grid.stencilAbi, lv, n, (int)grid.mode, grid.omega, grid.gamma, (int)grid.preSmoothing,
+                          (int)grid.postSmoothing, grid.stream()),
+          "gs_coarse_cycle");
+    const bool odd = ((grid.preSmoothing + grid.postSmoothing) & 1) != 0; // every level swept pre+post times
+    for (int j = 0; j < n; j++) {
+        auto& L = grid.getLevel(from + j);
+        if (odd) L.v.swap(L.vAlt);
+        L.vZero = false;
+    }
+}
+
 // The first pre-smoothing step of the next cycle, run into vAlt (v untouched) with the norm of the
 // residual of v: a fused pair when level 0 smooths in pairs and pre-smoothing has two sweeps, else
 // one sweep. *sweeps = how many sweeps vAlt holds.
@@ -426,7 +464,9 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
 {
     const std::size_t nl = grid.numLevels();
     const hipStream_t s = grid.stream();
-    for (std::size_t i = 0; i + 1 < nl; i++) {
+    // levels lc.. run as one gs_coarse_cycle launch (lc == nl: none); the host loops descend to lc
+    const std::size_t lc = grid.coarseFrom, last = std::min(lc, nl - 1);
+    for (std::size_t i = 0; i < last; i++) {
         std::size_t pre = grid.preSmoothing;
         if (i == 0 && pending && *pending > 0 && pre >= (std::size_t)*pending) {
             grid.getLevel(0).v.swap(grid.getLevel(0).vAlt); // adopt the speculative first sweep(s)
@@ -460,8 +500,9 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
             grid.halo(C, C.f, s);
         }
     }
-    jacobi(grid, nl - 1, grid.preSmoothing + grid.postSmoothing); // coarsest "solve"
-    for (std::size_t i = nl - 1; i > 0; i--) {
+    if (lc < nl) coarseCycle(grid, lc);
+    else jacobi(grid, nl - 1, grid.preSmoothing + grid.postSmoothing); // coarsest "solve"
+    for (std::size_t i = last; i > 0; i--) {
         auto& C = grid.getLevel(i);
         auto& F = grid.getLevel(i - 1);
         materialize(grid, i); // only if the level had no sweep at all

@@ -92,6 +92,9 @@ public:
     int rank() const { return comm_ ? comm_->rank() : 0; }
     int nranks() const { return comm_ ? comm_->size() : 1; }
     bool overlapHalo = true; // boundary planes first, halo on the comm stream beside the interior
+    // levels coarseFrom .. numLevels()-1 run as ONE gs_coarse_cycle launch in every V-cycle
+    // (numLevels(): none); set from GS_COARSE_POINTS at construction
+    std::size_t coarseFrom = 0;
 
     // residual-norm plumbing: per-block partials, device scalars, pinned host scalar
     double* partials() const { return partials_; }
@@ -139,6 +142,8 @@ public:
     static bool speculationEnabled(const HipGridData& grid);
     static void jacobi(HipGridData& grid, std::size_t level, std::size_t sweeps);
     static void materialize(HipGridData& grid, std::size_t level); // store a pending v = 0
+    // the V-cycle below level `from` (its f set) in one gs_coarse_cycle launch
+    static void coarseCycle(HipGridData& grid, std::size_t from);
     static double finishNorm(HipGridData& grid, int64_t nparts);
 
     // solve() records its residual history here when non-null (initial, then one per V-cycle)

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gpusolve_hip.h"
 
@@ -605,6 +606,7 @@ __global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so,
     constexpr int RR_VP = RR_VY * RR_VX, RR_RP = RR_FY * RR_FX;
     __shared__ double lds[4 * RR_VP + 3 * RR_RP];
     const int tid = threadIdx.x;
+    // (an XCD-aware tile order, as k_tb2y uses, measured 3% slower here: tools/ab_session.sh)
     const int X0 = 1 + blockIdx.x * RR_TXC, Y0 = 1 + blockIdx.y * RR_TYC;
     const int Zb = 1 + blockIdx.z * ZC, Ze = min(Zb + ZC - 1, cnz);
     if (Zb > Ze) return;
@@ -884,6 +886,169 @@ __global__ __launch_bounds__(256) void k_axpy(double* __restrict__ y, const doub
         if (a == 1.0) y[i] = y[i] + x[i];
         else if (a == -1.0) y[i] = y[i] - x[i];
         else y[i] = y[i] + a * x[i];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The coarse end of the V-cycle in ONE launch of ONE workgroup (gs_coarse_cycle). A level of a few
+// thousand points is pure launch latency per operator on a chip it cannot fill (~4.5 us a sweep);
+// here the whole recursion of CpuSolver::vcycle below level lv[0] (CpuSolver.cpp:92-135) runs in one
+// 1024-thread workgroup whose levels stay in L2, with a workgroup barrier between operators instead
+// of a kernel boundary (the waves of a workgroup share one CU's L1, so the barrier's workgroup-scope
+// fences order every store before the next operator's loads). Each point is computed by the
+// expression of the per-operator kernel it replaces (k_generic KIND 0 / 1 / 2, k_restrict,
+// k_prolong_add), so every field is bit-identical to the per-operator launch sequence.
+constexpr int CC_T = 1024, CC_MAXLEV = 8;
+
+struct CcLevel {
+    double *v, *va, *f, *r, *rv, *w; // iterate, ping-pong partner, rhs, residual, restV (FAS), newtonV
+    int64_t ldy, ldz;
+    int nx, ny, nz, vz; // vz: the iterate is the zero iterate, not stored
+    Coef k;
+};
+struct CcPlan {
+    CcLevel L[CC_MAXLEV];
+    int n, pre, post;
+};
+
+// every interior point of a level, x fastest, strided over the workgroup
+template <class F>
+__device__ __forceinline__ void cc_points(const CcLevel& L, F&& fn)
+{
+    const int n = L.nx * L.ny * L.nz;
+    for (int i = threadIdx.x; i < n; i += CC_T) {
+        const int t = i / L.nx, z = t / L.ny;
+        fn(1 + i - t * L.nx, 1 + t - z * L.ny, 1 + z);
+    }
+}
+
+__device__ __forceinline__ int64_t cc_at(const CcLevel& L, int x, int y, int z)
+{
+    return x + y * L.ldy + (int64_t)z * L.ldz;
+}
+
+// A(u) at p in config order (k_generic): the stencil sum, / h^2, the non-linear term; c = u(p),
+// wv = w(p) (NEWTON). uz: u is the zero iterate (literal zeros, as k_generic's v == NULL).
+template <int MODE>
+__device__ __forceinline__ double cc_op(const Coef& k, const double* __restrict__ u, bool uz,
+                                        const double* __restrict__ w, int64_t p, double& c, double& wv)
+{
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) s += k.s[i] * (uz ? 0.0 : u[p + k.off[i]]);
+    s = div_hh(k, s);
+    c = uz ? 0.0 : u[p];
+    wv = (MODE == GS_NEWTON) ? w[p] : 0.0;
+    if (MODE == GS_NEWTON) {
+        const double ew = exp(wv);
+        s += k.gamma * (1 + wv) * c * ew;
+    } else if (MODE == GS_NONLINEAR) {
+        const double ev = exp(c);
+        const double nl = k.gamma * c * ev;
+        s += nl;
+    }
+    return s;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
+{
+    unsigned alt = 0, zero = 0; // per level bit: the iterate is in va / is the unstored zero
+    for (int l = 0; l < P.n; l++)
+        if (P.L[l].vz) zero |= 1u << l;
+    auto cur = [&](int l) { return ((alt >> l) & 1) ? P.L[l].va : P.L[l].v; };
+    // v = 0 made real (HipSolver::materialize)
+    auto materialize = [&](int l) {
+        if (!((zero >> l) & 1)) return;
+        const CcLevel& L = P.L[l];
+        double* v = cur(l);
+        cc_points(L, [&](int x, int y, int z) { v[cc_at(L, x, y, z)] = 0.0; });
+        __syncthreads();
+        zero &= ~(1u << l);
+    };
+    // `sweeps` Jacobi sweeps, residual and update fused (k_generic KIND 0), ping-pong v <-> va
+    auto smooth = [&](int l, int sweeps) {
+        const CcLevel& L = P.L[l];
+        if (sweeps == 0) materialize(l);
+        for (int s = 0; s < sweeps; s++) {
+            const bool uz = (zero >> l) & 1;
+            const double* in = cur(l);
+            double* out = ((alt >> l) & 1) ? L.v : L.va;
+            cc_points(L, [&](int x, int y, int z) {
+                const int64_t p = cc_at(L, x, y, z);
+                double c, wv;
+                const double a = cc_op<MODE>(L.k, in, uz, L.w, p, c, wv);
+                const double r = L.f[p] - a;
+                out[p] = jacobi_update<MODE>(L.k, c, r, wv);
+            });
+            __syncthreads();
+            alt ^= 1u << l;
+            zero &= ~(1u << l);
+        }
+    };
+    // coarse interior of C <- 27-point full weighting of the fine field src of F (k_restrict)
+    auto restrict_to = [&](const double* __restrict__ src, const CcLevel& F, double* ca, double* cb,
+                           const CcLevel& C) {
+        cc_points(C, [&](int x, int y, int z) {
+            const double* c0 = src + 2 * x + (int64_t)(2 * y) * F.ldy + (int64_t)(2 * z) * F.ldz;
+            double acc = 0.0;
+#pragma unroll
+            for (int a = -1; a <= 1; a++)
+#pragma unroll
+                for (int b = -1; b <= 1; b++)
+#pragma unroll
+                    for (int c = -1; c <= 1; c++) {
+                        const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
+                                           ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                        acc += wgt * c0[a + b * F.ldy + c * F.ldz];
+                    }
+            const int64_t q = cc_at(C, x, y, z);
+            ca[q] = acc;
+            if (cb) cb[q] = acc;
+        });
+    };
+
+    // ---- down: pre-smoothing, f^2h = R(f - A v) [FAS: restV = v^2h = R v, f^2h += A(restV)] ----
+    for (int l = 0; l + 1 < P.n; l++) {
+        const CcLevel &F = P.L[l], &C = P.L[l + 1];
+        smooth(l, P.pre);
+        const double* u = cur(l);
+        cc_points(F, [&](int x, int y, int z) { // residual (k_generic KIND 1)
+            const int64_t p = cc_at(F, x, y, z);
+            double c, wv;
+            const double a = cc_op<MODE>(F.k, u, false, F.w, p, c, wv);
+            F.r[p] = F.f[p] - a;
+        });
+        __syncthreads();
+        restrict_to(F.r, F, C.f, nullptr, C);
+        if (MODE == GS_NONLINEAR) restrict_to(u, F, C.rv, cur(l + 1), C);
+        __syncthreads();
+        if (MODE == GS_NONLINEAR) { // f += A(restV)  (k_generic KIND 2, ADD)
+            cc_points(C, [&](int x, int y, int z) {
+                const int64_t p = cc_at(C, x, y, z);
+                double c, wv;
+                const double a = cc_op<GS_NONLINEAR>(C.k, C.rv, false, nullptr, p, c, wv);
+                C.f[p] = C.f[p] + a;
+            });
+            __syncthreads();
+        }
+    }
+    // ---- the coarsest level: pre + post sweeps (CpuSolver.cpp:117) ----
+    smooth(P.n - 1, P.pre + P.post);
+    // ---- up: v^h += P(v^2h [- restV^2h]) (k_prolong_add), post-smoothing ----
+    for (int l = P.n - 1; l > 0; l--) {
+        const CcLevel &C = P.L[l], &F = P.L[l - 1];
+        materialize(l);
+        const double* cv = cur(l);
+        double* fv = cur(l - 1);
+        cc_points(F, [&](int x, int y, int z) {
+            const int64_t p = cc_at(F, x, y, z);
+            const double e = MODE == GS_NONLINEAR ? prolong_value<true>(cv, C.rv, x, y, z, C.ldy, C.ldz, 0)
+                                                  : prolong_value<false>(cv, nullptr, x, y, z, C.ldy, C.ldz, 0);
+            fv[p] = fv[p] + e;
+        });
+        __syncthreads();
+        smooth(l - 1, P.post);
     }
 }
 
@@ -1838,6 +2003,51 @@ int gs_axpy(double* y, const double* x, double a, int64_t n, hipStream_t st)
     return launch_status();
 }
 
+int gs_coarse_cycle_max_levels(void) { return CC_MAXLEV; }
+
+int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int mode, double omega, double gamma,
+                    int pre, int post, hipStream_t st)
+{
+    if (!S || !valid_stencil(S) || !lv || n < 1 || n > CC_MAXLEV || mode < GS_LINEAR || mode > GS_NEWTON ||
+        pre < 0 || post < 0)
+        return GS_EINVAL;
+    CcPlan P{};
+    P.n = n;
+    P.pre = pre;
+    P.post = post;
+    for (int l = 0; l < n; l++) {
+        const gs_coarse_level& a = lv[l];
+        const gs_level* g = &a.geom;
+        if (bad_level(g) || g->z0 != 0 || g->nx < 1 || g->ny < 1 || g->nz < 1 ||
+            g->nx * g->ny * g->nz > (int64_t)INT32_MAX || !a.v || !a.v_alt || a.v == a.v_alt || !a.f ||
+            (l + 1 < n && !a.r) || (mode == GS_NEWTON && !a.newton_v) ||
+            (mode == GS_NONLINEAR && ((l > 0 && !a.rest_v) || a.v_zero)))
+            return GS_EINVAL;
+        if (l > 0) { // consecutive levels of one hierarchy (the restriction / prolongation bounds)
+            const gs_level* fg = &lv[l - 1].geom;
+            if (g->nx != fg->nx / 2 || g->ny != fg->ny / 2 || g->nz != fg->nz / 2) return GS_EINVAL;
+        }
+        CcLevel& L = P.L[l];
+        L.v = a.v;
+        L.va = a.v_alt;
+        L.f = a.f;
+        L.r = a.r;
+        L.rv = a.rest_v;
+        L.w = a.newton_v;
+        L.ldy = g->ldy;
+        L.ldz = g->ldz;
+        L.nx = (int)g->nx;
+        L.ny = (int)g->ny;
+        L.nz = (int)g->nz;
+        L.vz = a.v_zero != 0;
+        L.k = make_coef(S, g, omega, gamma);
+    }
+    if (mode == GS_LINEAR) hipLaunchKernelGGL(k_coarse_cycle<GS_LINEAR>, dim3(1), dim3(CC_T), 0, st, P);
+    else if (mode == GS_NONLINEAR) hipLaunchKernelGGL(k_coarse_cycle<GS_NONLINEAR>, dim3(1), dim3(CC_T), 0, st, P);
+    else hipLaunchKernelGGL(k_coarse_cycle<GS_NEWTON>, dim3(1), dim3(CC_T), 0, st, P);
+    return launch_status();
+}
+
 const char* gs_strerror(int code)
 {
     if (code == 0) return "success";
@@ -1847,8 +2057,9 @@ const char* gs_strerror(int code)
 
 const char* gs_build_info(void)
 {
-    return "gpusolve_hip v5: pairs k_tb2y(4x2 waves, 2 rows/wave, zc<=64) / k_tb2 (rows > 512), sweeps "
-           "k_rb(ry2 w4 zc<=32 dpp nt), 1-pt/thread small levels; fp-contract=off";
+    return "gpusolve_hip v6: pairs k_tb2y(4x2 waves, 2 rows/wave, zc<=64; +prolong) / k_tb2 (rows > 512), sweeps "
+           "k_rb(ry2 w4 zc<=32 dpp nt), fused residual+restriction, 1-pt/thread small levels, "
+           "one-workgroup coarse cycle; fp-contract=off";
 }
 
 int gs_debug_num_variants(void) { return kNumVariants; }

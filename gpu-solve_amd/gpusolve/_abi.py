@@ -28,6 +28,11 @@ class gs_level(C.Structure):
     _fields_ = [("nx", i64), ("ny", i64), ("nz", i64), ("ldy", i64), ("ldz", i64), ("z0", i64), ("h", C.c_double)]
 
 
+class gs_coarse_level(C.Structure):
+    _fields_ = [("v", C.c_void_p), ("v_alt", C.c_void_p), ("f", C.c_void_p), ("r", C.c_void_p),
+                ("rest_v", C.c_void_p), ("newton_v", C.c_void_p), ("geom", gs_level), ("v_zero", C.c_int)]
+
+
 class gs_params(C.Structure):
     _fields_ = [("maxiter", i64), ("tol", C.c_double), ("dims", i64 * 3), ("mode", C.c_int), ("pre", i64),
                 ("post", i64), ("omega", C.c_double), ("gamma", C.c_double), ("stencil", gs_stencil)]
@@ -73,6 +78,9 @@ KERNEL_API = {
     "gs_newton_F": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
                               C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_axpy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_double, i64, C.c_void_p]),
+    "gs_coarse_cycle_max_levels": (C.c_int, []),
+    "gs_coarse_cycle": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_coarse_level), C.c_int, C.c_int, C.c_double,
+                                  C.c_double, C.c_int, C.c_int, C.c_void_p]),
     "gs_strerror": (C.c_char_p, [C.c_int]),
     "gs_debug_num_variants": (C.c_int, []),
     "gs_debug_variant_name": (C.c_char_p, [C.c_int]),

@@ -18,6 +18,7 @@
  *   gs_apply_op_add      applyStencil then f += r (FAS)        src/cpu/CpuSolver.cpp:110-112
  *   gs_newton_F          NewtonSolver::compF                   src/cpu/NewtonSolver.cpp:48-81
  *   gs_axpy              Vector3::operator+= / -=              src/cpu/Vector3.cpp:34-53
+ *   gs_coarse_cycle      CpuSolver::vcycle below a level (one launch) src/cpu/CpuSolver.cpp:92-135
  *
  * Conventions
  *  - fp64 everywhere. A field of level (nx,ny,nz) is padded to (nx+2, ny+2, nz+2); element
@@ -161,6 +162,30 @@ int gs_newton_F(const gs_stencil* S, const gs_level* L, double gamma, const doub
 
 /* y[i] += a*x[i] for i < n (a = +-1 is exact: the reference's Vector3 += / -=). */
 int gs_axpy(double* y, const double* x, double a, int64_t n, hipStream_t stream);
+
+/* The coarse end of the V-cycle in ONE launch of one workgroup (its levels stay in L2): lv[0..n)
+ * are consecutive levels of the hierarchy, lv[0] the finest of them, whose f (and, NONLINEAR,
+ * rest_v and v) the caller has already set. Runs CpuSolver::vcycle's recursion below that point
+ * (src/cpu/CpuSolver.cpp:92-135: pre-smoothing, residual, full weighting, [FAS restV = v = R v,
+ * f += A(restV)], the coarsest level's pre+post sweeps, then prolongation + correction and
+ * post-smoothing back up to lv[0]) with the per-point expressions of the launchers above, so every
+ * field is bit-identical to launching them one by one. Jacobi ping-pongs between v and v_alt: on
+ * return every level's iterate is in v if pre+post is even, else in v_alt. v_zero: the level's
+ * iterate is the zero iterate and v is not read. n <= gs_coarse_cycle_max_levels(); levels
+ * unpartitioned (z0 = 0), each exactly half the previous one per axis (integer division); r is
+ * needed on all but the last level, rest_v (NONLINEAR) on all but the first, newton_v (NEWTON) on
+ * all. */
+typedef struct {
+    double *v, *v_alt, *f;
+    double* r;        /* residual scratch */
+    double* rest_v;   /* NONLINEAR: restricted iterate; else NULL */
+    double* newton_v; /* NEWTON: the linearisation point; else NULL */
+    gs_level geom;
+    int v_zero;
+} gs_coarse_level;
+int gs_coarse_cycle_max_levels(void);
+int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int mode, double omega, double gamma,
+                    int pre, int post, hipStream_t stream);
 
 const char* gs_strerror(int code);
 

@@ -40,6 +40,11 @@ def main():
             assert kl.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, v.ptr, v2.ptr, f.ptr, None, st) == 0
         for i in filter(None, a.pair_variants.split(",")):
             assert kl.gs_debug_pair_variant(int(i), C.byref(S), C.byref(L), 0.8, v.ptr, v2.ptr, f.ptr, a.zc, st) == 0
+        if "rr" in a.which.split(","):
+            c = DevField(n // 2, n // 2, n // 2)
+            Lc = c.level(2.0 / (n + 1))
+            assert kl.gs_residual_restrict(C.byref(S), C.byref(L), 0, 1.0, v.ptr, f.ptr, None, c.ptr, None,
+                                           C.byref(Lc), st) == 0
         if "residual" in a.which:
             assert kl.gs_residual(C.byref(S), C.byref(L), 0, 1.0, v.ptr, f.ptr, None, r.ptr, None, st) == 0
     torch.cuda.synchronize()
