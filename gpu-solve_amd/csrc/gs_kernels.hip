@@ -739,6 +739,210 @@ __global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so,
 }
 
 // ---------------------------------------------------------------------------------------------
+// Residual + full weighting in registers ("rr2": canonical stencil order, LINEAR / NONLINEAR,
+// unpartitioned levels of rows <= 1024 points). A block is the whole row of coarse columns of ONE
+// coarse row Y (WX waves of 64 lanes; lane = coarse column X, its fine pair x = 2X-1, 2X one dwordx4)
+// and marches a chunk of coarse planes. Per coarse plane Z it evaluates the residual on fine planes 2Z
+// and 2Z+1 (2Z-1 is kept from the previous plane) for the three fine rows 2Y-1 .. 2Y+1 the 27-point sum
+// reads (row 2Y+1 is also the next row's first: recomputed there, its loads hit L2) the way k_rb's
+// residual pass does: x-neighbours by DPP lane shifts with the wave-edge columns exchanged through LDS
+// (zero beyond the level's x-boundaries, which hold v = 0), y-neighbours from the lane's own rows plus
+// two halo rows, z-neighbours from the register window. r at the next coarse column's first fine
+// column (2X+1) is one more DPP shift (the right wave's lane 0 through LDS). The 27 terms are summed in
+// the reference's order (CpuSolver.cpp:225-231): 16 B of compulsory HBM reads per fine point (v, f)
+// plus 1 B of coarse writes, the residual never stored, and no LDS staging of the operands (the
+// LDS-tiled k_resrestrict, kept for the other cases, is latency-bound at 2 blocks per CU). The loads of
+// the next coarse plane are in flight while the current one is computed (two-slot ring, as in k_rb);
+// blocks go in XCD-aware order, y fastest, so the neighbouring rows that share 3 of a block's 5 v rows
+// run on the same XCD at the same time.
+constexpr int RR2_WXMAX = 8;
+
+template <int MODE>
+__global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* __restrict__ v,
+                                                         const double* __restrict__ f, double* __restrict__ ca,
+                                                         double* __restrict__ cb, int fnx, int fny, int fnz,
+                                                         int64_t fldy, int64_t fldz, int cnx, int cnz, int64_t cldy,
+                                                         int64_t cldz, int ZC)
+{
+    static_assert(MODE != GS_NEWTON, "NEWTON runs k_resrestrict (newtonV would exceed the register budget)");
+    // wave-edge columns [parity][1 + wave][side][plane * 3 + row] of v, and r at each wave's first fine
+    // column [parity][1 + wave][plane * 3 + row]; slots 0 and WX+1 are the zero x-boundary
+    __shared__ double ve[2][RR2_WXMAX + 2][2][6];
+    __shared__ double re[2][RR2_WXMAX + 2][6];
+    const int lane = threadIdx.x;
+    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int WX = blockDim.y;
+    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 2 * 6; i += WAVE * WX) (&ve[0][0][0][0])[i] = 0.0;
+    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 6; i += WAVE * WX) (&re[0][0][0])[i] = 0.0;
+    __syncthreads();
+    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+    const int Y = 1 + (int)(tile % gridDim.x);
+    const int Zb = 1 + (int)(tile / gridDim.x) * ZC, Ze = min(Zb + ZC - 1, cnz);
+    const int X = 1 + wx * WAVE + lane;
+    const int x = 2 * X - 1, xl = min(x, fnx + 1);
+    const bool okx0 = x <= fnx, okx1 = x + 1 <= fnx;
+    int64_t roff[5]; // fine rows 2Y-2 .. 2Y+2 (computed: 1..3)
+    bool rowc[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const int y = 2 * Y - 2 + j;
+        roff[j] = (int64_t)min(max(y, 0), fny + 1) * fldy;
+        rowc[j] = y >= 1 && y <= fny;
+    }
+    auto at = [&](const double* b, int j, int p) {
+        return b + xl + roff[j] + (int64_t)min(max(p, 0), fnz + 1) * fldz;
+    };
+    // one step's operands: v planes 2Z+1 (A), 2Z+2 (B) of rows 1..3; halo rows 0 / 4 of planes 2Z (H0)
+    // and 2Z+1 (H1); f of planes 2Z (F0), 2Z+1 (F1) rows 1..3
+    double2 VA[2][3], VB[2][3], H0[2][2], H1[2][2], F0[2][3], F1[2][3];
+    auto load_slot = [&](const int s, const int Z) {
+        const int p = 2 * Z;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            VA[s][j] = ld2(at(v, j + 1, p + 1));
+            VB[s][j] = ld2(at(v, j + 1, p + 2));
+            F0[s][j] = ld2(at(f, j + 1, p));
+            F1[s][j] = ld2(at(f, j + 1, p + 1));
+        }
+        H0[s][0] = ld2(at(v, 0, p));
+        H0[s][1] = ld2(at(v, 4, p));
+        H1[s][0] = ld2(at(v, 0, p + 1));
+        H1[s][1] = ld2(at(v, 4, p + 1));
+    };
+    // LDS-only barrier: the outstanding prefetch stays in flight across it
+    auto lds_barrier = [] {
+        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+    };
+    // the columns left of lane 0 / right of lane 63 on two planes: v(x-1) of lane 0, v(x+2) of lane 63
+    auto edges_v = [&](int par, const double2 (&P)[3], const double2 (&Q)[3], double (&CLp)[3], double (&CRp)[3],
+                       double (&CLq)[3], double (&CRq)[3]) {
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                ve[par][wx + 1][0][j] = P[j].x;
+                ve[par][wx + 1][0][3 + j] = Q[j].x;
+            }
+        }
+        if (lane == WAVE - 1) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                ve[par][wx + 1][1][j] = P[j].y;
+                ve[par][wx + 1][1][3 + j] = Q[j].y;
+            }
+        }
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            CLp[j] = uniform_d(ve[par][wx][1][j]);
+            CRp[j] = uniform_d(ve[par][wx + 2][0][j]);
+            CLq[j] = uniform_d(ve[par][wx][1][3 + j]);
+            CRq[j] = uniform_d(ve[par][wx + 2][0][3 + j]);
+        }
+    };
+    // r(2X+1) of every lane for two planes: the right neighbour lane's r.x (lane 63: the right wave's)
+    auto edges_r = [&](int par, const double2 (&R)[3], const double2 (&S)[3], double (&NR)[3], double (&NS)[3]) {
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                re[par][wx + 1][j] = R[j].x;
+                re[par][wx + 1][3 + j] = S[j].x;
+            }
+        }
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            NR[j] = lane_from_right<true>(R[j].x, uniform_d(re[par][wx + 2][j]));
+            NS[j] = lane_from_right<true>(S[j].x, uniform_d(re[par][wx + 2][3 + j]));
+        }
+    };
+    // r = f - A v on fine plane p, rows 1..3 (k_rb KIND 1: same expression, same term order); 0 outside
+    // the interior, as the reference's never-written boundary of r
+    auto resid = [&](const double2 (&Vm)[3], const double2 (&Vc)[3], const double2 (&H)[2], const double2 (&Vp)[3],
+                     const double2 (&F)[3], const double (&CL)[3], const double (&CR)[3], int p, double2 (&R)[3]) {
+        const bool pin = p >= 1 && p <= fnz;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const double2 c = Vc[j];
+            const double2 ym = j == 0 ? H[0] : Vc[j - 1], yp = j == 2 ? H[1] : Vc[j + 1];
+            const double xm0 = lane_from_left<true>(c.y, CL[j]);
+            const double xp1 = lane_from_right<true>(c.x, CR[j]);
+            const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, Vp[j].x, Vm[j].x, 0.0);
+            const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, Vp[j].y, Vm[j].y, 0.0);
+            const bool ok = pin && rowc[j + 1];
+            R[j] = make_double2((ok && okx0) ? F[j].x - a0 : 0.0, (ok && okx1) ? F[j].y - a1 : 0.0);
+        }
+    };
+
+    // prologue: r on fine plane 2Zb-1 (the top plane of the previous coarse plane's stencil)
+    double2 Vm[3], V0[3], Rm[3];
+    double Nm[3];
+    {
+        const int p = 2 * Zb - 1;
+        double2 Vq[3], Hq[2], Fq[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            Vm[j] = ld2(at(v, j + 1, p - 1));
+            Vq[j] = ld2(at(v, j + 1, p));
+            V0[j] = ld2(at(v, j + 1, p + 1));
+            Fq[j] = ld2(at(f, j + 1, p));
+        }
+        Hq[0] = ld2(at(v, 0, p));
+        Hq[1] = ld2(at(v, 4, p));
+        double CL[3], CR[3], CL2[3], CR2[3], N2[3];
+        edges_v(1, Vq, Vq, CL, CR, CL2, CR2);
+        resid(Vm, Vq, Hq, V0, Fq, CL, CR, p, Rm);
+        edges_r(1, Rm, Rm, Nm, N2);
+#pragma unroll
+        for (int j = 0; j < 3; j++) Vm[j] = Vq[j]; // window: Vm = v(2Zb-1), V0 = v(2Zb)
+    }
+    load_slot(1, Zb);
+    // Both halves always run (an odd chunk ends with a step whose results are discarded), and every
+    // load is unconditional (plane indices clamped), so the slots keep fixed registers.
+    for (int z0 = Zb; z0 <= Ze; z0 += 2) {
+#pragma unroll
+        for (int ph = 0; ph < 2; ph++) {
+            const int Z = z0 + ph;
+            const int cs = ph ^ 1; // slot holding this step's operands
+            load_slot(ph, Z + 1);
+            double CL0[3], CR0[3], CL1[3], CR1[3];
+            edges_v(ph, V0, VA[cs], CL0, CR0, CL1, CR1);
+            double2 R0[3], R1[3];
+            resid(Vm, V0, H0[cs], VA[cs], F0[cs], CL0, CR0, 2 * Z, R0);
+            resid(V0, VA[cs], H1[cs], VB[cs], F1[cs], CL1, CR1, 2 * Z + 1, R1);
+            double N0[3], N1[3];
+            edges_r(ph, R0, R1, N0, N1);
+            if (Z <= Ze && X <= cnx) {
+                double acc = 0.0;
+#pragma unroll
+                for (int a = -1; a <= 1; a++)
+#pragma unroll
+                    for (int b = -1; b <= 1; b++)
+#pragma unroll
+                        for (int c = -1; c <= 1; c++) {
+                            const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
+                                               ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                            const int j = b + 1;
+                            const double2 rp = c < 0 ? Rm[j] : (c == 0 ? R0[j] : R1[j]);
+                            const double rn = c < 0 ? Nm[j] : (c == 0 ? N0[j] : N1[j]);
+                            acc += wgt * (a < 0 ? rp.x : (a == 0 ? rp.y : rn));
+                        }
+                const int64_t q = X + Y * cldy + (int64_t)Z * cldz;
+                ca[q] = acc;
+                if (cb) cb[q] = acc;
+            }
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                Vm[j] = VA[cs][j];
+                V0[j] = VB[cs][j];
+                Rm[j] = R1[j];
+                Nm[j] = N1[j];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Trilinear prolongation, closed form per fine point (the reference's inject + X, Y, Z passes,
 // CpuSolver.cpp:240-290, combined in the same X -> Y -> Z order). Fine index P-1 is never written by
 // the reference (stays 0) and coarse index Pc-1 is the zero boundary, so along each axis:
@@ -1921,6 +2125,20 @@ int gs_residual_restrict(const gs_stencil* S, const gs_level* fl, int mode, doub
         2 * cl->nz + zoff + 1 > fl->nz + 1)
         return GS_EINVAL;
     const Coef k = make_coef(S, fl, 0.0, gamma);
+    const int64_t wxs = ((fl->nx + 1) / 2 + WAVE - 1) / WAVE; // x-waves covering coarse columns 1..(fnx+1)/2
+    static const bool ldsOnly = getenv("GS_RR_LDS") != nullptr;   // A/B switch for tools/ measurements
+    if (!ldsOnly && canonical_order(S) && zoff == 0 && mode != GS_NEWTON && wxs <= RR2_WXMAX) {
+        // >= 2048 blocks of one coarse row where the level has them (chunks of <= 32 coarse planes)
+        const int64_t chunks = (2048 + cl->ny - 1) / cl->ny;
+        int64_t zc = (cl->nz + chunks - 1) / chunks;
+        zc = zc < 1 ? 1 : (zc > 32 ? 32 : zc);
+        const dim3 g((unsigned)cl->ny, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
+#define GS_RR2(M) hipLaunchKernelGGL(k_rr2<M>, g, b, 0, st, k, v, f, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->nz, cl->ldy, cl->ldz, (int)zc)
+        if (mode == GS_LINEAR) GS_RR2(GS_LINEAR);
+        else GS_RR2(GS_NONLINEAR);
+#undef GS_RR2
+        return launch_status();
+    }
     StencilOffsets so;
     for (int t = 0; t < 7; t++) {
         so.lds[t] = S->ox[t] + S->oy[t] * RR_VX;

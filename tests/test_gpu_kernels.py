@@ -281,7 +281,8 @@ def test_invalid_arguments_fail_loudly():
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("fd", [(2, 2, 2), (3, 5, 7), (16, 17, 18), (129, 33, 20), (130, 8, 9), (255, 10, 33),
-                                (64, 64, 64)])
+                                (64, 64, 64), (511, 9, 10), (512, 6, 5), (1023, 5, 6), (1024, 4, 3), (1100, 3, 4),
+                                (127, 2, 70), (258, 66, 1)])
 def test_residual_restrict_fused(fd, mode):
     """gs_residual_restrict == gs_residual + gs_restrict2 bit for bit (and == the oracle's restrict of
     the oracle's residual, to the mode's tolerance); odd and even fine extents, partial tiles."""

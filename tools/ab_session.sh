@@ -30,5 +30,5 @@ vc() { # name, env...
 vc default GS_AB=default
 vc nocoarse GS_COARSE_POINTS=0
 
-vc coarse32k GS_COARSE_POINTS=40000
+vc rrlds GS_RR_LDS=1
 step done
