@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--vcycles", type=int, default=20, help="timed V-cycles after one warm-up cycle (0: skip)")
     ap.add_argument("--cpu-sweeps", type=int, default=6, help="cpu_baseline sample size (0: skip)")
     ap.add_argument("--cpu-vcycles", type=int, default=1, help="cpu_baseline V-cycles (0: skip)")
+    ap.add_argument("--newton-iters", type=int, default=2,
+                    help="timed Newton iterations of BASELINE config #4 (512^3 Newton 2+2) at N=1 (0: skip)")
     return ap.parse_args()
 
 
@@ -190,6 +192,24 @@ def triad_ceiling(n):
             "ms": round(ms, 4), "gbps": round(24.0 * n / (ms * 1e-3) / 1e9, 1)}
 
 
+def newton_timing(n, iters):
+    """BASELINE config #4: the n^3 Newton solve (mode 2, 2+2, omega 0.8, gamma 1, tol 0), `iters` outer
+    iterations through the driver (NewtonSolver::solve: per iteration restrict newtonV, an inner solve
+    of 10 V-cycles, newtonV += v, compF + norm), on its own grid after one untimed iteration."""
+    p = gsv.GridParams(maxiter=1, tol=0.0, gridDim=(n, n, n), mode=gsv.GS_NEWTON, preSmoothing=2, postSmoothing=2)
+    with gsv.HipGridData(p) as g:
+        gsv.NewtonSolver.solve(g)  # warm-up: first touch of every level
+    p.maxiter = iters
+    with gsv.HipGridData(p) as g:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hist = gsv.NewtonSolver.solve(g)
+        ms = (time.perf_counter() - t0) * 1e3
+    return {"ms_per_iteration": round(ms / iters, 2), "iterations": iters,
+            "config": f"{n}^3 Newton 2+2 (BASELINE config #4), 10 inner V-cycles per iteration, norm readbacks included",
+            "residuals": hist}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,6 +288,10 @@ def main():
         vc = {"ms": round(vt.item(), 3), "cycles": a.vcycles,
               "config": f"{dims[0]}x{dims[1]}x{dims[2]} linear 2+2, norm readback included", "first_residual": res}
 
+    newton = None
+    if world == 1 and a.newton_iters > 0:
+        newton = newton_timing(n, a.newton_iters)
+
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sweeps > 0:
         try:
@@ -305,6 +329,7 @@ def main():
             "single_sweep_kernel": single,
             "measured_ceiling": ceiling,
             "vcycle": vc,
+            "newton": newton,
             "cpu_baseline": cpu,
             "kernel_build": gsv.build_info(),
         }
