@@ -216,6 +216,17 @@ __device__ __forceinline__ double jacobi_update(const Coef& k, double v, double 
     return v + k.omega * (r / den);
 }
 
+// NEWTON's linearisation terms of a point, A = gamma (1 + w) and E = exp(w), computed ONCE per point
+// and pass and shared by the operator and the update of both sweeps of a fused pair: bit-identical to
+// op_finish / jacobi_update, whose reference expressions evaluate gamma * (1 + w) first and multiply
+// by exp(w) last (CpuSolver.cpp:63-66, :157-171).
+__device__ __forceinline__ double newton_op(double q, double c, double A, double E) { return q + A * c * E; }
+__device__ __forceinline__ double newton_update(const Coef& k, double v, double r, double A, double E)
+{
+    const double den = k.preFac + A * E;
+    return v + k.omega * (r / den);
+}
+
 __device__ __forceinline__ double wave_sum(double x)
 {
 #pragma unroll
@@ -424,15 +435,24 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
                 const double xp1 = lane_from_right<DPP>(c.x, ER[cs][r]);
                 const double wx = (MODE == GS_NEWTON) ? WL[cs][r].x : 0.0;
                 const double wy = (MODE == GS_NEWTON) ? WL[cs][r].y : 0.0;
-                const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
-                const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
+                // NEWTON sweep: exp(w) once per point, shared by the operator and the update
+                constexpr bool NS = MODE == GS_NEWTON && KIND == 0;
+                const double Ax = NS ? k.gamma * (1 + wx) : 0.0, Ay = NS ? k.gamma * (1 + wy) : 0.0;
+                const double Ex = NS ? exp(wx) : 0.0, Ey = NS ? exp(wy) : 0.0;
+                const double a0 = NS ? newton_op(div_hh(k, stencil_sum(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x)), c.x, Ax, Ex)
+                                     : op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
+                const double a1 = NS ? newton_op(div_hh(k, stencil_sum(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)), c.y, Ay, Ey)
+                                     : op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
                 double r0 = 0.0, r1 = 0.0; // residual of the input iterate
                 if (KIND != 2 || ADD) {
                     r0 = FL[cs][r].x - a0;
                     r1 = FL[cs][r].y - a1;
                 }
                 double o0, o1;
-                if (KIND == 0) {
+                if (NS) {
+                    o0 = newton_update(k, c.x, r0, Ax, Ex);
+                    o1 = newton_update(k, c.y, r1, Ay, Ey);
+                } else if (KIND == 0) {
                     o0 = jacobi_update<MODE>(k, c.x, r0, wx);
                     o1 = jacobi_update<MODE>(k, c.y, r1, wy);
                 } else if (KIND == 1) {
@@ -1519,7 +1539,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     auto at = [&](const double* base, int j, int z) { return base + xl + roff[j + 1] + (int64_t)z * ldz; };
 
     double2 Vp[NV], Vc[NV], VL[2][NV], FL[2][NV], WL[2][NV], HL[2];
-    double2 V1p[RY], V1c[NV], Fprev[RY], Wprev[RY];
+    double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
 #pragma unroll
     for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
 #pragma unroll
@@ -1647,6 +1667,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             // ---- the two sweeps; wave 1 (mirrored rows) runs its own copy of the code, so the swap of
             // its y-neighbours costs no selects ----
             double2 V1n[NV];
+            double2 Acur[RY], Ecur[RY]; // NEWTON terms of sweep 1's own rows (-> Aprev / Eprev)
             const bool pz = planeok(z);
             auto sweeps = [&](auto mirc) {
                 const bool M = mirc.get();
@@ -1669,13 +1690,26 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                     double q[2] = {stencil_sum(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
                                    stencil_sum(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
                     div_hh_row<MODE>(k, q);
-                    const double wx0 = (MODE == GS_NEWTON) ? WL[cs][j].x : 0.0;
-                    const double wx1 = (MODE == GS_NEWTON) ? WL[cs][j].y : 0.0;
-                    const double a0 = op_finish<MODE>(k, q[0], c.x, wx0);
-                    const double a1 = op_finish<MODE>(k, q[1], c.y, wx1);
+                    double a0, a1, n0, n1;
+                    if constexpr (MODE == GS_NEWTON) {
+                        const double2 wv = WL[cs][j];
+                        const double2 A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
+                        const double2 E = make_double2(exp(wv.x), exp(wv.y));
+                        if (j >= 1) {
+                            Acur[j - 1] = A;
+                            Ecur[j - 1] = E;
+                        }
+                        a0 = newton_op(q[0], c.x, A.x, E.x);
+                        a1 = newton_op(q[1], c.y, A.y, E.y);
+                        n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
+                        n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
+                    } else {
+                        a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
+                        a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
+                        n0 = jacobi_update<MODE>(k, c.x, FL[cs][j].x - a0, 0.0);
+                        n1 = jacobi_update<MODE>(k, c.y, FL[cs][j].y - a1, 0.0);
+                    }
                     const double r0 = FL[cs][j].x - a0, r1 = FL[cs][j].y - a1;
-                    const double n0 = jacobi_update<MODE>(k, c.x, r0, wx0);
-                    const double n1 = jacobi_update<MODE>(k, c.y, r1, wx1);
                     if (partials && j >= 1 && z >= zb && z <= ze && rowc[j + 1]) {
                         if (okx0) sumsq += r0 * r0;
                         if (okx1) sumsq += r1 * r1;
@@ -1696,12 +1730,19 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         double q[2] = {stencil_sum(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
                                        stencil_sum(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
                         div_hh_row<MODE>(k, q);
-                        const double wx0 = (MODE == GS_NEWTON) ? Wprev[j - 1].x : 0.0;
-                        const double wx1 = (MODE == GS_NEWTON) ? Wprev[j - 1].y : 0.0;
-                        const double a0 = op_finish<MODE>(k, q[0], c.x, wx0);
-                        const double a1 = op_finish<MODE>(k, q[1], c.y, wx1);
-                        const double o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 1].x - a0, wx0);
-                        const double o1 = jacobi_update<MODE>(k, c.y, Fprev[j - 1].y - a1, wx1);
+                        double o0, o1;
+                        if constexpr (MODE == GS_NEWTON) {
+                            const double2 A = Aprev[j - 1], E = Eprev[j - 1];
+                            const double a0 = newton_op(q[0], c.x, A.x, E.x);
+                            const double a1 = newton_op(q[1], c.y, A.y, E.y);
+                            o0 = newton_update(k, c.x, Fprev[j - 1].x - a0, A.x, E.x);
+                            o1 = newton_update(k, c.y, Fprev[j - 1].y - a1, A.y, E.y);
+                        } else {
+                            const double a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
+                            const double a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
+                            o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 1].x - a0, 0.0);
+                            o1 = jacobi_update<MODE>(k, c.y, Fprev[j - 1].y - a1, 0.0);
+                        }
                         if (yof(j) <= ny) {
                             double* qo = out + x + roff[j + 1] + zo;
                             if (okx1) st2s<NT>(qo, o0, o1);
@@ -1721,7 +1762,10 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             for (int j = 1; j <= RY; j++) {
                 V1p[j - 1] = V1c[j];
                 Fprev[j - 1] = FL[cs][j];
-                if (MODE == GS_NEWTON) Wprev[j - 1] = WL[cs][j];
+                if (MODE == GS_NEWTON) {
+                    Aprev[j - 1] = Acur[j - 1];
+                    Eprev[j - 1] = Ecur[j - 1];
+                }
             }
 #pragma unroll
             for (int j = 0; j < NV; j++) {
