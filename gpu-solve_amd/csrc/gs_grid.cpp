@@ -513,7 +513,8 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
             // iterate is never stored), then the remaining ones
             materialize(grid, i - 1);
             check(gs_jacobi_sweep2_prolong(&grid.stencilAbi, &F.geom, (int)grid.mode, grid.omega, grid.gamma,
-                                           F.v.data(), C.v.data(), nullptr, &C.geom, F.vAlt.data(), F.f.data(), s),
+                                           F.v.data(), C.v.data(), nullptr, &C.geom, F.vAlt.data(), F.f.data(),
+                                           F.newtonV ? F.newtonV.data() : nullptr, s),
                   "gs_jacobi_sweep2_prolong");
             F.v.swap(F.vAlt);
             jacobi(grid, i - 1, grid.postSmoothing - 2);

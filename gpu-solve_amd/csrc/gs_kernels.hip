@@ -2038,9 +2038,7 @@ const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int 
     dim3 g, b;
     bool y2 = false;
     if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode)) return "";
-    if (y2)
-        return mode == GS_NEWTON ? "k_tb2y: 4x2 waves, 2 rows per wave, LDS halo-row exchange"
-                                 : "k_tb2y: 4x2 waves, 2 rows per wave, LDS halo-row exchange, per-wave-row code";
+    if (y2) return "k_tb2y: 4x2 waves, 2 rows per wave, LDS halo-row exchange, per-wave-row code";
     return "k_tb2: <= 8 x-waves, 2 rows per wave";
 }
 
@@ -2065,7 +2063,7 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
 #define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
-#define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, M != GS_NEWTON>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
     const bool zv = !v_in;
     if (y2) {
         if (mode == GS_LINEAR) {
@@ -2092,27 +2090,28 @@ int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, i
     int zc;
     dim3 g, b;
     bool y2 = false;
-    // LINEAR only: the NONLINEAR (FAS) variant carries the coarse restV too and exceeds the register
-    // budget of two waves per SIMD; NEWTON runs the per-use-select code (no per-wave copies)
-    return !bad_level(L) && valid_stencil(S) && mode == GS_LINEAR && L->z0 == 0 &&
+    // LINEAR and NEWTON: the NONLINEAR (FAS) variant carries the coarse restV too and exceeds the
+    // register budget of two waves per SIMD
+    return !bad_level(L) && valid_stencil(S) && (mode == GS_LINEAR || mode == GS_NEWTON) && L->z0 == 0 &&
            tb2_plan(S, L, &zc, &g, &b, &y2, mode) && y2;
 }
 
 int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                              const double* v_in, const double* coarse_v, const double* coarse_sub, const gs_level* cl,
-                             double* v_out, const double* f, hipStream_t st)
+                             double* v_out, const double* f, const double* w, hipStream_t st)
 {
     int zc;
     dim3 g, b;
     bool y2 = false;
     if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || bad_level(cl) || cl->z0 != 0 || !v_in || !coarse_v ||
-        !v_out || !f || v_in == v_out || (mode == GS_NONLINEAR) != (coarse_sub != nullptr) ||
+        !v_out || !f || v_in == v_out || (mode == GS_NONLINEAR) != (coarse_sub != nullptr) || (mode == GS_NEWTON && !w) ||
         (L->nx + 1) / 2 > cl->nx + 1 || (L->ny + 1) / 2 > cl->ny + 1 || (L->nz + 1) / 2 > cl->nz + 1 ||
         !tb2_plan(S, L, &zc, &g, &b, &y2, mode))
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, gamma);
-#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, false, true, P>), g, b, 0, st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, 0, 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz)
-    GS_TBP(GS_LINEAR, 1);
+#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, false, true, P>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, 0, 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz)
+    if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1);
+    else GS_TBP(GS_LINEAR, 1);
 #undef GS_TBP
     return launch_status();
 }

@@ -186,28 +186,33 @@ PRO_SHAPES = [(1, 1, 1), (2, 5, 3), (5, 4, 33), (127, 9, 17), (128, 8, 8), (129,
               (500, 7, 9), (512, 4, 5), (64, 64, 64), (63, 31, 65), (200, 33, 70)]
 
 
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("shape", PRO_SHAPES)
-def test_prolong_fused_pair_bit_identical(shape):
-    """gs_jacobi_sweep2_prolong == gs_prolong_add then gs_jacobi_sweep2, bit for bit (LINEAR); odd and
-    even fine extents, partial row tiles and z-chunks."""
-    rng = np.random.default_rng(sum(shape) * 13)
+def test_prolong_fused_pair_bit_identical(shape, mode):
+    """gs_jacobi_sweep2_prolong == gs_prolong_add then gs_jacobi_sweep2, bit for bit (LINEAR and NEWTON,
+    whose newtonV enters both sweeps); odd and even fine extents, partial row tiles and z-chunks."""
+    rng = np.random.default_rng(sum(shape) * 13 + mode)
     nx, ny, nz = shape
     cd = [x // 2 for x in shape]
     h = 1.0 / (ny + 1)
     v0, f0, c0 = rand_full(rng, *shape), rand_full(rng, *shape, 100.0), rand_full(rng, *[max(c, 0) for c in cd])
+    w0 = rand_full(rng, *shape, 0.5)
     L = DevField(nx, ny, nz).level(h)
-    if not k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), 0):
+    if not k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), mode):
         pytest.skip("shape outside the fused path")
     # reference: prolongation + correction stored, then the plain fused pair
     v, f, c, out_ref = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
                         DevField(*cd).from_xyz(c0), DevField(nx, ny, nz))
+    w = DevField(nx, ny, nz).from_xyz(w0) if mode == 2 else None
+    wp = w.ptr if w else None
     Lc = c.level(2 * h)
     ok(k().gs_prolong_add(c.ptr, None, C.byref(Lc), v.ptr, C.byref(L), st()))
-    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, out_ref.ptr, f.ptr, None, 0, 0, st()))
+    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, out_ref.ptr, f.ptr, wp, 0, 0,
+                            st()))
     # fused
     v2, out = DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz)
-    ok(k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v2.ptr, c.ptr, None, C.byref(Lc),
-                                    out.ptr, f.ptr, st()))
+    ok(k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v2.ptr, c.ptr, None,
+                                    C.byref(Lc), out.ptr, f.ptr, wp, st()))
     np.testing.assert_array_equal(out.to_xyz(), out_ref.to_xyz())
     np.testing.assert_array_equal(v2.to_xyz(), v0)  # the input iterate is left as it was
 
@@ -215,6 +220,10 @@ def test_prolong_fused_pair_bit_identical(shape):
 def test_prolong_fused_pair_rejects():
     L = DevField(16, 16, 16).level(1 / 17.0)
     assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), 1) == 0  # NONLINEAR
-    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), 2) == 0  # NEWTON
+    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), 2) != 0  # NEWTON
+    f, out, c = DevField(16, 16, 16), DevField(16, 16, 16), DevField(8, 8, 8)
+    rc = k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), 2, 0.8, 1.0, f.ptr, c.ptr, None,
+                                      C.byref(c.level(1 / 9.0)), out.ptr, f.ptr, None, st())
+    assert rc == gsv._abi.GS_EINVAL  # NEWTON needs newtonV
     L2 = DevField(600, 4, 4).level(0.2)
     assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 0) == 0  # rows > 512
