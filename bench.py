@@ -12,8 +12,9 @@ including the 8-byte norm readback) is measured after the timed region ("vcycle"
 
 Multi-GPU (torchrun, one process per GPU): the grid is Z-slab partitioned over RCCL (xGMI), ghost
 planes exchanged every sweep on a second stream while the interior planes are swept; weak scaling
-with 512^3 lattice points per rank: N=2 -> 1024x512x512, N=4 -> 1024x1024x512, N=8 -> 1024^3
-(BASELINE config #5); other N -> 512x512x(512N).
+with 512^3 lattice points per rank: N=2 -> 512x512x1024, N=4 -> 512x1024x1024 (every rank's slab has
+the single-GPU run's 512-point rows, so the per-rank kernels are the N=1 ones), N=8 -> 1024^3
+(BASELINE config #5: 1024-point rows, the 8-wave-row pair k_tb2); other N -> 512x512x(512N).
 
 Roofline: the smoother is HBM-bound (0.5 flop/B per sweep); algorithmic bytes per launch = 24 B
 per lattice point (read v, read f, write the result) x 512^3, for a single sweep
@@ -101,7 +102,7 @@ def cpu_baseline(n, sweeps, vcycles):
 
 
 def global_dims(n, world):
-    table = {1: (n, n, n), 2: (2 * n, n, n), 4: (2 * n, 2 * n, n), 8: (2 * n, 2 * n, 2 * n)}
+    table = {1: (n, n, n), 2: (n, n, 2 * n), 4: (n, 2 * n, 2 * n), 8: (2 * n, 2 * n, 2 * n)}
     return table.get(world, (n, n, n * world))
 
 
