@@ -22,7 +22,7 @@ vc() { # name, env...
     local name=$1; shift
     step "vcycle $name"
     env "$@" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/vc_$name" -o run --output-format csv -- \
-        python bench.py --steps 2 --warmup 2 --cpu-sweeps 0 --vcycles 10 > "$OUT/vc_$name.json" 2> "$OUT/vc_$name.err" \
+        python bench.py --steps 2 --warmup 2 --cpu-sweeps 0 --newton-iters 0 --vcycles 10 > "$OUT/vc_$name.json" 2> "$OUT/vc_$name.err" \
         || { tail -20 "$OUT/vc_$name.err"; exit 1; }
     python tools/vc_breakdown.py "$OUT/vc_$name/run_kernel_trace.csv" 14 > "$OUT/vc_$name.txt"
     head -1 "$OUT/vc_$name.txt"
