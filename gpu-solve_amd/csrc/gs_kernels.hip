@@ -779,12 +779,13 @@ constexpr int RR2_WXMAX = 8;
 
 template <int MODE, bool PF> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
 __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* __restrict__ v,
-                                                         const double* __restrict__ f, double* __restrict__ ca,
+                                                         const double* __restrict__ f, const double* __restrict__ w,
+                                                         double* __restrict__ ca,
                                                          double* __restrict__ cb, int fnx, int fny, int fnz,
                                                          int64_t fldy, int64_t fldz, int cnx, int cnz, int64_t cldy,
                                                          int64_t cldz, int ZC)
 {
-    static_assert(MODE != GS_NEWTON, "NEWTON runs k_resrestrict (newtonV would exceed the register budget)");
+    static_assert(MODE != GS_NEWTON || !PF, "NEWTON: newtonV rows exceed the budget of the prefetch ring");
     // wave-edge columns [parity][1 + wave][side][plane * 3 + row] of v, and r at each wave's first fine
     // column [parity][1 + wave][plane * 3 + row]; slots 0 and WX+1 are the zero x-boundary
     __shared__ double ve[2][RR2_WXMAX + 2][2][6];
@@ -814,7 +815,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     };
     // one step's operands: v planes 2Z+1 (A), 2Z+2 (B) of rows 1..3; halo rows 0 / 4 of planes 2Z (H0)
     // and 2Z+1 (H1); f of planes 2Z (F0), 2Z+1 (F1) rows 1..3
-    double2 VA[2][3], VB[2][3], H0[2][2], H1[2][2], F0[2][3], F1[2][3];
+    double2 VA[2][3], VB[2][3], H0[2][2], H1[2][2], F0[2][3], F1[2][3], W0[2][3], W1[2][3];
     auto load_slot = [&](const int s, const int Z) {
         const int p = 2 * Z;
 #pragma unroll
@@ -823,6 +824,10 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             VB[s][j] = ld2(at(v, j + 1, p + 2));
             F0[s][j] = ld2(at(f, j + 1, p));
             F1[s][j] = ld2(at(f, j + 1, p + 1));
+            if (MODE == GS_NEWTON) {
+                W0[s][j] = ld2(at(w, j + 1, p));
+                W1[s][j] = ld2(at(w, j + 1, p + 1));
+            }
         }
         H0[s][0] = ld2(at(v, 0, p));
         H0[s][1] = ld2(at(v, 4, p));
@@ -879,7 +884,8 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     // r = f - A v on fine plane p, rows 1..3 (k_rb KIND 1: same expression, same term order); 0 outside
     // the interior, as the reference's never-written boundary of r
     auto resid = [&](const double2 (&Vm)[3], const double2 (&Vc)[3], const double2 (&H)[2], const double2 (&Vp)[3],
-                     const double2 (&F)[3], const double (&CL)[3], const double (&CR)[3], int p, double2 (&R)[3]) {
+                     const double2 (&F)[3], const double2 (&W)[3], const double (&CL)[3], const double (&CR)[3], int p,
+                     double2 (&R)[3]) {
         const bool pin = p >= 1 && p <= fnz;
 #pragma unroll
         for (int j = 0; j < 3; j++) {
@@ -887,8 +893,9 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             const double2 ym = j == 0 ? H[0] : Vc[j - 1], yp = j == 2 ? H[1] : Vc[j + 1];
             const double xm0 = lane_from_left<true>(c.y, CL[j]);
             const double xp1 = lane_from_right<true>(c.x, CR[j]);
-            const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, Vp[j].x, Vm[j].x, 0.0);
-            const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, Vp[j].y, Vm[j].y, 0.0);
+            const double w0 = MODE == GS_NEWTON ? W[j].x : 0.0, w1 = MODE == GS_NEWTON ? W[j].y : 0.0;
+            const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, Vp[j].x, Vm[j].x, w0);
+            const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, Vp[j].y, Vm[j].y, w1);
             const bool ok = pin && rowc[j + 1];
             R[j] = make_double2((ok && okx0) ? F[j].x - a0 : 0.0, (ok && okx1) ? F[j].y - a1 : 0.0);
         }
@@ -899,19 +906,20 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     double Nm[3];
     {
         const int p = 2 * Zb - 1;
-        double2 Vq[3], Hq[2], Fq[3];
+        double2 Vq[3], Hq[2], Fq[3], Wq[3];
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             Vm[j] = ld2(at(v, j + 1, p - 1));
             Vq[j] = ld2(at(v, j + 1, p));
             V0[j] = ld2(at(v, j + 1, p + 1));
             Fq[j] = ld2(at(f, j + 1, p));
+            Wq[j] = MODE == GS_NEWTON ? ld2(at(w, j + 1, p)) : make_double2(0.0, 0.0);
         }
         Hq[0] = ld2(at(v, 0, p));
         Hq[1] = ld2(at(v, 4, p));
         double CL[3], CR[3], CL2[3], CR2[3], N2[3];
         edges_v(1, Vq, Vq, CL, CR, CL2, CR2);
-        resid(Vm, Vq, Hq, V0, Fq, CL, CR, p, Rm);
+        resid(Vm, Vq, Hq, V0, Fq, Wq, CL, CR, p, Rm);
         edges_r(1, Rm, Rm, Nm, N2);
 #pragma unroll
         for (int j = 0; j < 3; j++) Vm[j] = Vq[j]; // window: Vm = v(2Zb-1), V0 = v(2Zb)
@@ -929,8 +937,8 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             double CL0[3], CR0[3], CL1[3], CR1[3];
             edges_v(ph, V0, VA[cs], CL0, CR0, CL1, CR1);
             double2 R0[3], R1[3];
-            resid(Vm, V0, H0[cs], VA[cs], F0[cs], CL0, CR0, 2 * Z, R0);
-            resid(V0, VA[cs], H1[cs], VB[cs], F1[cs], CL1, CR1, 2 * Z + 1, R1);
+            resid(Vm, V0, H0[cs], VA[cs], F0[cs], W0[cs], CL0, CR0, 2 * Z, R0);
+            resid(V0, VA[cs], H1[cs], VB[cs], F1[cs], W1[cs], CL1, CR1, 2 * Z + 1, R1);
             double N0[3], N1[3];
             edges_r(ph, R0, R1, N0, N1);
             if (Z <= Ze && X <= cnx) {
@@ -2171,7 +2179,7 @@ int gs_residual_restrict(const gs_stencil* S, const gs_level* fl, int mode, doub
     const Coef k = make_coef(S, fl, 0.0, gamma);
     const int64_t wxs = ((fl->nx + 1) / 2 + WAVE - 1) / WAVE; // x-waves covering coarse columns 1..(fnx+1)/2
     static const bool ldsOnly = getenv("GS_RR_LDS") != nullptr;   // A/B switch for tools/ measurements
-    if (!ldsOnly && canonical_order(S) && zoff == 0 && mode != GS_NEWTON && wxs <= RR2_WXMAX) {
+    if (!ldsOnly && canonical_order(S) && zoff == 0 && wxs <= RR2_WXMAX) {
         // >= 2048 blocks of one coarse row where the level has them (chunks of <= 32 coarse planes)
         const int64_t chunks = (2048 + cl->ny - 1) / cl->ny;
         int64_t zc = (cl->nz + chunks - 1) / chunks;
@@ -2179,9 +2187,10 @@ int gs_residual_restrict(const gs_stencil* S, const gs_level* fl, int mode, doub
         const dim3 g((unsigned)cl->ny, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
-#define GS_RR2(M) hipLaunchKernelGGL((k_rr2<M, false>), g, b, 0, st, k, v, f, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->nz, cl->ldy, cl->ldz, (int)zc)
+#define GS_RR2(M) hipLaunchKernelGGL((k_rr2<M, false>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->nz, cl->ldy, cl->ldz, (int)zc)
         if (mode == GS_LINEAR) GS_RR2(GS_LINEAR);
-        else GS_RR2(GS_NONLINEAR);
+        else if (mode == GS_NONLINEAR) GS_RR2(GS_NONLINEAR);
+        else GS_RR2(GS_NEWTON);
 #undef GS_RR2
         return launch_status();
     }
