@@ -38,7 +38,11 @@ def single(params, sweeps, solve):
 
 
 @pytest.mark.parametrize("dims,nranks", [((33, 17, 40), 2), ((64, 64, 64), 4), ((31, 20, 61), 3),
-                                         ((128, 64, 96), 8)])
+                                         ((128, 64, 96), 8),
+                                         # slabs large enough for the fused pairs (k_tb2y; k_tb2 for rows
+                                         # > 512), their depth-2 ghosts and the overlapped boundary planes
+                                         ((64, 256, 64), 2), ((32, 512, 64), 4), ((600, 128, 64), 2),
+                                         ((48, 512, 70), 3)])
 def test_sweeps_bit_identical(dims, nranks):
     p = gsv.GridParams(maxiter=0, gridDim=dims, mode=0)
     _, ref = single(p, 5, False)
@@ -48,7 +52,8 @@ def test_sweeps_bit_identical(dims, nranks):
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("dims,nranks,min_points", [((32, 32, 32), 2, 0), ((31, 31, 63), 4, 0),
-                                                    ((48, 40, 64), 3, 4096), ((64, 64, 64), 2, -1)])
+                                                    ((48, 40, 64), 3, 4096), ((64, 64, 64), 2, -1),
+                                                    ((64, 256, 64), 2, -1), ((32, 512, 64), 4, -1)])
 def test_solve_matches_single_gpu(mode, dims, nranks, min_points):
     p = gsv.GridParams(maxiter=3 if mode == 2 else 5, tol=0.0, gridDim=dims, mode=mode)
     ref_h, ref_v = single(p, 0, True)
