@@ -137,12 +137,13 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
                        (!L.distributed || L.minPlanes >= 2);
     }
     // The coarse end of the V-cycle runs as one gs_coarse_cycle launch from the first level of at
-    // most GS_COARSE_POINTS points (default 4096 = 16^3: below that each operator is launch latency,
-    // above it one workgroup is slower than the whole chip) that is not Z-slab partitioned; 0 = off.
+    // most GS_COARSE_POINTS points that is not Z-slab partitioned; 0 = off. Default 512 = 8^3: a 16^3
+    // level costs 42 us inside the one workgroup (a single CU's L2 bandwidth: ~6 us per operator)
+    // against 30 us as six chip-wide launches; from 8^3 down the launch wins (tools/ab_coarse.sh).
     coarseFrom = levels_.size();
     {
         const char* e = std::getenv("GS_COARSE_POINTS");
-        const int64_t thr = e ? std::atoll(e) : 4096;
+        const int64_t thr = e ? std::atoll(e) : 512;
         if (thr > 0 && preSmoothing + postSmoothing < (1u << 20))
             for (int l = nlev - 1; l >= 1; l--) {
                 if (levels_[l].distributed || pts[l] > thr || nlev - l > gs_coarse_cycle_max_levels()) break;

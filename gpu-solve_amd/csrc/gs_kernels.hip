@@ -1124,7 +1124,7 @@ __global__ __launch_bounds__(256) void k_axpy(double* __restrict__ y, const doub
 
 // ---------------------------------------------------------------------------------------------
 // The coarse end of the V-cycle in ONE launch of ONE workgroup (gs_coarse_cycle). A level of a few
-// thousand points is pure launch latency per operator on a chip it cannot fill (~4.5 us a sweep);
+// hundred points is pure launch latency per operator on a chip it cannot fill (~4.5 us a sweep);
 // here the whole recursion of CpuSolver::vcycle below level lv[0] (CpuSolver.cpp:92-135) runs in one
 // 1024-thread workgroup whose levels stay in L2, with a workgroup barrier between operators instead
 // of a kernel boundary (the waves of a workgroup share one CU's L1, so the barrier's workgroup-scope
@@ -1144,20 +1144,44 @@ struct CcPlan {
     int n, pre, post;
 };
 
-// every interior point of a level, x fastest, strided over the workgroup
-template <class F>
-__device__ __forceinline__ void cc_points(const CcLevel& L, F&& fn)
-{
-    const int n = L.nx * L.ny * L.nz;
-    for (int i = threadIdx.x; i < n; i += CC_T) {
-        const int t = i / L.nx, z = t / L.ny;
-        fn(1 + i - t * L.nx, 1 + t - z * L.ny, 1 + z);
-    }
-}
-
 __device__ __forceinline__ int64_t cc_at(const CcLevel& L, int x, int y, int z)
 {
     return x + y * L.ldy + (int64_t)z * L.ldz;
+}
+
+// dst[p] (and dst2[p]) = fn(x, y, z, p) for every interior point p of a level, x fastest, strided
+// over the workgroup, B points per thread and pass: all B values are computed before any is stored,
+// so a phase reading the field it writes (prolongation, f += A u) sees only old values.
+template <int B, class F>
+__device__ __forceinline__ void cc_map_b(const CcLevel& L, double* dst, double* dst2, F& fn)
+{
+    const int n = L.nx * L.ny * L.nz;
+    for (int i0 = threadIdx.x; i0 < n; i0 += B * CC_T) {
+        double val[B];
+        int64_t q[B];
+        bool ok[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            const int i = i0 + b * CC_T;
+            ok[b] = i < n;
+            const int ii = ok[b] ? i : i0; // a valid point; its value is discarded
+            const int t = ii / L.nx, z = t / L.ny;
+            const int x = 1 + ii - t * L.nx, y = 1 + t - z * L.ny;
+            q[b] = cc_at(L, x, y, 1 + z);
+            val[b] = fn(x, y, 1 + z, q[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < B; b++)
+            if (ok[b]) {
+                dst[q[b]] = val[b];
+                if (dst2) dst2[q[b]] = val[b];
+            }
+    }
+}
+template <class F>
+__device__ __forceinline__ void cc_map(const CcLevel& L, double* dst, double* dst2, F&& fn)
+{
+    cc_map_b<1>(L, dst, dst2, fn); // 2 points per pass measured no faster (the levels it runs are tiny)
 }
 
 // A(u) at p in config order (k_generic): the stencil sum, / h^2, the non-linear term; c = u(p),
@@ -1195,7 +1219,7 @@ __global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
         if (!((zero >> l) & 1)) return;
         const CcLevel& L = P.L[l];
         double* v = cur(l);
-        cc_points(L, [&](int x, int y, int z) { v[cc_at(L, x, y, z)] = 0.0; });
+        cc_map(L, v, nullptr, [&](int, int, int, int64_t) { return 0.0; });
         __syncthreads();
         zero &= ~(1u << l);
     };
@@ -1207,12 +1231,11 @@ __global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
             const bool uz = (zero >> l) & 1;
             const double* in = cur(l);
             double* out = ((alt >> l) & 1) ? L.v : L.va;
-            cc_points(L, [&](int x, int y, int z) {
-                const int64_t p = cc_at(L, x, y, z);
+            cc_map(L, out, nullptr, [&](int, int, int, int64_t p) {
                 double c, wv;
                 const double a = cc_op<MODE>(L.k, in, uz, L.w, p, c, wv);
                 const double r = L.f[p] - a;
-                out[p] = jacobi_update<MODE>(L.k, c, r, wv);
+                return jacobi_update<MODE>(L.k, c, r, wv);
             });
             __syncthreads();
             alt ^= 1u << l;
@@ -1222,7 +1245,7 @@ __global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
     // coarse interior of C <- 27-point full weighting of the fine field src of F (k_restrict)
     auto restrict_to = [&](const double* __restrict__ src, const CcLevel& F, double* ca, double* cb,
                            const CcLevel& C) {
-        cc_points(C, [&](int x, int y, int z) {
+        cc_map(C, ca, cb, [&](int x, int y, int z, int64_t) {
             const double* c0 = src + 2 * x + (int64_t)(2 * y) * F.ldy + (int64_t)(2 * z) * F.ldz;
             double acc = 0.0;
 #pragma unroll
@@ -1235,9 +1258,7 @@ __global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
                                            ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
                         acc += wgt * c0[a + b * F.ldy + c * F.ldz];
                     }
-            const int64_t q = cc_at(C, x, y, z);
-            ca[q] = acc;
-            if (cb) cb[q] = acc;
+            return acc;
         });
     };
 
@@ -1246,22 +1267,20 @@ __global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
         const CcLevel &F = P.L[l], &C = P.L[l + 1];
         smooth(l, P.pre);
         const double* u = cur(l);
-        cc_points(F, [&](int x, int y, int z) { // residual (k_generic KIND 1)
-            const int64_t p = cc_at(F, x, y, z);
+        cc_map(F, F.r, nullptr, [&](int, int, int, int64_t p) { // residual (k_generic KIND 1)
             double c, wv;
             const double a = cc_op<MODE>(F.k, u, false, F.w, p, c, wv);
-            F.r[p] = F.f[p] - a;
+            return F.f[p] - a;
         });
         __syncthreads();
         restrict_to(F.r, F, C.f, nullptr, C);
         if (MODE == GS_NONLINEAR) restrict_to(u, F, C.rv, cur(l + 1), C);
         __syncthreads();
         if (MODE == GS_NONLINEAR) { // f += A(restV)  (k_generic KIND 2, ADD)
-            cc_points(C, [&](int x, int y, int z) {
-                const int64_t p = cc_at(C, x, y, z);
+            cc_map(C, C.f, nullptr, [&](int, int, int, int64_t p) {
                 double c, wv;
                 const double a = cc_op<GS_NONLINEAR>(C.k, C.rv, false, nullptr, p, c, wv);
-                C.f[p] = C.f[p] + a;
+                return C.f[p] + a;
             });
             __syncthreads();
         }
@@ -1274,11 +1293,10 @@ __global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
         materialize(l);
         const double* cv = cur(l);
         double* fv = cur(l - 1);
-        cc_points(F, [&](int x, int y, int z) {
-            const int64_t p = cc_at(F, x, y, z);
+        cc_map(F, fv, nullptr, [&](int x, int y, int z, int64_t p) {
             const double e = MODE == GS_NONLINEAR ? prolong_value<true>(cv, C.rv, x, y, z, C.ldy, C.ldz, 0)
                                                   : prolong_value<false>(cv, nullptr, x, y, z, C.ldy, C.ldz, 0);
-            fv[p] = fv[p] + e;
+            return fv[p] + e;
         });
         __syncthreads();
         smooth(l - 1, P.post);

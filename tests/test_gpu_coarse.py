@@ -34,6 +34,7 @@ def solve_with(params, coarse_points):
 CASES = [
     # dims, mode, pre, post, threshold (points of the first level inside the launch)
     ((64, 64, 64), 0, 2, 2, 4096),
+    ((64, 64, 64), 0, 2, 2, 512),  # the default start level (8^3)
     ((64, 64, 64), 0, 2, 2, 40000),  # the 32^3 level inside the launch too
     ((31, 31, 31), 0, 3, 3, 4096),
     ((33, 31, 29), 0, 1, 0, 4096),
