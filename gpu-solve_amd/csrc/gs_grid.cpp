@@ -478,13 +478,43 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
         auto& L = grid.getLevel(i);
         auto& C = grid.getLevel(i + 1);
         static const bool noFusedRR = std::getenv("GS_NO_FUSED_RR") != nullptr;
-        if (!noFusedRR && !(L.distributed && grid.nranks() > 1)) {
-            // f^2h = R (f^h - A v^h) in one pass: the fine residual is never stored
+        // f^2h = R (f^h - A v^h) in one pass: the fine residual is never stored
+        bool fused = false;
+        if (!noFusedRR) {
             materialize(grid, i);
-            check(gs_residual_restrict(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(), L.f.data(),
-                                       L.newtonV ? L.newtonV.data() : nullptr, C.f.data(), nullptr, &C.geom, s),
-                  "gs_residual_restrict");
-        } else {
+            const double* w = L.newtonV ? L.newtonV.data() : nullptr;
+            if (!(L.distributed && grid.nranks() > 1)) {
+                check(gs_residual_restrict(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(),
+                                           L.f.data(), w, C.f.data(), nullptr, &C.geom, s),
+                      "gs_residual_restrict");
+                fused = true;
+            } else {
+                // Z-slab: this rank's coarse planes from its fine slab, whose top ghost planes are current
+                // (v after the sweep's exchange, f / newtonV after theirs); then the coarse ghosts / gather
+                // every rank must take the same branch (the ghost exchanges are collective): the slab
+                // kernel needs each rank's coarse planes over its even fine planes
+                bool slabOk = true;
+                for (int q = 0; q < grid.nranks(); q++)
+                    if (C.ranksHi[q] >= C.ranksLo[q]) slabOk = slabOk && 2 * (C.ranksLo[q] - 1) == L.ranksLo[q] - 1;
+                int64_t off = 0;
+                const gs_level cg = grid.ownedGeom(C, &off);
+                const int zhi = grid.rank() + 1 < grid.nranks();
+                // (the residual on the top ghost plane reads v two planes deep)
+                slabOk = slabOk && grid.vDepth(L) == 2 &&
+                         gs_residual_restrict_slab_supported(&grid.stencilAbi, &L.geom) != 0;
+                if (slabOk) {
+                    if (cg.nz > 0)
+                        check(gs_residual_restrict_slab(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma,
+                                                        L.v.data(), L.f.data(), w, C.f.data() + off, nullptr, &cg,
+                                                        zhi, s),
+                              "gs_residual_restrict_slab");
+                    if (transitionLevel(grid, i + 1)) grid.gather(C, C.f);
+                    else grid.halo(C, C.f, s);
+                    fused = true;
+                }
+            }
+        }
+        if (!fused) {
             compResidual(grid, i, true, false);
             restrictTo(grid, L.r, i, C.f, nullptr, true); // f^2h = R r^h (ghosts: the fused pair reads them)
         }

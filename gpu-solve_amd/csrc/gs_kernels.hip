@@ -783,7 +783,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
                                                          double* __restrict__ ca,
                                                          double* __restrict__ cb, int fnx, int fny, int fnz,
                                                          int64_t fldy, int64_t fldz, int cnx, int cnz, int64_t cldy,
-                                                         int64_t cldz, int ZC)
+                                                         int64_t cldz, int ZC, int zhi)
 {
     static_assert(MODE != GS_NEWTON || !PF, "NEWTON: newtonV rows exceed the budget of the prefetch ring");
     // wave-edge columns [parity][1 + wave][side][plane * 3 + row] of v, and r at each wave's first fine
@@ -810,8 +810,10 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
         roff[j] = (int64_t)min(max(y, 0), fny + 1) * fldy;
         rowc[j] = y >= 1 && y <= fny;
     }
+    // zhi: plane fnz+1 is an internal Z-slab boundary (current ghost planes fnz+1 of v, f, w and
+    // fnz+2 of v): the residual there is real, not the zero of a level boundary
     auto at = [&](const double* b, int j, int p) {
-        return b + xl + roff[j] + (int64_t)min(max(p, 0), fnz + 1) * fldz;
+        return b + xl + roff[j] + (int64_t)min(max(p, 0), fnz + 1 + zhi) * fldz;
     };
     // one step's operands: v planes 2Z+1 (A), 2Z+2 (B) of rows 1..3; halo rows 0 / 4 of planes 2Z (H0)
     // and 2Z+1 (H1); f of planes 2Z (F0), 2Z+1 (F1) rows 1..3
@@ -886,7 +888,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     auto resid = [&](const double2 (&Vm)[3], const double2 (&Vc)[3], const double2 (&H)[2], const double2 (&Vp)[3],
                      const double2 (&F)[3], const double2 (&W)[3], const double (&CL)[3], const double (&CR)[3], int p,
                      double2 (&R)[3]) {
-        const bool pin = p >= 1 && p <= fnz;
+        const bool pin = p >= 1 && (p <= fnz || (zhi && p == fnz + 1));
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const double2 c = Vc[j];
@@ -2184,6 +2186,20 @@ int gs_restrict2(const double* fine, const gs_level* fl, double* ca, double* cb,
 int gs_residual_restrict(const gs_stencil* S, const gs_level* fl, int mode, double gamma, const double* v,
                          const double* f, const double* w, double* ca, double* cb, const gs_level* cl, hipStream_t st)
 {
+    return gs_residual_restrict_slab(S, fl, mode, gamma, v, f, w, ca, cb, cl, 0, st);
+}
+
+int gs_residual_restrict_slab_supported(const gs_stencil* S, const gs_level* fl)
+{
+    static const bool ldsOnly = getenv("GS_RR_LDS") != nullptr;
+    return S && fl && !bad_level(fl) && valid_stencil(S) && canonical_order(S) && !ldsOnly &&
+           ((fl->nx + 1) / 2 + WAVE - 1) / WAVE <= RR2_WXMAX;
+}
+
+int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode, double gamma, const double* v,
+                              const double* f, const double* w, double* ca, double* cb, const gs_level* cl, int zhi,
+                              hipStream_t st)
+{
     if (!S || !valid_stencil(S) || !v || !f || !ca || (mode == GS_NEWTON && !w) || mode < GS_LINEAR ||
         mode > GS_NEWTON || bad_level(fl) || bad_level(cl))
         return GS_EINVAL;
@@ -2197,7 +2213,9 @@ int gs_residual_restrict(const gs_stencil* S, const gs_level* fl, int mode, doub
     const Coef k = make_coef(S, fl, 0.0, gamma);
     const int64_t wxs = ((fl->nx + 1) / 2 + WAVE - 1) / WAVE; // x-waves covering coarse columns 1..(fnx+1)/2
     static const bool ldsOnly = getenv("GS_RR_LDS") != nullptr;   // A/B switch for tools/ measurements
-    if (!ldsOnly && canonical_order(S) && zoff == 0 && wxs <= RR2_WXMAX) {
+    const bool rr2 = !ldsOnly && canonical_order(S) && zoff == 0 && wxs <= RR2_WXMAX;
+    if (zhi && !rr2) return GS_EINVAL; // the slab form exists for the register kernel only
+    if (rr2) {
         // >= 2048 blocks of one coarse row where the level has them (chunks of <= 32 coarse planes)
         const int64_t chunks = (2048 + cl->ny - 1) / cl->ny;
         int64_t zc = (cl->nz + chunks - 1) / chunks;
@@ -2205,7 +2223,7 @@ int gs_residual_restrict(const gs_stencil* S, const gs_level* fl, int mode, doub
         const dim3 g((unsigned)cl->ny, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
-#define GS_RR2(M) hipLaunchKernelGGL((k_rr2<M, false>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->nz, cl->ldy, cl->ldz, (int)zc)
+#define GS_RR2(M) hipLaunchKernelGGL((k_rr2<M, false>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
         if (mode == GS_LINEAR) GS_RR2(GS_LINEAR);
         else if (mode == GS_NONLINEAR) GS_RR2(GS_NONLINEAR);
         else GS_RR2(GS_NEWTON);

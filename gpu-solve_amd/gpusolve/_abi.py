@@ -66,6 +66,10 @@ KERNEL_API = {
     "gs_residual_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.POINTER(gs_level), C.c_void_p]),
+    "gs_residual_restrict_slab_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),
+    "gs_residual_restrict_slab": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double,
+                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.POINTER(gs_level), C.c_int, C.c_void_p]),
     "gs_restrict2": (C.c_int, [C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.c_void_p, C.POINTER(gs_level),
                                C.c_void_p]),
     "gs_interpolate": (C.c_int, [C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.POINTER(gs_level), C.c_void_p]),

@@ -138,6 +138,15 @@ int gs_sumsq_finish(const double* partials, int64_t n, double* out, int accumula
 int gs_residual_restrict(const gs_stencil* S, const gs_level* fine, int mode, double gamma, const double* v,
                          const double* f, const double* w, double* coarse_a, double* coarse_b,
                          const gs_level* coarse, hipStream_t stream);
+/* The same on a Z-slab whose top (plane fine->nz + 1) is an internal boundary when zhi != 0: the
+ * residual on that ghost plane is evaluated from the current ghost planes nz+1 of v, f, w and nz+2
+ * of v instead of being the zero of a level boundary. Coarse plane z must sit over fine plane 2z
+ * (2 coarse->z0 == fine->z0), canonical stencil, rows <= 1024 points
+ * (gs_residual_restrict_slab_supported(S, fine) != 0 and the plane condition); GS_EINVAL otherwise. */
+int gs_residual_restrict_slab_supported(const gs_stencil* S, const gs_level* fine);
+int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fine, int mode, double gamma, const double* v,
+                              const double* f, const double* w, double* coarse_a, double* coarse_b,
+                              const gs_level* coarse, int zhi, hipStream_t stream);
 int gs_restrict(const double* fine, const gs_level* fl, double* coarse, const gs_level* cl, hipStream_t stream);
 /* Same, writing two coarse outputs (FAS restV and v). */
 int gs_restrict2(const double* fine, const gs_level* fl, double* coarse_a, double* coarse_b, const gs_level* cl,

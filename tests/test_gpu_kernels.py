@@ -322,3 +322,35 @@ def test_residual_restrict_generic_stencil():
                                 C.byref(ca.level(0.2)), stream()))
     rr, _ = O.residual(v0, f0, 0.1, 0, 0.5, stencil=O.Stencil.make(vals, offs))
     np.testing.assert_array_equal(ca.to_xyz(), O.restrict(rr, cd))
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("fd,m", [((64, 33, 40), 20), ((129, 17, 30), 14), ((512, 6, 12), 6), ((33, 9, 41), 10)])
+def test_residual_restrict_slab_top_ghost(fd, m, mode):
+    """gs_residual_restrict_slab on the lower slab (local planes 1..m, m even) of a grid, zhi = 1: its
+    top ghost planes m+1, m+2 are the grid's own planes, so its coarse planes 1..m/2 must equal the
+    whole grid's gs_residual_restrict bit for bit (with zhi = 0 the top fine plane reads as a level
+    boundary instead)."""
+    rng = np.random.default_rng(sum(fd) + m + 7 * mode)
+    cd = [x // 2 for x in fd]
+    h = 1.0 / (fd[1] + 1)
+    v0, f0, w0 = rand_field(rng, *fd), rand_field(rng, *fd, 100.0), rand_field(rng, *fd)
+    S = S_abi()
+    v, f, w = dev(v0), dev(f0), dev(w0)
+    L = v.level(h)
+    ref, got = DevField(*cd), DevField(*cd)
+    Lc = ref.level(2 * h)
+    ok(k().gs_residual_restrict(C.byref(S), C.byref(L), mode, 0.7, v.ptr, f.ptr, w.ptr, ref.ptr, None, C.byref(Lc),
+                                stream()))
+    Ls = gsv.gs_level(L.nx, L.ny, m, L.ldy, L.ldz, 0, L.h)
+    Lcs = gsv.gs_level(Lc.nx, Lc.ny, m // 2, Lc.ldy, Lc.ldz, 0, Lc.h)
+    assert k().gs_residual_restrict_slab_supported(C.byref(S), C.byref(Ls)) == 1
+    ok(k().gs_residual_restrict_slab(C.byref(S), C.byref(Ls), mode, 0.7, v.ptr, f.ptr, w.ptr, got.ptr, None,
+                                     C.byref(Lcs), 1, stream()))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.to_xyz()[:, :, 1:m // 2 + 1], ref.to_xyz()[:, :, 1:m // 2 + 1])
+    # not supported for a generic stencil order
+    G = S_abi((6, -1, -1, -1, -1, -1, -1), [(0, 0, 0), (-1, 0, 0), (1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1),
+                                            (0, 0, -1)])
+    assert k().gs_residual_restrict_slab(C.byref(G), C.byref(Ls), mode, 0.7, v.ptr, f.ptr, w.ptr, got.ptr, None,
+                                         C.byref(Lcs), 1, stream()) == gsv._abi.GS_EINVAL
