@@ -759,8 +759,8 @@ __global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Residual + full weighting in registers ("rr2": canonical stencil order, LINEAR / NONLINEAR,
-// unpartitioned levels of rows <= 1024 points). A block is the whole row of coarse columns of ONE
+// Residual + full weighting in registers ("rr2": canonical stencil order, all three modes, levels
+// or Z-slabs (zhi) of rows <= 1024 points). A block is the whole row of coarse columns of ONE
 // coarse row Y (WX waves of 64 lanes; lane = coarse column X, its fine pair x = 2X-1, 2X one dwordx4)
 // and marches a chunk of coarse planes. Per coarse plane Z it evaluates the residual on fine planes 2Z
 // and 2Z+1 (2Z-1 is kept from the previous plane) for the three fine rows 2Y-1 .. 2Y+1 the 27-point sum
@@ -771,10 +771,11 @@ __global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so,
 // column (2X+1) is one more DPP shift (the right wave's lane 0 through LDS). The 27 terms are summed in
 // the reference's order (CpuSolver.cpp:225-231): 16 B of compulsory HBM reads per fine point (v, f)
 // plus 1 B of coarse writes, the residual never stored, and no LDS staging of the operands (the
-// LDS-tiled k_resrestrict, kept for the other cases, is latency-bound at 2 blocks per CU). The loads of
-// the next coarse plane are in flight while the current one is computed (two-slot ring, as in k_rb);
-// blocks go in XCD-aware order, y fastest, so the neighbouring rows that share 3 of a block's 5 v rows
-// run on the same XCD at the same time.
+// LDS-tiled k_resrestrict, kept for the other cases, is latency-bound at 2 blocks per CU). PF = true
+// keeps the next coarse plane's loads in flight (two-slot ring, as in k_rb); production runs PF =
+// false: one slot loaded per step, 154 VGPRs and 3 waves per SIMD, measured faster. Blocks go in
+// XCD-aware order, y fastest, so the neighbouring rows that share 3 of a block's 5 v rows run on the
+// same XCD at the same time.
 constexpr int RR2_WXMAX = 8;
 
 template <int MODE, bool PF> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
