@@ -133,7 +133,11 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         if (L.distributed)
             for (int q = 0; q < nranks(); q++) L.minPlanes = std::min(L.minPlanes, L.ranksHi[q] - L.ranksLo[q] + 1);
         static const bool noPairs = std::getenv("GS_NO_FUSED_SWEEPS") != nullptr;
-        L.fusedPairs = !noPairs && gs_jacobi_sweep2_supported(&stencilAbi, &L.geom) == 2 &&
+        // rank-uniform on a Z-slab level (the smoothing schedule decides the ghost exchanges): judged
+        // on the thinnest slab, as the kernel's fill count grows with the plane count
+        gs_level thin = L.geom;
+        thin.nz = L.minPlanes;
+        L.fusedPairs = !noPairs && gs_jacobi_sweep2_supported(&stencilAbi, &thin) == 2 &&
                        (!L.distributed || L.minPlanes >= 2);
     }
     // The coarse end of the V-cycle runs as one gs_coarse_cycle launch from the first level of at
@@ -255,6 +259,27 @@ int64_t pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_
     return partials ? gs_jacobi_sweep2_num_partials(&g.stencilAbi, &sub, (int)g.mode) : 0;
 }
 
+// The first post-smoothing pair of v^h + P v^2h (gs_jacobi_sweep2_prolong) on planes z1..z2 of F
+// into F.vAlt. Every plane range starts on an odd plane (the kernel's parities are global ones) and
+// ends two planes below the level's top or on it: the planes past an internal range end are
+// interior planes (or a neighbour's ghost copies), which the kernel corrects as it reads them.
+void proPlanes(HipGridData& g, HipGridData::LevelData& F, HipGridData::LevelData& C, int64_t z1, int64_t z2,
+               hipStream_t s)
+{
+    if (z2 < z1) return;
+    gs_level sub = F.geom;
+    sub.nz = z2 - z1 + 1;
+    sub.z0 += z1 - 1;
+    const int64_t off = (z1 - 1) * F.geom.ldz;
+    const bool dist = F.distributed && g.nranks() > 1;
+    const int zlo = z1 > 1 || (dist && g.rank() > 0);
+    const int zhi = z2 < F.geom.nz || (dist && g.rank() + 1 < g.nranks());
+    check(gs_jacobi_sweep2_prolong(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, F.v.data() + off, C.v.data(),
+                                   nullptr, &C.geom, F.vAlt.data() + off, F.f.data() + off,
+                                   F.newtonV ? F.newtonV.data() + off : nullptr, zlo, zhi, s),
+          "gs_jacobi_sweep2_prolong");
+}
+
 bool transitionLevel(HipGridData& g, std::size_t l)
 {
     return l > 0 && g.nranks() > 1 && !g.getLevel(l).distributed && g.getLevel(l - 1).distributed;
@@ -342,6 +367,23 @@ double HipSolver::compResidual(HipGridData& grid, std::size_t l, bool storeR, bo
     if (storeR) grid.halo(L, L.r, s);
     if (!norm) return 0.0;
     return finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L.geom));
+}
+
+// Whether level l's first post-smoothing pair can take the prolongation from level l+1 (rank-uniform:
+// the pair's ghost exchange is collective). A Z-slab level needs every slab to start on an even global
+// plane (the kernel's plane parities) and, under a Z-slab coarse level, each rank's coarse planes over
+// its fine ones with two coarse ghost planes (the bottom ghost fine plane interpolates from coarse
+// plane -1); a replicated coarse level holds every plane.
+static bool proSlabOk(HipGridData& grid, std::size_t l)
+{
+    auto& F = grid.getLevel(l);
+    auto& C = grid.getLevel(l + 1);
+    if (!(F.distributed && grid.nranks() > 1)) return true;
+    for (int q = 0; q < grid.nranks(); q++) {
+        if ((F.ranksLo[q] - 1) % 2 != 0) return false;
+        if (C.distributed && 2 * (C.ranksLo[q] - 1) != F.ranksLo[q] - 1) return false;
+    }
+    return !C.distributed || grid.vDepth(C) == 2;
 }
 
 // k sweeps (src/cpu/CpuSolver.cpp:141-180). Each reads v and writes vAlt, then the two swap. Where
@@ -538,16 +580,32 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
         auto& F = grid.getLevel(i - 1);
         materialize(grid, i); // only if the level had no sweep at all
         static const bool noFusedPro = std::getenv("GS_NO_FUSED_PROLONG") != nullptr;
-        if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && !(F.distributed && grid.nranks() > 1) &&
+        if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && proSlabOk(grid, i - 1) &&
             gs_jacobi_sweep2_prolong_supported(&grid.stencilAbi, &F.geom, (int)grid.mode)) {
             // the first two post-smoothing sweeps of v^h + P v^2h in one pass (the corrected
-            // iterate is never stored), then the remaining ones
+            // iterate is never stored), then the remaining ones. On a Z-slab each rank corrects its
+            // ghost planes itself, from the coarse planes under them, and the pair's outermost planes
+            // go first so that their exchange overlaps the interior (as in jacobi())
             materialize(grid, i - 1);
-            check(gs_jacobi_sweep2_prolong(&grid.stencilAbi, &F.geom, (int)grid.mode, grid.omega, grid.gamma,
-                                           F.v.data(), C.v.data(), nullptr, &C.geom, F.vAlt.data(), F.f.data(),
-                                           F.newtonV ? F.newtonV.data() : nullptr, s),
-                  "gs_jacobi_sweep2_prolong");
+            const int64_t nz = F.geom.nz;
+            if (!(F.distributed && grid.nranks() > 1)) {
+                proPlanes(grid, F, C, 1, nz, s);
+            } else if (grid.overlapHalo && nz >= 5) {
+                const int64_t zt = nz % 2 == 0 ? nz - 1 : nz - 2; // odd start: 2 or 3 top planes
+                proPlanes(grid, F, C, 1, 2, s);
+                proPlanes(grid, F, C, zt, nz, s);
+                check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
+                check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
+                grid.comm()->halo(F.vAlt.data(), F.vAlt.ldz(), nz, grid.vDepth(F), grid.commStream());
+                check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+                proPlanes(grid, F, C, 3, zt - 1, s);
+                check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
+            } else {
+                proPlanes(grid, F, C, 1, nz, s);
+                grid.comm()->halo(F.vAlt.data(), F.vAlt.ldz(), nz, grid.vDepth(F), s);
+            }
             F.v.swap(F.vAlt);
+            F.vZero = false;
             jacobi(grid, i - 1, grid.postSmoothing - 2);
             continue;
         }

@@ -1598,7 +1598,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     double2 W0[NCR], W1[NCR];        // X-pass values of coarse planes K, K+1
     double RA[NCR], RB[NCR], SA[NCR], SB[NCR]; // raw c (and sub) of plane K+2, in flight
     auto craw = [&](int cz) {
-        const int64_t zo = (int64_t)min(max(cz, 0), cnz + 1) * cldz + cxl;
+        // coarse planes -1 .. cnz+2 exist in the layout; only those under corrected fine planes matter
+        const int64_t zo = (int64_t)min(max(cz, -1), cnz + 2) * cldz + cxl;
 #pragma unroll
         for (int r = 0; r < NCR; r++) {
             RA[r] = pc[zo + crow[r]];
@@ -1639,6 +1640,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             if (okx1) val.y = val.y + e.y;
         }
     };
+    // a fine plane gets the correction when it is interior or a ghost plane of an internal slab side
+    auto pok = [&](int p) { return (p >= 1 && p <= nz) || (zlo && p <= 0) || (zhi && p > nz); };
     if (PRO) {
         const int m0 = (zb - 1) >> 1; // zb is odd: planes zb-2 = 2 m0 - 1, zb - 1 = 2 m0
         double2 Wm[NCR];
@@ -1651,8 +1654,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         auto pro_init = [&](auto mirc) {
 #pragma unroll
             for (int j = 0; j < NV; j++) {
-                correct(Vp[j], j, true, zb - 2 >= 1, Wm, W0, mirc);
-                correct(Vc[j], j, false, zb - 1 >= 1, W0, W0, mirc);
+                correct(Vp[j], j, true, pok(zb - 2), Wm, W0, mirc);
+                correct(Vc[j], j, false, pok(zb - 1), W0, W0, mirc);
             }
         };
         if (mir) pro_init(BoolC<true>{});
@@ -1706,8 +1709,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                     // even, ph 0 has z even (z+1 odd: coarse K, K+1) and ph 1 has z odd
 #pragma unroll
                     for (int j = 0; j < NV; j++)
-                        correct(VL[cs][j], j, ph == 0, z + 1 <= nz, ph == 0 ? W0 : W1, W1, mirc);
-                    correct(HL[cs], -1, ph == 1, z >= 1 && z <= nz, W0, W1, mirc);
+                        correct(VL[cs][j], j, ph == 0, pok(z + 1), ph == 0 ? W0 : W1, W1, mirc);
+                    correct(HL[cs], -1, ph == 1, pok(z), W0, W1, mirc);
                 }
                 // sweep 1 at plane z, local rows 0..RY
 #pragma unroll
@@ -2123,24 +2126,30 @@ int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, i
     // LINEAR only: the NEWTON variant (newtonV rows on top of the coarse planes) spills 240 B per lane
     // (measured 3.0 ms per 512^3 launch against 1.54 ms for gs_prolong_add + the pair) and the
     // NONLINEAR one carries restV too
-    return !bad_level(L) && valid_stencil(S) && mode == GS_LINEAR && L->z0 == 0 &&
+    // the fine planes' parities must be the global ones (even z0): they select each plane's combination
+    return !bad_level(L) && valid_stencil(S) && mode == GS_LINEAR && L->z0 % 2 == 0 &&
            tb2_plan(S, L, &zc, &g, &b, &y2, mode) && y2;
 }
 
 int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                              const double* v_in, const double* coarse_v, const double* coarse_sub, const gs_level* cl,
-                             double* v_out, const double* f, const double* w, hipStream_t st)
+                             double* v_out, const double* f, const double* w, int zlo, int zhi, hipStream_t st)
 {
     int zc;
     dim3 g, b;
     bool y2 = false;
-    if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || bad_level(cl) || cl->z0 != 0 || !v_in || !coarse_v ||
+    // coarse plane of fine local plane z: (z >> 1) + czoff, z0 even (a slab, or a plane range of one)
+    const int64_t czoff = cl ? L->z0 / 2 - cl->z0 : 0;
+    if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || bad_level(cl) || czoff < 0 || !v_in || !coarse_v ||
         !v_out || !f || v_in == v_out || (mode == GS_NONLINEAR) != (coarse_sub != nullptr) || (mode == GS_NEWTON && !w) ||
-        (L->nx + 1) / 2 > cl->nx + 1 || (L->ny + 1) / 2 > cl->ny + 1 || (L->nz + 1) / 2 > cl->nz + 1 ||
+        (L->nx + 1) / 2 > cl->nx + 1 || (L->ny + 1) / 2 > cl->ny + 1 || (L->nz + 1) / 2 + czoff > cl->nz + 1 ||
         !tb2_plan(S, L, &zc, &g, &b, &y2, mode))
         return GS_EINVAL;
+    // the kernel indexes the coarse field from the plane under fine local plane 0
+    coarse_v += czoff * cl->ldz;
+    if (coarse_sub) coarse_sub += czoff * cl->ldz;
     const Coef k = make_coef(S, L, omega, gamma);
-#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, false, true, P>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, 0, 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz)
+#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, false, true, P>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz)
     GS_TBP(GS_LINEAR, 1);
 #undef GS_TBP
     return launch_status();

@@ -212,9 +212,55 @@ def test_prolong_fused_pair_bit_identical(shape, mode):
     # fused
     v2, out = DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz)
     ok(k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v2.ptr, c.ptr, None,
-                                    C.byref(Lc), out.ptr, f.ptr, wp, st()))
+                                    C.byref(Lc), out.ptr, f.ptr, wp, 0, 0, st()))
     np.testing.assert_array_equal(out.to_xyz(), out_ref.to_xyz())
     np.testing.assert_array_equal(v2.to_xyz(), v0)  # the input iterate is left as it was
+
+
+# plane ranges as the Z-slab driver launches them (HipSolver::vcycleSpeculative: bottom pair, top
+# planes, interior): odd first planes; an internal range end lies two planes below the top or on it
+PRO_SPLITS = [((64, 64, 64), [(1, 2), (63, 64), (3, 62)]),
+              ((63, 31, 65), [(1, 2), (63, 65), (3, 62)]),  # odd extent: three top planes
+              ((200, 33, 70), [(1, 14), (15, 40), (41, 70)]),
+              ((5, 4, 33), [(1, 2), (3, 30), (31, 33)]),
+              ((127, 9, 17), [(1, 1), (2, 2), (1, 2), (3, 14), (15, 17), (17, 17)])]  # (2, 2): even start, refused
+
+
+@pytest.mark.parametrize("coarse_view", [False, True])
+@pytest.mark.parametrize("shape,ranges", PRO_SPLITS)
+def test_prolong_fused_pair_plane_ranges(shape, ranges, coarse_view):
+    """gs_jacobi_sweep2_prolong on plane ranges (z0 > 0, internal sides flagged zlo / zhi, whose
+    planes the kernel corrects as it reads them) assembles the whole-level result bit for bit. With
+    coarse_view the coarse level is passed as the plane range under the fine one (a Z-slab coarse
+    level: coarse z0 = fine z0 / 2, its ghost plane -1 read), else whole (a replicated coarse level)."""
+    rng = np.random.default_rng(sum(shape) * 7 + coarse_view)
+    nx, ny, nz = shape
+    cd = [x // 2 for x in shape]
+    h = 1.0 / (ny + 1)
+    v0, f0, c0 = rand_full(rng, *shape), rand_full(rng, *shape, 100.0), rand_full(rng, *cd)
+    L = DevField(nx, ny, nz).level(h)
+    v, f, c, out_ref = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
+                        DevField(*cd).from_xyz(c0), DevField(nx, ny, nz))
+    Lc = c.level(2 * h)
+    ok(k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, c.ptr, None, C.byref(Lc),
+                                    out_ref.ptr, f.ptr, None, 0, 0, st()))
+    out = DevField(nx, ny, nz)
+    for z1, z2 in ranges:
+        off = 8 * (z1 - 1) * L.ldz
+        sub = gsv._abi.gs_level(nx, ny, z2 - z1 + 1, L.ldy, L.ldz, z1 - 1, h)
+        cptr, cl = c.ptr, Lc
+        if coarse_view and z1 % 2 == 1:
+            z0c = (z1 - 1) // 2
+            cptr = c.ptr + 8 * z0c * Lc.ldz
+            cl = gsv._abi.gs_level(Lc.nx, Lc.ny, min((z2 - z1 + 2) // 2, cd[2] - z0c), Lc.ldy, Lc.ldz, z0c, 2 * h)
+        rc = k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(sub), 0, 0.8, 1.0, v.ptr + off, cptr, None,
+                                          C.byref(cl), out.ptr + off, f.ptr + off, None, int(z1 > 1), int(z2 < nz),
+                                          st())
+        if z1 % 2 == 0:
+            assert rc == gsv._abi.GS_EINVAL  # plane parities must be the global ones
+        else:
+            ok(rc)
+    np.testing.assert_array_equal(out.to_xyz(), out_ref.to_xyz())
 
 
 def test_prolong_fused_pair_rejects():
@@ -223,7 +269,7 @@ def test_prolong_fused_pair_rejects():
     assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), 2) == 0  # NEWTON
     f, out, c = DevField(16, 16, 16), DevField(16, 16, 16), DevField(8, 8, 8)
     rc = k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), 2, 0.8, 1.0, f.ptr, c.ptr, None,
-                                      C.byref(c.level(1 / 9.0)), out.ptr, f.ptr, None, st())
+                                      C.byref(c.level(1 / 9.0)), out.ptr, f.ptr, None, 0, 0, st())
     assert rc == gsv._abi.GS_EINVAL  # NEWTON needs newtonV
     L2 = DevField(600, 4, 4).level(0.2)
     assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 0) == 0  # rows > 512

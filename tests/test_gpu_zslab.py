@@ -75,3 +75,22 @@ def test_example_config_distributed(histories):
     assert len(h) == len(ref)
     for a, b in zip(h, ref):
         assert rel(a, b) < 1e-6
+
+
+@pytest.mark.parametrize("dims,nranks,min_points,pre,post", [
+    ((64, 128, 128), 2, -1, 2, 2),   # even slabs on every level: the fused prolongation pair throughout
+    ((64, 128, 127), 2, -1, 1, 3),   # odd top slab (three top planes first), a single sweep after the pair
+    ((48, 96, 130), 2, -1, 2, 2),    # slab of 65 planes: odd z0, the unfused path
+    ((32, 64, 96), 3, 4096, 3, 2),   # replicated coarse levels under Z-slab ones
+    ((40, 64, 20), 4, -1, 2, 2),     # thin slabs: no overlap, one exchange after the pair
+])
+def test_fused_prolong_slabs_match_single_gpu(dims, nranks, min_points, pre, post):
+    """The first post-smoothing pair fused with the prolongation on Z-slab levels (each rank corrects
+    its ghost planes from the coarse planes under them) leaves every field as on one GPU."""
+    p = gsv.GridParams(maxiter=4, tol=0.0, gridDim=dims, mode=0, preSmoothing=pre, postSmoothing=post)
+    ref_h, ref_v = single(p, 0, True)
+    h, v = loopback(p, nranks, min_points, 0, True)
+    assert len(h) == len(ref_h)
+    for a, b in zip(h, ref_h):
+        assert rel(a, b) < 1e-12, (a, b)
+    np.testing.assert_array_equal(v[:, :, 1:-1], ref_v[:, :, 1:-1])
