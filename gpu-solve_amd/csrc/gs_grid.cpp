@@ -386,6 +386,20 @@ static bool proSlabOk(HipGridData& grid, std::size_t l)
     return !C.distributed || grid.vDepth(C) == 2;
 }
 
+// NEWTON's fused prolongation pair keeps part of its state in LDS and recomputes exp(newtonV) for
+// its second sweep: on 512^3 it saves 0.14 ms per V-cycle against gs_prolong_add + the plain pair, on
+// 256^3 / 128^3 it costs 0.065 / 0.05 ms more (profiles/r01l_summary.md), so NEWTON levels take it
+// from GS_NEWTON_PRO_POINTS (default 2^26) points per rank on (judged on the thinnest slab: rank-
+// uniform). LINEAR levels always do.
+static bool proWorthIt(HipGridData& grid, std::size_t l)
+{
+    if (grid.mode != GridParams::NEWTON) return true;
+    const char* e = std::getenv("GS_NEWTON_PRO_POINTS"); // read per call: tests switch it
+    const int64_t minPoints = e ? std::strtoll(e, nullptr, 10) : (int64_t)1 << 26;
+    const auto& F = grid.getLevel(l);
+    return (int64_t)F.levelDim[0] * (int64_t)F.levelDim[1] * F.minPlanes >= minPoints;
+}
+
 // k sweeps (src/cpu/CpuSolver.cpp:141-180). Each reads v and writes vAlt, then the two swap. Where
 // the level allows, sweeps run in fused pairs (gs_jacobi_sweep2: one read of v and f, one write, for
 // two sweeps), an odd one as a single sweep. On a Z-slab the outermost planes (one per side for a
@@ -580,7 +594,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
         auto& F = grid.getLevel(i - 1);
         materialize(grid, i); // only if the level had no sweep at all
         static const bool noFusedPro = std::getenv("GS_NO_FUSED_PROLONG") != nullptr;
-        if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && proSlabOk(grid, i - 1) &&
+        if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && proWorthIt(grid, i - 1) && proSlabOk(grid, i - 1) &&
             gs_jacobi_sweep2_prolong_supported(&grid.stencilAbi, &F.geom, (int)grid.mode)) {
             // the first two post-smoothing sweeps of v^h + P v^2h in one pass (the corrected
             // iterate is never stored), then the remaining ones. On a Z-slab each rank corrects its

@@ -1570,6 +1570,12 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 
     double2 Vp[NV], Vc[NV], VL[2][NV], FL[2][NV], WL[2][NV], HL[2];
     double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
+    // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes them from
+    // the newtonV rows at z-1 (same expressions, same values)
+    constexpr bool RECOMP = MODE == GS_NEWTON && PRO != 0;
+    // (Wprev, Fprev: sweep 2's newtonV / f rows at z-1, in LDS like the coarse rows below)
+    __shared__ double2 wprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
+    __shared__ double2 fprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
 #pragma unroll
     for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
 #pragma unroll
@@ -1595,7 +1601,18 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     int64_t crow[NCR];
 #pragma unroll
     for (int r = 0; r < NCR; r++) crow[r] = (int64_t)min(max(cyb + r, 0), cny + 1) * cldy;
-    double2 W0[NCR], W1[NCR];        // X-pass values of coarse planes K, K+1
+    double2 W0[NCR], W1[NCR], Wm[NCR]; // X-pass values of coarse planes K, K+1 (Wm: K-1, first step)
+    // NEWTON (RECOMP): the X-pass rows of planes K, K+1 live in LDS, slot wsl / wsl^1 — each lane
+    // reads back only what it wrote, so no barrier; this keeps the variant inside 256 VGPRs
+    __shared__ double2 wlds[RECOMP ? 2 : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? NCR : 1][RECOMP ? WAVE : 1];
+    int wsl = 0;
+    const int wid_l = RECOMP ? wx + WX * wy : 0;
+    // coarse X-pass row r of plane slot s (0: K, 1: K+1, 2: K-1 on the first step)
+    auto wget = [&](int s, int r) -> double2 {
+        if (s == 2) return Wm[r];
+        if constexpr (RECOMP) return wlds[s ^ wsl][wid_l][r][lane];
+        else return s == 0 ? W0[r] : W1[r];
+    };
     double RA[NCR], RB[NCR], SA[NCR], SB[NCR]; // raw c (and sub) of plane K+2, in flight
     auto craw = [&](int cz) {
         // coarse planes -1 .. cnz+2 exist in the layout; only those under corrected fine planes matter
@@ -1611,28 +1628,33 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         }
     };
     // X pass of gs_prolong_add: e(x odd) = 0.5 a + 0.5 b, e(x+1 even) = b, a / b = c(cx) / c(cx+1)
-    auto xpass = [&](double2 (&X)[NCR]) {
+    auto xpass = [&](int s) {
 #pragma unroll
         for (int r = 0; r < NCR; r++) {
             const double a = PRO == 2 ? RA[r] - SA[r] : RA[r], b = PRO == 2 ? RB[r] - SB[r] : RB[r];
-            X[r] = make_double2(0.5 * a + 0.5 * b, b);
+            const double2 X = make_double2(0.5 * a + 0.5 * b, b);
+            if (s == 2) Wm[r] = X;
+            else if constexpr (RECOMP) wlds[s ^ wsl][wid_l][r][lane] = X;
+            else if (s == 0) W0[r] = X;
+            else W1[r] = X;
         }
     };
     // the correction of local row j on a plane whose coarse neighbours are Wa (and Wb when the fine
     // plane is odd), Y pass then Z pass; added where the fine point is interior
-    auto correct = [&](double2& val, int j, bool zodd, bool zin, const double2 (&Wa)[NCR], const double2 (&Wb)[NCR],
-                       auto mirc) {
+    auto correct = [&](double2& val, int j, bool zodd, bool zin, int sa, int sb, auto mirc) {
         constexpr bool M = decltype(mirc)::get();
         const int u = M ? 2 * RY + 1 - j : j + 2; // fine row = 2 (coarse base) + u
         const int ri = M ? (u >> 1) - RY / 2 : (u >> 1);
         const bool yodd = u & 1;
-        auto ypass = [&](const double2 (&X)[NCR]) {
-            if (!yodd) return X[ri];
-            return make_double2(0.5 * X[ri].x + 0.5 * X[ri + 1].x, 0.5 * X[ri].y + 0.5 * X[ri + 1].y);
+        auto ypass = [&](int s) {
+            const double2 X0 = wget(s, ri);
+            if (!yodd) return X0;
+            const double2 X1 = wget(s, ri + 1);
+            return make_double2(0.5 * X0.x + 0.5 * X1.x, 0.5 * X0.y + 0.5 * X1.y);
         };
-        double2 e = ypass(Wa);
+        double2 e = ypass(sa);
         if (zodd) {
-            const double2 g = ypass(Wb);
+            const double2 g = ypass(sb);
             e = make_double2(0.5 * e.x + 0.5 * g.x, 0.5 * e.y + 0.5 * g.y);
         }
         if (zin && rowc[j + 1]) {
@@ -1644,18 +1666,17 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     auto pok = [&](int p) { return (p >= 1 && p <= nz) || (zlo && p <= 0) || (zhi && p > nz); };
     if (PRO) {
         const int m0 = (zb - 1) >> 1; // zb is odd: planes zb-2 = 2 m0 - 1, zb - 1 = 2 m0
-        double2 Wm[NCR];
         craw(m0 - 1);
-        xpass(Wm);
+        xpass(2);
         craw(m0);
-        xpass(W0);
+        xpass(0);
         craw(m0 + 1);
-        xpass(W1);
+        xpass(1);
         auto pro_init = [&](auto mirc) {
 #pragma unroll
             for (int j = 0; j < NV; j++) {
-                correct(Vp[j], j, true, pok(zb - 2), Wm, W0, mirc);
-                correct(Vc[j], j, false, pok(zb - 1), W0, W0, mirc);
+                correct(Vp[j], j, true, pok(zb - 2), 2, 0, mirc);
+                correct(Vc[j], j, false, pok(zb - 1), 0, 0, mirc);
             }
         };
         if (mir) pro_init(BoolC<true>{});
@@ -1709,8 +1730,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                     // even, ph 0 has z even (z+1 odd: coarse K, K+1) and ph 1 has z odd
 #pragma unroll
                     for (int j = 0; j < NV; j++)
-                        correct(VL[cs][j], j, ph == 0, pok(z + 1), ph == 0 ? W0 : W1, W1, mirc);
-                    correct(HL[cs], -1, ph == 1, pok(z), W0, W1, mirc);
+                        correct(VL[cs][j], j, ph == 0, pok(z + 1), ph == 0 ? 0 : 1, 1, mirc);
+                    correct(HL[cs], -1, ph == 1, pok(z), 0, 1, mirc);
                 }
                 // sweep 1 at plane z, local rows 0..RY
 #pragma unroll
@@ -1728,7 +1749,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         const double2 wv = WL[cs][j];
                         const double2 A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
                         const double2 E = make_double2(exp(wv.x), exp(wv.y));
-                        if (j >= 1) {
+                        if (!RECOMP && j >= 1) {
                             Acur[j - 1] = A;
                             Ecur[j - 1] = E;
                         }
@@ -1765,11 +1786,20 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         div_hh_row<MODE>(k, q);
                         double o0, o1;
                         if constexpr (MODE == GS_NEWTON) {
-                            const double2 A = Aprev[j - 1], E = Eprev[j - 1];
+                            double2 A, E;
+                            if constexpr (RECOMP) {
+                                const double2 wv = wprev_l[j - 1][wx + WX * wy][lane];
+                                A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
+                                E = make_double2(exp(wv.x), exp(wv.y));
+                            } else {
+                                A = Aprev[j - 1];
+                                E = Eprev[j - 1];
+                            }
                             const double a0 = newton_op(q[0], c.x, A.x, E.x);
                             const double a1 = newton_op(q[1], c.y, A.y, E.y);
-                            o0 = newton_update(k, c.x, Fprev[j - 1].x - a0, A.x, E.x);
-                            o1 = newton_update(k, c.y, Fprev[j - 1].y - a1, A.y, E.y);
+                            const double2 fp = RECOMP ? fprev_l[j - 1][wx + WX * wy][lane] : Fprev[j - 1];
+                            o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
+                            o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
                         } else {
                             const double a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                             const double a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
@@ -1794,8 +1824,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 #pragma unroll
             for (int j = 1; j <= RY; j++) {
                 V1p[j - 1] = V1c[j];
-                Fprev[j - 1] = FL[cs][j];
-                if (MODE == GS_NEWTON) {
+                if (!RECOMP) Fprev[j - 1] = FL[cs][j];
+                if constexpr (RECOMP) {
+                    wprev_l[j - 1][wx + WX * wy][lane] = WL[cs][j];
+                    fprev_l[j - 1][wx + WX * wy][lane] = FL[cs][j];
+                } else if (MODE == GS_NEWTON) {
                     Aprev[j - 1] = Acur[j - 1];
                     Eprev[j - 1] = Ecur[j - 1];
                 }
@@ -1807,9 +1840,13 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                 Vc[j] = VL[cs][j];
             }
             if (PRO && ph == 1) { // next step: coarse planes K+1, K+2
+                if constexpr (RECOMP) {
+                    wsl ^= 1;
+                } else {
 #pragma unroll
-                for (int r = 0; r < NCR; r++) W0[r] = W1[r];
-                xpass(W1);
+                    for (int r = 0; r < NCR; r++) W0[r] = W1[r];
+                }
+                xpass(1);
             }
         }
     }
@@ -2127,7 +2164,7 @@ int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, i
     // (measured 3.0 ms per 512^3 launch against 1.54 ms for gs_prolong_add + the pair) and the
     // NONLINEAR one carries restV too
     // the fine planes' parities must be the global ones (even z0): they select each plane's combination
-    return !bad_level(L) && valid_stencil(S) && mode == GS_LINEAR && L->z0 % 2 == 0 &&
+    return !bad_level(L) && valid_stencil(S) && (mode == GS_LINEAR || mode == GS_NEWTON) && L->z0 % 2 == 0 &&
            tb2_plan(S, L, &zc, &g, &b, &y2, mode) && y2;
 }
 
@@ -2149,8 +2186,9 @@ int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, d
     coarse_v += czoff * cl->ldz;
     if (coarse_sub) coarse_sub += czoff * cl->ldz;
     const Coef k = make_coef(S, L, omega, gamma);
-#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, false, true, P>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz)
-    GS_TBP(GS_LINEAR, 1);
+#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, false, true, P>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz)
+    if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1);
+    else GS_TBP(GS_LINEAR, 1);
 #undef GS_TBP
     return launch_status();
 }

@@ -110,12 +110,12 @@ int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L, in
  * trilinear interpolation of gs_prolong_add; bit-identical to gs_prolong_add followed by
  * gs_jacobi_sweep2, with the corrected iterate never stored. Replaces CpuSolver.cpp:127-135
  * (interpolate, v += e, jacobi(post)) for the first two post-smoothing sweeps. Supported
- * (gs_jacobi_sweep2_prolong_supported != 0) for LINEAR levels of rows <= 512 points whose z0 is even
- * (a level, a Z-slab of one, or a plane range of either); coarse_sub must then be NULL. Fine local
+ * (gs_jacobi_sweep2_prolong_supported != 0) for LINEAR and NEWTON levels of rows <= 512 points whose
+ * z0 is even (a level, a Z-slab of one, or a plane range of either); coarse_sub must then be NULL. Fine local
  * plane z interpolates from coarse planes (z + z0) / 2 - coarse->z0 (+1); zlo / zhi as for
  * gs_jacobi_sweep2 — the ghost planes of an internal side are corrected too, from the coarse field's
- * planes under them (coarse ghost planes -1 / nz+1 must then be current). w: the level's newtonV for
- * a NEWTON level (not supported yet: that variant exceeds the register budget), else ignored. */
+ * planes under them (coarse ghost planes -1 / nz+1 must then be current). w: the level's newtonV
+ * for a NEWTON level, else ignored. */
 int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, int mode);
 int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                              const double* v_in, const double* coarse_v, const double* coarse_sub,

@@ -186,7 +186,7 @@ PRO_SHAPES = [(1, 1, 1), (2, 5, 3), (5, 4, 33), (127, 9, 17), (128, 8, 8), (129,
               (500, 7, 9), (512, 4, 5), (64, 64, 64), (63, 31, 65), (200, 33, 70)]
 
 
-@pytest.mark.parametrize("mode", [0])  # NEWTON: unsupported (register budget), see the rejects test
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("shape", PRO_SHAPES)
 def test_prolong_fused_pair_bit_identical(shape, mode):
     """gs_jacobi_sweep2_prolong == gs_prolong_add then gs_jacobi_sweep2, bit for bit (LINEAR and NEWTON,
@@ -266,7 +266,7 @@ def test_prolong_fused_pair_plane_ranges(shape, ranges, coarse_view):
 def test_prolong_fused_pair_rejects():
     L = DevField(16, 16, 16).level(1 / 17.0)
     assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), 1) == 0  # NONLINEAR
-    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), 2) == 0  # NEWTON
+    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), 2) == 1  # NEWTON
     f, out, c = DevField(16, 16, 16), DevField(16, 16, 16), DevField(8, 8, 8)
     rc = k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), 2, 0.8, 1.0, f.ptr, c.ptr, None,
                                       C.byref(c.level(1 / 9.0)), out.ptr, f.ptr, None, 0, 0, st())
