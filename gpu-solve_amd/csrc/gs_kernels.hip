@@ -1520,7 +1520,8 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
 // is consumed (the loads stay in flight as before): X-pass values of the two coarse planes under the
 // current fine planes live in registers (W0, W1) and the next coarse plane is prefetched one step
 // ahead; the z-chunk is even, so every fine plane's parity, hence its Y/Z combination, is static.
-template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0>
+template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0,
+          int PFD = 1>
 __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* __restrict__ v,
                                                            const double* __restrict__ f, const double* __restrict__ w,
                                                            double* __restrict__ out, double* __restrict__ partials,
@@ -1568,7 +1569,12 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     auto planeok = [&](int z) { return (z >= 1 && z <= nz) || (z == 0 && zlo) || (z == nz + 1 && zhi); };
     auto at = [&](const double* base, int j, int z) { return base + xl + roff[j + 1] + (int64_t)z * ldz; };
 
-    double2 Vp[NV], Vc[NV], VL[2][NV], FL[2][NV], WL[2][NV], HL[2];
+    // PFD: prefetch distance in plane steps. 1: two operand slots (this step's, the next one's in
+    // flight); 2: four named slots, three live (this step's and the next two in flight), the z loop
+    // unrolled by 4 so every slot index is static
+    static_assert(PFD == 1 || PFD == 2, "prefetch distance 1 or 2");
+    constexpr int NS = PFD == 2 ? 4 : 2, UNR = PFD == 2 ? 4 : 2;
+    double2 Vp[NV], Vc[NV], VL[NS][NV], FL[NS][NV], WL[NS][NV], HL[NS];
     double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
     // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes them from
     // the newtonV rows at z-1 (same expressions, same values)
@@ -1682,14 +1688,23 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         if (mir) pro_init(BoolC<true>{});
         else pro_init(BoolC<false>{});
     }
-    load_slot(1, zb - 1, zb);
+    if (PFD == 1) {
+        load_slot(1, zb - 1, zb);
+    } else {
+        load_slot(0, zb - 1, zb);
+        load_slot(1, zb, zb + 1);
+    }
     double sumsq = 0.0;
-    for (int z0 = zb - 1; z0 <= ze + 1; z0 += 2) {
+    for (int z0 = zb - 1; z0 <= ze + 1; z0 += UNR) {
 #pragma unroll
-        for (int ph = 0; ph < 2; ph++) {
-            const int z = z0 + ph;
-            const int cs = ph ^ 1;
-            load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
+        for (int ph4 = 0; ph4 < UNR; ph4++) {
+            // the last two steps of a 4-step round are skipped past the chunk (uniform branch)
+            if (UNR == 4 && ph4 == 2 && z0 + 2 > ze + 1) break;
+            const int ph = ph4 & 1; // plane parity (z0 is even): LDS double buffers, PRO combinations
+            const int z = z0 + ph4;
+            const int cs = PFD == 1 ? ph ^ 1 : ph4; // slot holding this step's operands
+            if (PFD == 1) load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
+            else load_slot((ph4 + 2) & 3, min(z + 2, nz + 1), min(z + 3, nz + 2));
             if (PRO && ph == 0) craw((z >> 1) + 2); // consumed at the end of the next step
             // ---- publish: x-edge columns (v(z) rows 0..RY, sweep-1(z-1) rows 1..RY) and the y-edge row
             if (lane == 0) {
@@ -1871,6 +1886,10 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 // a wave needs ~216 VGPRs, so two waves share a SIMD and hide each other's latency, which beats the
 // lower halo overhead of 3-6 rows at one wave per SIMD by 20-25%).
 constexpr int TBY_RY = 2, TBY_RY_NEWTON = 2, TBY_WX = 4, TB_RY_B = 2, TB_WX_B = 8;
+// prefetch distance of k_tb2y (plane steps): LINEAR keeps two steps in flight (215 VGPRs, still two
+// waves per SIMD; 0.662 vs 0.673 ms per 512^3 pair, profiles/r01m_summary.md), the other modes and
+// the fused prolongation one (VGPR budget: the LINEAR prolongation pair at distance 2 spills)
+constexpr int tby_pfd(int mode) { return mode == GS_LINEAR ? 2 : 1; }
 
 // Geometry rule of the fused pair: the whole x-row in one block and enough work for >= 512 blocks of
 // 4-plane chunks; the z-chunk is then chosen for >= 1024 blocks (4..64 planes: at 512^3, 64-plane
@@ -2133,7 +2152,7 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
 #define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
-#define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M)>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
     const bool zv = !v_in;
     if (y2) {
         if (mode == GS_LINEAR) {
@@ -2186,7 +2205,7 @@ int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, d
     coarse_v += czoff * cl->ldz;
     if (coarse_sub) coarse_sub += czoff * cl->ldz;
     const Coef k = make_coef(S, L, omega, gamma);
-#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, false, true, P>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz)
+#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, false, true, P, 1>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz)
     if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1);
     else GS_TBP(GS_LINEAR, 1);
 #undef GS_TBP
@@ -2458,7 +2477,9 @@ const PairVariant kPairVariants[] = {GS_PVF(2, 4),
                                      GS_PVY(3, false, false, " f-cached"),
                                      GS_PVY(2, false, true, " f-cached spec"),
                                      GS_PVY(3, false, true, " f-cached spec"),
-                                     GS_PVY(3, true, false, " f-nt")};
+                                     GS_PVY(3, true, false, " f-nt"),
+                                     {"tb2y ry2 wx4 wy2 f-cached spec pfd2", 2, 4, 2,
+                                      k_tb2y<GS_LINEAR, 2, 4, true, false, false, true, 0, 2>}};
 #undef GS_PVY
 #undef GS_PVF
 #undef GS_PV
