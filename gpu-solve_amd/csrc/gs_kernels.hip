@@ -776,37 +776,40 @@ __global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so,
 // false: one slot loaded per step, 154 VGPRs and 3 waves per SIMD, measured faster. Blocks go in
 // XCD-aware order, y fastest, so the neighbouring rows that share 3 of a block's 5 v rows run on the
 // same XCD at the same time.
-constexpr int RR2_WXMAX = 8;
+constexpr int RR2_WXMAX = 8, RR2_NR2_LOG2_POINTS = 26;
 
-template <int MODE, bool PF> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
+// NR: coarse rows per block (1: fine rows 2Y-1..2Y+1 computed; 2: 2Y-1..2Y+3, the shared row 2Y+1 and three
+// of the seven v rows once instead of twice)
+template <int MODE, bool PF, int NR = 1> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
 __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* __restrict__ v,
                                                          const double* __restrict__ f, const double* __restrict__ w,
                                                          double* __restrict__ ca,
                                                          double* __restrict__ cb, int fnx, int fny, int fnz,
-                                                         int64_t fldy, int64_t fldz, int cnx, int cnz, int64_t cldy,
+                                                         int64_t fldy, int64_t fldz, int cnx, int cny, int cnz, int64_t cldy,
                                                          int64_t cldz, int ZC, int zhi)
 {
     static_assert(MODE != GS_NEWTON || !PF, "NEWTON: newtonV rows exceed the budget of the prefetch ring");
+    constexpr int RR = 2 * NR + 1; // computed fine rows; v rows 0 .. RR+1 (0 and RR+1: halo rows)
     // wave-edge columns [parity][1 + wave][side][plane * 3 + row] of v, and r at each wave's first fine
     // column [parity][1 + wave][plane * 3 + row]; slots 0 and WX+1 are the zero x-boundary
-    __shared__ double ve[2][RR2_WXMAX + 2][2][6];
-    __shared__ double re[2][RR2_WXMAX + 2][6];
+    __shared__ double ve[2][RR2_WXMAX + 2][2][2 * RR];
+    __shared__ double re[2][RR2_WXMAX + 2][2 * RR];
     const int lane = threadIdx.x;
     const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int WX = blockDim.y;
-    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 2 * 6; i += WAVE * WX) (&ve[0][0][0][0])[i] = 0.0;
-    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 6; i += WAVE * WX) (&re[0][0][0])[i] = 0.0;
+    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 2 * 2 * RR; i += WAVE * WX) (&ve[0][0][0][0])[i] = 0.0;
+    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 2 * RR; i += WAVE * WX) (&re[0][0][0])[i] = 0.0;
     __syncthreads();
     const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-    const int Y = 1 + (int)(tile % gridDim.x);
+    const int Y = 1 + NR * (int)(tile % gridDim.x);
     const int Zb = 1 + (int)(tile / gridDim.x) * ZC, Ze = min(Zb + ZC - 1, cnz);
     const int X = 1 + wx * WAVE + lane;
     const int x = 2 * X - 1, xl = min(x, fnx + 1);
     const bool okx0 = x <= fnx, okx1 = x + 1 <= fnx;
-    int64_t roff[5]; // fine rows 2Y-2 .. 2Y+2 (computed: 1..3)
-    bool rowc[5];
+    int64_t roff[RR + 2]; // fine rows 2Y-2 .. 2Y+2NR (computed: 1..RR)
+    bool rowc[RR + 2];
 #pragma unroll
-    for (int j = 0; j < 5; j++) {
+    for (int j = 0; j < RR + 2; j++) {
         const int y = 2 * Y - 2 + j;
         roff[j] = (int64_t)min(max(y, 0), fny + 1) * fldy;
         rowc[j] = y >= 1 && y <= fny;
@@ -818,11 +821,11 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     };
     // one step's operands: v planes 2Z+1 (A), 2Z+2 (B) of rows 1..3; halo rows 0 / 4 of planes 2Z (H0)
     // and 2Z+1 (H1); f of planes 2Z (F0), 2Z+1 (F1) rows 1..3
-    double2 VA[2][3], VB[2][3], H0[2][2], H1[2][2], F0[2][3], F1[2][3], W0[2][3], W1[2][3];
+    double2 VA[2][RR], VB[2][RR], H0[2][2], H1[2][2], F0[2][RR], F1[2][RR], W0[2][RR], W1[2][RR];
     auto load_slot = [&](const int s, const int Z) {
         const int p = 2 * Z;
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
+        for (int j = 0; j < RR; j++) {
             VA[s][j] = ld2(at(v, j + 1, p + 1));
             VB[s][j] = ld2(at(v, j + 1, p + 2));
             F0[s][j] = ld2(at(f, j + 1, p));
@@ -833,9 +836,9 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             }
         }
         H0[s][0] = ld2(at(v, 0, p));
-        H0[s][1] = ld2(at(v, 4, p));
+        H0[s][1] = ld2(at(v, RR + 1, p));
         H1[s][0] = ld2(at(v, 0, p + 1));
-        H1[s][1] = ld2(at(v, 4, p + 1));
+        H1[s][1] = ld2(at(v, RR + 1, p + 1));
     };
     // LDS-only barrier: the outstanding prefetch stays in flight across it
     auto lds_barrier = [] {
@@ -843,57 +846,57 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
         __builtin_amdgcn_s_barrier();
     };
     // the columns left of lane 0 / right of lane 63 on two planes: v(x-1) of lane 0, v(x+2) of lane 63
-    auto edges_v = [&](int par, const double2 (&P)[3], const double2 (&Q)[3], double (&CLp)[3], double (&CRp)[3],
-                       double (&CLq)[3], double (&CRq)[3]) {
+    auto edges_v = [&](int par, const double2 (&P)[RR], const double2 (&Q)[RR], double (&CLp)[RR], double (&CRp)[RR],
+                       double (&CLq)[RR], double (&CRq)[RR]) {
         if (lane == 0) {
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
+            for (int j = 0; j < RR; j++) {
                 ve[par][wx + 1][0][j] = P[j].x;
-                ve[par][wx + 1][0][3 + j] = Q[j].x;
+                ve[par][wx + 1][0][RR + j] = Q[j].x;
             }
         }
         if (lane == WAVE - 1) {
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
+            for (int j = 0; j < RR; j++) {
                 ve[par][wx + 1][1][j] = P[j].y;
-                ve[par][wx + 1][1][3 + j] = Q[j].y;
+                ve[par][wx + 1][1][RR + j] = Q[j].y;
             }
         }
         lds_barrier();
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
+        for (int j = 0; j < RR; j++) {
             CLp[j] = uniform_d(ve[par][wx][1][j]);
             CRp[j] = uniform_d(ve[par][wx + 2][0][j]);
-            CLq[j] = uniform_d(ve[par][wx][1][3 + j]);
-            CRq[j] = uniform_d(ve[par][wx + 2][0][3 + j]);
+            CLq[j] = uniform_d(ve[par][wx][1][RR + j]);
+            CRq[j] = uniform_d(ve[par][wx + 2][0][RR + j]);
         }
     };
     // r(2X+1) of every lane for two planes: the right neighbour lane's r.x (lane 63: the right wave's)
-    auto edges_r = [&](int par, const double2 (&R)[3], const double2 (&S)[3], double (&NR)[3], double (&NS)[3]) {
+    auto edges_r = [&](int par, const double2 (&R)[RR], const double2 (&S)[RR], double (&NQ)[RR], double (&NS)[RR]) {
         if (lane == 0) {
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
+            for (int j = 0; j < RR; j++) {
                 re[par][wx + 1][j] = R[j].x;
-                re[par][wx + 1][3 + j] = S[j].x;
+                re[par][wx + 1][RR + j] = S[j].x;
             }
         }
         lds_barrier();
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            NR[j] = lane_from_right<true>(R[j].x, uniform_d(re[par][wx + 2][j]));
-            NS[j] = lane_from_right<true>(S[j].x, uniform_d(re[par][wx + 2][3 + j]));
+        for (int j = 0; j < RR; j++) {
+            NQ[j] = lane_from_right<true>(R[j].x, uniform_d(re[par][wx + 2][j]));
+            NS[j] = lane_from_right<true>(S[j].x, uniform_d(re[par][wx + 2][RR + j]));
         }
     };
     // r = f - A v on fine plane p, rows 1..3 (k_rb KIND 1: same expression, same term order); 0 outside
     // the interior, as the reference's never-written boundary of r
-    auto resid = [&](const double2 (&Vm)[3], const double2 (&Vc)[3], const double2 (&H)[2], const double2 (&Vp)[3],
-                     const double2 (&F)[3], const double2 (&W)[3], const double (&CL)[3], const double (&CR)[3], int p,
-                     double2 (&R)[3]) {
+    auto resid = [&](const double2 (&Vm)[RR], const double2 (&Vc)[RR], const double2 (&H)[2], const double2 (&Vp)[RR],
+                     const double2 (&F)[RR], const double2 (&W)[RR], const double (&CL)[RR], const double (&CR)[RR], int p,
+                     double2 (&R)[RR]) {
         const bool pin = p >= 1 && (p <= fnz || (zhi && p == fnz + 1));
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
+        for (int j = 0; j < RR; j++) {
             const double2 c = Vc[j];
-            const double2 ym = j == 0 ? H[0] : Vc[j - 1], yp = j == 2 ? H[1] : Vc[j + 1];
+            const double2 ym = j == 0 ? H[0] : Vc[j - 1], yp = j == RR - 1 ? H[1] : Vc[j + 1];
             const double xm0 = lane_from_left<true>(c.y, CL[j]);
             const double xp1 = lane_from_right<true>(c.x, CR[j]);
             const double w0 = MODE == GS_NEWTON ? W[j].x : 0.0, w1 = MODE == GS_NEWTON ? W[j].y : 0.0;
@@ -905,13 +908,13 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     };
 
     // prologue: r on fine plane 2Zb-1 (the top plane of the previous coarse plane's stencil)
-    double2 Vm[3], V0[3], Rm[3];
-    double Nm[3];
+    double2 Vm[RR], V0[RR], Rm[RR];
+    double Nm[RR];
     {
         const int p = 2 * Zb - 1;
-        double2 Vq[3], Hq[2], Fq[3], Wq[3];
+        double2 Vq[RR], Hq[2], Fq[RR], Wq[RR];
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
+        for (int j = 0; j < RR; j++) {
             Vm[j] = ld2(at(v, j + 1, p - 1));
             Vq[j] = ld2(at(v, j + 1, p));
             V0[j] = ld2(at(v, j + 1, p + 1));
@@ -919,13 +922,13 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             Wq[j] = MODE == GS_NEWTON ? ld2(at(w, j + 1, p)) : make_double2(0.0, 0.0);
         }
         Hq[0] = ld2(at(v, 0, p));
-        Hq[1] = ld2(at(v, 4, p));
-        double CL[3], CR[3], CL2[3], CR2[3], N2[3];
+        Hq[1] = ld2(at(v, RR + 1, p));
+        double CL[RR], CR[RR], CL2[RR], CR2[RR], N2[RR];
         edges_v(1, Vq, Vq, CL, CR, CL2, CR2);
         resid(Vm, Vq, Hq, V0, Fq, Wq, CL, CR, p, Rm);
         edges_r(1, Rm, Rm, Nm, N2);
 #pragma unroll
-        for (int j = 0; j < 3; j++) Vm[j] = Vq[j]; // window: Vm = v(2Zb-1), V0 = v(2Zb)
+        for (int j = 0; j < RR; j++) Vm[j] = Vq[j]; // window: Vm = v(2Zb-1), V0 = v(2Zb)
     }
     if (PF) load_slot(1, Zb);
     // Both halves always run (an odd chunk ends with a step whose results are discarded), and every
@@ -937,34 +940,38 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             const int cs = PF ? ph ^ 1 : 0; // slot holding this step's operands
             if (PF) load_slot(ph, Z + 1);
             else load_slot(0, Z);
-            double CL0[3], CR0[3], CL1[3], CR1[3];
+            double CL0[RR], CR0[RR], CL1[RR], CR1[RR];
             edges_v(ph, V0, VA[cs], CL0, CR0, CL1, CR1);
-            double2 R0[3], R1[3];
+            double2 R0[RR], R1[RR];
             resid(Vm, V0, H0[cs], VA[cs], F0[cs], W0[cs], CL0, CR0, 2 * Z, R0);
             resid(V0, VA[cs], H1[cs], VB[cs], F1[cs], W1[cs], CL1, CR1, 2 * Z + 1, R1);
-            double N0[3], N1[3];
+            double N0[RR], N1[RR];
             edges_r(ph, R0, R1, N0, N1);
-            if (Z <= Ze && X <= cnx) {
-                double acc = 0.0;
 #pragma unroll
-                for (int a = -1; a <= 1; a++)
+            for (int i = 0; i < NR; i++) {
+                if (Z <= Ze && X <= cnx && Y + i <= cny) {
+                    double acc = 0.0;
 #pragma unroll
-                    for (int b = -1; b <= 1; b++)
+                    for (int a = -1; a <= 1; a++)
 #pragma unroll
-                        for (int c = -1; c <= 1; c++) {
-                            const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
-                                               ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
-                            const int j = b + 1;
-                            const double2 rp = c < 0 ? Rm[j] : (c == 0 ? R0[j] : R1[j]);
-                            const double rn = c < 0 ? Nm[j] : (c == 0 ? N0[j] : N1[j]);
-                            acc += wgt * (a < 0 ? rp.x : (a == 0 ? rp.y : rn));
-                        }
-                const int64_t q = X + Y * cldy + (int64_t)Z * cldz;
-                ca[q] = acc;
-                if (cb) cb[q] = acc;
+                        for (int b = -1; b <= 1; b++)
+#pragma unroll
+                            for (int c = -1; c <= 1; c++) {
+                                const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
+                                                   ((2.0 - (b < 0 ? -b : b)) / 2.0) *
+                                                   ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                                const int j = 2 * i + b + 1;
+                                const double2 rp = c < 0 ? Rm[j] : (c == 0 ? R0[j] : R1[j]);
+                                const double rn = c < 0 ? Nm[j] : (c == 0 ? N0[j] : N1[j]);
+                                acc += wgt * (a < 0 ? rp.x : (a == 0 ? rp.y : rn));
+                            }
+                    const int64_t q = X + (Y + i) * cldy + (int64_t)Z * cldz;
+                    ca[q] = acc;
+                    if (cb) cb[q] = acc;
+                }
             }
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
+            for (int j = 0; j < RR; j++) {
                 Vm[j] = VA[cs][j];
                 V0[j] = VB[cs][j];
                 Rm[j] = R1[j];
@@ -2284,16 +2291,24 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
     if (zhi && !rr2) return GS_EINVAL; // the slab form exists for the register kernel only
     if (rr2) {
         // >= 2048 blocks of one coarse row where the level has them (chunks of <= 32 coarse planes)
-        const int64_t chunks = (2048 + cl->ny - 1) / cl->ny;
+        // LINEAR levels of >= 2^26 points: two coarse rows per block (231 VGPRs, 2 waves per SIMD): 0.507 vs
+        // 0.529 ms at 512^3, but 0.072 vs 0.068 ms at 256^3 (gpurun_out/rrnr2, tools/rr_ab.py);
+        // NONLINEAR / NEWTON: one row (VGPR budget). GS_RR_NR=1|2 forces the choice (A/B, tests).
+        static const int nr_env = getenv("GS_RR_NR") ? std::atoi(getenv("GS_RR_NR")) : 0;
+        const bool big = fl->nx * fl->ny * fl->nz >= ((int64_t)1 << RR2_NR2_LOG2_POINTS);
+        const int nr = mode == GS_LINEAR && (nr_env == 2 || (nr_env == 0 && big)) ? 2 : 1;
+        const int64_t rows = (cl->ny + nr - 1) / nr; // blocks along y
+        const int64_t chunks = (2048 + rows - 1) / rows;
         int64_t zc = (cl->nz + chunks - 1) / chunks;
         zc = zc < 1 ? 1 : (zc > 32 ? 32 : zc);
-        const dim3 g((unsigned)cl->ny, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
+        const dim3 g((unsigned)rows, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
-#define GS_RR2(M) hipLaunchKernelGGL((k_rr2<M, false>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
-        if (mode == GS_LINEAR) GS_RR2(GS_LINEAR);
-        else if (mode == GS_NONLINEAR) GS_RR2(GS_NONLINEAR);
-        else GS_RR2(GS_NEWTON);
+#define GS_RR2(M, N) hipLaunchKernelGGL((k_rr2<M, false, N>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
+        if (mode == GS_LINEAR && nr == 2) GS_RR2(GS_LINEAR, 2);
+        else if (mode == GS_LINEAR) GS_RR2(GS_LINEAR, 1);
+        else if (mode == GS_NONLINEAR) GS_RR2(GS_NONLINEAR, 1);
+        else GS_RR2(GS_NEWTON, 1);
 #undef GS_RR2
         return launch_status();
     }

@@ -309,6 +309,32 @@ def test_residual_restrict_fused(fd, mode):
     assert_field(ca.to_xyz(), O.restrict(rr, cd), mode, f"rr {fd} m{mode}")
 
 
+def test_residual_restrict_fused_two_rows_per_block():
+    """A LINEAR level of >= 2^26 points takes k_rr2's two-coarse-rows-per-block shape: still bit-identical
+    to gs_residual + gs_restrict2; odd coarse ny (the last block's second row is outside the level)."""
+    fd = (511, 515, 256)
+    assert fd[0] * fd[1] * fd[2] >= 1 << 26
+    cd = [x // 2 for x in fd]
+    h = 1.0 / (fd[1] + 1)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    v, f = DevField(*fd), DevField(*fd)
+    for fld, scale in ((v, 1.0), (f, 100.0)):
+        inner = fld.zyx[1:-1, 1:-1, 1:fd[0] + 1]
+        inner.copy_((torch.rand(inner.shape, generator=g, device="cuda", dtype=torch.float64) - 0.5) * scale)
+    S = S_abi((6, -1, -1.5, -1, -0.5, -1, -1))
+    L = v.level(h)
+    r = DevField(*fd)
+    r.buf.zero_()
+    ok(k().gs_residual(C.byref(S), C.byref(L), 0, 0.0, v.ptr, f.ptr, None, r.ptr, None, stream()))
+    ca_ref, ca = DevField(*cd), DevField(*cd)
+    Lc = ca.level(2 * h)
+    ok(k().gs_restrict2(r.ptr, C.byref(r.level(h)), ca_ref.ptr, None, C.byref(Lc), stream()))
+    ok(k().gs_residual_restrict(C.byref(S), C.byref(L), 0, 0.0, v.ptr, f.ptr, None, ca.ptr, None, C.byref(Lc),
+                                stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(ca.buf, ca_ref.buf)
+
+
 def test_residual_restrict_generic_stencil():
     rng = np.random.default_rng(11)
     fd = (37, 11, 9)

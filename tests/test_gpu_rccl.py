@@ -1,0 +1,50 @@
+"""The RCCL communicator on ONE GPU (one rank): ncclGetUniqueId / ncclCommInitRank through the C ABI
+(gs_rccl_unique_id, gs_grid_create_rccl — the calls bench.py makes on every rank at N > 1) and a solve
+on the resulting grid, which must be bit-identical to the plain single-GPU grid. Two ranks cannot share
+one GPU under RCCL, so the send/recv halo and the broadcast of replicated levels are covered by the
+loopback communicator (test_gpu_zslab.py) and the 2-rank gloo emulation (test_zslab_cpu.py)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import gpusolve as gsv  # noqa: E402
+
+
+def rccl_grid(params):
+    drv = gsv.driver()
+    uid = (C.c_ubyte * 128)()
+    assert drv.gs_rccl_unique_id(uid) == 0, drv.gs_last_error().decode()
+    g = gsv.HipGridData.__new__(gsv.HipGridData)
+    g.params = params
+    g._abi_params = params.to_abi()
+    g.handle = drv.gs_grid_create_rccl(C.byref(g._abi_params), 0, 1, uid)
+    assert g.handle, drv.gs_last_error().decode()
+    return g
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_rccl_one_rank_solve_bit_identical(mode):
+    p = gsv.GridParams(maxiter=3 if mode == 2 else 4, tol=0.0, gridDim=(40, 33, 48), mode=mode)
+    with gsv.HipGridData(p) as g:
+        ref_h = gsv.NewtonSolver.solve(g) if mode == 2 else gsv.HipSolver.solve(g)
+        ref_v = g.field(0, "v")
+    g = rccl_grid(p)
+    try:
+        h = gsv.NewtonSolver.solve(g) if mode == 2 else gsv.HipSolver.solve(g)
+        v = g.field(0, "v")
+    finally:
+        g.close()
+    assert h == ref_h
+    np.testing.assert_array_equal(v, ref_v)
+
+
+def test_rccl_bad_rank_rejected():
+    drv = gsv.driver()
+    uid = (C.c_ubyte * 128)()
+    p = gsv.GridParams(maxiter=1, gridDim=(8, 8, 8)).to_abi()
+    assert not drv.gs_grid_create_rccl(C.byref(p), 1, 1, uid)
+    assert b"bad arguments" in drv.gs_last_error()
