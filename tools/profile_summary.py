@@ -86,6 +86,22 @@ def main():
         lines += ["", "## PMC (level-0 sweep, bench.py config)", "", "```", json.dumps(d, indent=1), "```"]
     if bench:
         lines += ["", "## bench.py line", "", "```", json.dumps(bench, indent=1), "```"]
+    # the profiled bench run's timed launches (the last steps/2 pair launches of its kernel trace) against
+    # the kernel_ms that run measured itself with HIP events on the solver's stream
+    trace, bp = os.path.join(src, "prof", "run_kernel_trace.csv"), os.path.join(src, "bench_prof.json")
+    if os.path.exists(trace) and os.path.exists(bp):
+        b2 = json.loads(open(bp).read().strip().splitlines()[-1])
+        rows = [r for r in csv.DictReader(open(trace)) if sweep_kernel(r["Kernel_Name"])]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        k = b2["steps"] // 2 + b2["steps"] % 2
+        if len(rows) >= k > 0:
+            timed = rows[-k:]
+            avg = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed) / k / 1e6
+            lines += ["", "## rocprofv3 vs bench.py's own HIP-event timing (same profiled run)", "",
+                      f"- timed pair launches in the trace (last {k} of {len(rows)}): average {avg:.4f} ms",
+                      f"- bench.py roofline.kernel_ms of that run: {b2['roofline']['kernel_ms']:.4f} ms "
+                      f"(ratio {b2['roofline']['kernel_ms'] / avg:.3f}); the stats table's average also "
+                      f"includes the warm-up launches"]
     vct = os.path.join(src, "prof_vc", "run_kernel_trace.csv")
     if os.path.exists(vct):
         import subprocess
