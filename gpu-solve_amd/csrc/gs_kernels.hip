@@ -1583,12 +1583,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     constexpr int NS = PFD == 2 ? 4 : 2, UNR = PFD == 2 ? 4 : 2;
     double2 Vp[NV], Vc[NV], VL[NS][NV], FL[NS][NV], WL[NS][NV], HL[NS];
     double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
-    // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes them from
-    // the newtonV rows at z-1 (same expressions, same values)
+    // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes A from the
+    // newtonV rows at z-1 and reads E = exp(w) from LDS (same expressions, same values)
     constexpr bool RECOMP = MODE == GS_NEWTON && PRO != 0;
     // (Wprev, Fprev: sweep 2's newtonV / f rows at z-1, in LDS like the coarse rows below)
     __shared__ double2 wprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
     __shared__ double2 fprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
+    // exp(w) of sweep 1's own rows, by plane parity: sweep 2 reads the previous plane's (each lane its own
+    // values, no barrier) instead of evaluating exp a second time (+32 KB: 148 KB, one block per CU as before)
+    __shared__ double2 eprev_l[RECOMP ? 2 : 1][RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
 #pragma unroll
     for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
 #pragma unroll
@@ -1775,6 +1778,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                             Acur[j - 1] = A;
                             Ecur[j - 1] = E;
                         }
+                        if (RECOMP && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
                         a0 = newton_op(q[0], c.x, A.x, E.x);
                         a1 = newton_op(q[1], c.y, A.y, E.y);
                         n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
@@ -1812,7 +1816,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                             if constexpr (RECOMP) {
                                 const double2 wv = wprev_l[j - 1][wx + WX * wy][lane];
                                 A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
-                                E = make_double2(exp(wv.x), exp(wv.y));
+                                E = eprev_l[ph ^ 1][j - 1][wx + WX * wy][lane];
                             } else {
                                 A = Aprev[j - 1];
                                 E = Eprev[j - 1];

@@ -86,6 +86,38 @@ def main():
         print(f"pair {n}^3 {name}: median {med:.4f} ms  min {min(xs):.4f}  {24 * n ** 3 / med / 1e6:.0f} GB/s (24 B/pt)")
     print("bitwise_equal", same)
 
+    # NEWTON: the fused prolongation pair (gs_jacobi_sweep2_prolong, mode 2) of both builds
+    w = DevField(n, n, n)
+    inner = w.zyx[1:-1, 1:-1, 1:n + 1]
+    inner.copy_(torch.rand(inner.shape, generator=g, device="cuda", dtype=torch.float64) * 1e-2)
+    c = DevField(nc, nc, nc)
+    cin = c.zyx[1:-1, 1:-1, 1:nc + 1]
+    cin.copy_(torch.rand(cin.shape, generator=g, device="cuda", dtype=torch.float64) * 1e-3)
+    Lc2 = c.level(hc)
+
+    def pro(lib, src, dst):
+        rc = lib.gs_jacobi_sweep2_prolong(C.byref(S), C.byref(L), 2, 0.8, 1.0, src.ptr, c.ptr, None, C.byref(Lc2),
+                                          dst.ptr, f.ptr, w.ptr, 0, 0, st)
+        assert rc == 0, rc
+    pro(new, v, a1)
+    pro(old, v, a2)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(a1.buf, a2.buf))
+    t = {"new": [], "old": []}
+    for _ in range(5):
+        for name, lib in (("new", new), ("old", old)):
+            pro(lib, v, a1)
+            ev[0].record()
+            for i in range(6):
+                pro(lib, v, a1 if i % 2 else a2)
+            ev[1].record()
+            torch.cuda.synchronize()
+            t[name].append(ev[0].elapsed_time(ev[1]) / 6)
+    for name, xs in t.items():
+        med = statistics.median(xs)
+        print(f"newton prolongation pair {n}^3 {name}: median {med:.4f} ms  min {min(xs):.4f}")
+    print("bitwise_equal", same)
+
 
 if __name__ == "__main__":
     main()
