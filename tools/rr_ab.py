@@ -95,29 +95,29 @@ def main():
     cin.copy_(torch.rand(cin.shape, generator=g, device="cuda", dtype=torch.float64) * 1e-3)
     Lc2 = c.level(hc)
 
-    def pro(lib, src, dst):
-        rc = lib.gs_jacobi_sweep2_prolong(C.byref(S), C.byref(L), 2, 0.8, 1.0, src.ptr, c.ptr, None, C.byref(Lc2),
-                                          dst.ptr, f.ptr, w.ptr, 0, 0, st)
-        assert rc == 0, rc
-    pro(new, v, a1)
-    pro(old, v, a2)
-    torch.cuda.synchronize()
-    same = bool(torch.equal(a1.buf, a2.buf))
-    t = {"new": [], "old": []}
-    for _ in range(5):
-        for name, lib in (("new", new), ("old", old)):
-            pro(lib, v, a1)
-            ev[0].record()
-            for i in range(6):
-                pro(lib, v, a1 if i % 2 else a2)
-            ev[1].record()
-            torch.cuda.synchronize()
-            t[name].append(ev[0].elapsed_time(ev[1]) / 6)
-    for name, xs in t.items():
-        med = statistics.median(xs)
-        print(f"newton prolongation pair {n}^3 {name}: median {med:.4f} ms  min {min(xs):.4f}")
-    print("bitwise_equal", same)
-
+    for mode, label in ((0, "linear"), (2, "newton")):
+        def pro(lib, src, dst):
+            rc = lib.gs_jacobi_sweep2_prolong(C.byref(S), C.byref(L), mode, 0.8, 1.0, src.ptr, c.ptr, None,
+                                              C.byref(Lc2), dst.ptr, f.ptr, w.ptr if mode == 2 else None, 0, 0, st)
+            assert rc == 0, rc
+        pro(new, v, a1)
+        pro(old, v, a2)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(a1.buf, a2.buf))
+        t = {"new": [], "old": []}
+        for _ in range(5):
+            for name, lib in (("new", new), ("old", old)):
+                pro(lib, v, a1)
+                ev[0].record()
+                for i in range(6):
+                    pro(lib, v, a1 if i % 2 else a2)
+                ev[1].record()
+                torch.cuda.synchronize()
+                t[name].append(ev[0].elapsed_time(ev[1]) / 6)
+        for name, xs in t.items():
+            med = statistics.median(xs)
+            print(f"{label} prolongation pair {n}^3 {name}: median {med:.4f} ms  min {min(xs):.4f}")
+        print("bitwise_equal", same)
 
 if __name__ == "__main__":
     main()
