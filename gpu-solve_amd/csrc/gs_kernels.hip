@@ -1917,6 +1917,14 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
     const int fills = tiles * ((L->nz + 3) / 4) >= 512 ? 2 : 1;
     int64_t c = tiles * L->nz / 1024;
     c = c < 4 ? 4 : (c > 64 ? 64 : c);
+    // levels of >= 2^26 points: chunks for ~512 blocks, up to 128 planes (one 8-wave block per CU, two
+    // rounds at 512^3; fewer re-read chunk-boundary planes): 0.658 vs 0.674 ms per 512^3 pair
+    // (tools/kbench.py --pairs --zc 64,96,128). GS_PAIR_BIG_CHUNKS=0 keeps the 64-plane rule (A/B).
+    static const bool big_chunks = !getenv("GS_PAIR_BIG_CHUNKS") || std::atoi(getenv("GS_PAIR_BIG_CHUNKS")) != 0;
+    if (big_chunks && L->nx * L->ny * L->nz >= ((int64_t)1 << 26)) {
+        const int64_t b = tiles * L->nz / 512;
+        c = b < 64 ? 64 : (b > 128 ? 128 : b);
+    }
     c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)
     *zc = (int)c;
     *grid = dim3((unsigned)tiles, (unsigned)((L->nz + c - 1) / c));
