@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=200, help="untimed sweeps first (also brings the GPU clocks up)")
+    ap.add_argument("--ramp-ms", type=float, default=400.0,
+                    help="after --warmup, keep running untimed sweeps until this much wall time has passed")
     ap.add_argument("--size", type=int, default=512, help="per-rank cube edge (BASELINE config #3: 512)")
     ap.add_argument("--vcycles", type=int, default=20, help="timed V-cycles after one warm-up cycle (0: skip)")
     ap.add_argument("--cpu-sweeps", type=int, default=6, help="cpu_baseline sample size (0: skip)")
@@ -69,30 +71,54 @@ def pmc_traffic(n):
     return None, None
 
 
+def _cpu_run(exe, args, threads, timeout):
+    env = dict(os.environ)
+    env["OMP_NUM_THREADS"] = str(threads)
+    env.setdefault("OMP_PROC_BIND", "close")
+    r = subprocess.run([exe, *args], capture_output=True, text=True, env=env, timeout=timeout)
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def cpu_baseline(n, sweeps, vcycles):
-    """Reference CPU smoother on this host (kind "reference"); falls back to the oracle port."""
+    """CPU baseline on this host's cores, a bounded sample of the same workload.
+
+    kind "reference": oracle/_ref/ref_probe, the reference's own src/cpu (CpuSolver::jacobi / vcycle)
+    compiled from /root/reference by oracle/Makefile in the build container and shipped to the GPU box
+    as a built binary (no reference source travels). Without it, kind "port": the oracle restatement
+    (oracle/build/gso_cli). Legs: all host threads (OMP_NUM_THREADS = the box's CPU share), one thread,
+    and the port timed on the same sample (calibration: port / reference speed ratio)."""
     ref = os.path.join(REPO, "oracle", "_ref", "ref_probe")
     port = os.path.join(REPO, "oracle", "build", "gso_cli")
     exe, kind = (ref, "reference") if os.path.exists(ref) else (port, "port")
     if not os.path.exists(exe):
         return None
-    env = dict(os.environ)
-    threads = int(env.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    env["OMP_NUM_THREADS"] = str(threads)
-    env.setdefault("OMP_PROC_BIND", "close")
-    out = {"unit": "MLUPS", "cores": threads, "kind": kind}
-    r = subprocess.run([exe, "time_jacobi", str(n), str(n), str(n), "0", str(sweeps)], capture_output=True,
-                       text=True, env=env, timeout=600)
-    j = json.loads(r.stdout.strip().splitlines()[-1])
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    out = {"unit": "MLUPS", "cores": threads, "kind": kind,
+           "binary": os.path.relpath(exe, REPO) + (" (reference src/cpu compiled by oracle/Makefile)"
+                                                    if kind == "reference" else " (oracle restatement)")}
+    j = _cpu_run(exe, ["time_jacobi", str(n), str(n), str(n), "0", str(sweeps)], threads, 600)
     out["value"] = round(float(j["mlups"]), 3)
     out["sample"] = (f"{sweeps} level-0 Jacobi sweeps (CpuSolver::jacobi, residual+update) of the {n}^3 linear "
                      f"grid after 1 warm-up sweep, {threads} OpenMP threads")
     if vcycles > 0:
-        r = subprocess.run([exe, "time_vcycle", str(n), str(n), str(n), "0", str(vcycles)], capture_output=True,
-                           text=True, env=env, timeout=900)
-        j = json.loads(r.stdout.strip().splitlines()[-1])
+        j = _cpu_run(exe, ["time_vcycle", str(n), str(n), str(n), "0", str(vcycles)], threads, 900)
         out["vcycle_ms"] = round(float(j["ms_per_cycle"]), 1)
         out["sample"] += f"; {vcycles} 2+2 V-cycle(s) after 1 warm-up cycle"
+    # one-thread leg (SURVEY.md §8(d): OMP_NUM_THREADS=1), 1 timed sweep of the same grid
+    try:
+        j = _cpu_run(exe, ["time_jacobi", str(n), str(n), str(n), "0", "1"], 1, 600)
+        out["one_thread"] = {"value": round(float(j["mlups"]), 3), "cores": 1,
+                             "sample": f"1 level-0 Jacobi sweep of the {n}^3 linear grid after 1 warm-up sweep"}
+    except Exception as e:  # reported, never required
+        out["one_thread"] = {"error": str(e)}
+    if kind == "reference" and os.path.exists(port):
+        try:
+            j = _cpu_run(port, ["time_jacobi", str(n), str(n), str(n), "0", str(sweeps)], threads, 600)
+            out["port_calibration"] = {"port_value": round(float(j["mlups"]), 3),
+                                       "port_over_reference": round(float(j["mlups"]) / out["value"], 3),
+                                       "sample": f"same {sweeps} sweeps, {threads} threads, oracle/build/gso_cli"}
+        except Exception as e:
+            out["port_calibration"] = {"error": str(e)}
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
         out["cpu_model"] = model
@@ -240,8 +266,17 @@ def main():
             raise gsv.GpuSolveError(drv.gs_last_error().decode())
 
     fused = drv.gs_grid_level_fused(grid.handle, 0) == 1
+    # untimed ramp: the requested warm-up sweeps, then more until at least --ramp-ms of smoother launches
+    # have run (cold launches run ~25 % slower: BENCH_r01 timed them inside a 7.8 ms window)
+    tw = time.perf_counter()
     sweeps(a.warmup)
     grid.sync()
+    ramp = 0
+    while (time.perf_counter() - tw) * 1e3 < a.ramp_ms:
+        sweeps(40)
+        grid.sync()
+        ramp += 40
+    warmup_ms = (time.perf_counter() - tw) * 1e3
     barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -308,6 +343,8 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "warmup_ms": round(warmup_ms, 1),
+            "warmup_sweeps_total": a.warmup + ramp,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
@@ -318,7 +355,10 @@ def main():
                                     if world == 1 else
                                     f"{dims[0]}x{dims[1]}x{dims[2]} linear 7-point fused Jacobi sweep (level 0), "
                                     f"Z-slab over {world} GPUs (BASELINE config #5 at N=8)"),
-                       "grid": list(dims), "points_per_rank": int(lups_per_rank), "mode": "linear", "omega": 0.8,
+                       "grid": list(dims), "points_per_rank": int(lups_per_rank),
+                       "per_rank_slab": [int(dims[0]), int(dims[1]), int(dims[2]) // world],
+                       "per_rank_pair_kernel": pair_kernel.split(":")[0],
+                       "mode": "linear", "omega": 0.8,
                        "parallelism": f"zslab{world}-rccl" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_GBPS, 4),
@@ -326,7 +366,15 @@ def main():
                          "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
                          "kernel": (pair_kernel + ": two fused sweeps per launch (24 B per point per launch)"
                                     if fused else "k_rb: one sweep per launch (24 B per point per launch)"),
-                         "algorithmic_bytes_per_launch": BYTES_PER_LUP * lups_per_rank},
+                         "lups_per_launch": 2 if fused else 1,
+                         "points_per_launch": int(lups_per_rank),
+                         "compulsory_bytes_per_lup": BYTES_PER_LUP / (2 if fused else 1),
+                         "algorithmic_bytes_per_launch": BYTES_PER_LUP * lups_per_rank,
+                         "effective_GBps": round(value / world * BYTES_PER_LUP / 1e3, 1),
+                         "effective_GBps_note": ("MLUPS x 24 B per lattice update per GPU, the BASELINE.md "
+                                                 "definition; with temporal blocking (2 updates per pass) this is "
+                                                 "NOT HBM traffic: the HBM-side figure is `achieved` "
+                                                 "(24 B per point per launch / kernel_ms)")},
             "single_sweep_kernel": single,
             "measured_ceiling": ceiling,
             "vcycle": vc,

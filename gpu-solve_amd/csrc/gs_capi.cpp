@@ -134,18 +134,7 @@ int gs_grid_solve(void* grid, int print, double* hist, int cap, int* count)
         if (g.mode == gs::GridParams::NEWTON) {
             gs::NewtonSolver::history = &h;
             try {
-                if (print) gs::NewtonSolver::solve(g);
-                else {
-                    // NewtonSolver::solve prints unconditionally (reference behaviour); silence it here
-                    std::streambuf* old = std::cout.rdbuf(nullptr);
-                    try {
-                        gs::NewtonSolver::solve(g);
-                    } catch (...) {
-                        std::cout.rdbuf(old);
-                        throw;
-                    }
-                    std::cout.rdbuf(old);
-                }
+                gs::NewtonSolver::solve(g);
             } catch (...) {
                 gs::NewtonSolver::history = nullptr;
                 throw;
@@ -301,9 +290,24 @@ int gs_grid_dump(void* grid, int level, int field, const char* path)
     return gs_dump_write(host.data(), L.nx + 2, L.ny + 2, L.nz + 2, path);
 }
 
+int gs_grid_metrics(void* grid, char* line, int cap, double* level_ms, int levels_cap)
+{
+    return guarded([&] {
+        auto& g = G(grid);
+        if (!g.clock.on) throw gs::Error("metrics are off (set GS_METRICS=1 before creating the grid)");
+        const std::string s = gs::metricsLine(g);
+        if (line && cap > 0) {
+            std::strncpy(line, s.c_str(), (size_t)cap - 1);
+            line[cap - 1] = 0;
+        }
+        for (int l = 0; level_ms && l < levels_cap && l < (int)g.clock.levelMs.size(); l++)
+            level_ms[l] = g.clock.cycles ? g.clock.levelMs[l] / g.clock.cycles : 0.0;
+    });
+}
+
 int gs_grid_sync(void* grid)
 {
-    return guarded([&] { gs::check((int)hipStreamSynchronize(G(grid).stream()), "hipStreamSynchronize"); });
+    return guarded([&] { G(grid).sync(); });
 }
 
 int gs_grid_time_jacobi(void* grid, int level, int warmup, int sweeps, float* ms)
@@ -421,9 +425,7 @@ int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, in
                 std::vector<double> h;
                 if (g.mode == gs::GridParams::NEWTON) {
                     gs::NewtonSolver::history = &h;
-                    std::streambuf* old = std::cout.rdbuf(nullptr);
                     gs::NewtonSolver::solve(g);
-                    std::cout.rdbuf(old);
                     gs::NewtonSolver::history = nullptr;
                 } else {
                     gs::HipSolver::history = &h;
@@ -444,11 +446,19 @@ int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, in
             }
         } catch (const std::exception& e) {
             errs[r] = e.what();
+            // the other ranks may be parked in (or heading for) a hub barrier this rank will never
+            // reach: wake them, and make every later barrier throw, so all threads unwind and join
+            gs::abortLoopbackHub(*hub, e.what());
         }
     };
     std::vector<std::thread> th;
     for (int r = 0; r < nranks; r++) th.emplace_back(body, r);
     for (auto& t : th) t.join();
+    const std::string first = gs::loopbackHubError(*hub); // the failure that aborted the others
+    if (!first.empty()) {
+        g_err = first;
+        return 1;
+    }
     for (auto& e : errs)
         if (!e.empty()) {
             g_err = e;
@@ -458,6 +468,52 @@ int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, in
     if (hist)
         for (int i = 0; i < cap && i < (int)h0.size(); i++) hist[i] = h0[i];
     return 0;
+}
+
+int gs_debug_bounded_wait(int scenario, int k, double timeout_s, char* msg, int cap)
+{
+    int polls = 0;
+    const std::string err = gs::boundedWait(
+        [&]() -> int {
+            polls++;
+            if (scenario == 0) return polls >= k ? 0 : 1;     // completes at poll k
+            if (scenario == 1) return polls >= k ? 2 + 3 : 1; // asynchronous error (ncclInternalError = 3)
+            return 1;                                          // never completes
+        },
+        [](int st) { return st == 5 ? std::string("internal error - please report this issue to the NCCL developers")
+                                    : std::string("error ") + std::to_string(st); },
+        timeout_s, "debug wait");
+    if (msg && cap > 0) {
+        std::strncpy(msg, err.c_str(), (size_t)cap - 1);
+        msg[cap - 1] = 0;
+    }
+    return err.empty() ? 0 : 1;
+}
+
+int gs_debug_loopback_abort(int nranks, int failing_rank)
+{
+    // nranks threads meet at hub barriers; failing_rank throws before its second barrier. Every
+    // thread must unwind (no hang) and the first error must be the one reported.
+    if (nranks < 1 || failing_rank < 0 || failing_rank >= nranks) return -1;
+    auto hub = gs::makeLoopbackHub(nranks);
+    std::vector<int> unwound(nranks, 0);
+    auto body = [&](int r) {
+        try {
+            gs::loopbackHubBarrier(*hub);
+            if (r == failing_rank) throw gs::Error("rank " + std::to_string(r) + " failed");
+            for (int i = 0; i < 3; i++) gs::loopbackHubBarrier(*hub);
+        } catch (const std::exception& e) {
+            unwound[r] = 1;
+            gs::abortLoopbackHub(*hub, e.what());
+        }
+    };
+    std::vector<std::thread> th;
+    for (int r = 0; r < nranks; r++) th.emplace_back(body, r);
+    for (auto& t : th) t.join();
+    g_err = gs::loopbackHubError(*hub);
+    int n = 0;
+    for (int u : unwound) n += u;
+    return n; // == nranks when every rank unwound
 }
 
 const char* gs_last_error(void) { return g_err.c_str(); }

@@ -1,10 +1,14 @@
 // gs_comm.cpp — Z-slab plan, RCCL communicator, single-device loopback communicator.
 #include "gs_comm.hpp"
 
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -25,44 +29,57 @@ void ncclOk(ncclResult_t e, const char* what)
 } // namespace
 
 // ---------------------------------------------------------------------------------------------
-SlabPlan planZSlabs(const std::vector<int64_t>& levelNz, const std::vector<int64_t>& levelPoints, int nranks,
-                    int64_t minPoints)
+void Comm::sync(hipStream_t s) { hipOk(hipStreamSynchronize(s), "hipStreamSynchronize"); }
+
+double commTimeoutS(const char* env, double dflt)
 {
-    const size_t L = levelNz.size();
-    SlabPlan p;
-    p.distributed.assign(L, 0);
-    p.lo.assign(L, std::vector<int64_t>(nranks, 1));
-    p.hi.assign(L, std::vector<int64_t>(nranks, 0));
-    bool parent = nranks > 1;
-    for (size_t l = 0; l < L; l++) {
-        bool nonEmpty = true;
-        for (int r = 0; r < nranks; r++) {
-            if (l == 0) {
-                p.lo[0][r] = 1 + (int64_t)r * levelNz[0] / nranks;
-                p.hi[0][r] = (int64_t)(r + 1) * levelNz[0] / nranks;
-            } else {
-                p.lo[l][r] = (p.lo[l - 1][r] + 1) / 2; // coarse plane zc owned iff 2 zc is owned
-                p.hi[l][r] = p.hi[l - 1][r] / 2;
-            }
-            nonEmpty = nonEmpty && p.hi[l][r] >= p.lo[l][r];
-        }
-        const bool dist = parent && nonEmpty && l + 1 < L && (l == 0 || levelPoints[l] >= minPoints);
-        p.distributed[l] = dist;
-        parent = dist;
-    }
-    return p;
+    const char* e = std::getenv(env);
+    if (!e || !*e) return dflt;
+    const double v = std::strtod(e, nullptr);
+    return v > 0 ? v : dflt;
 }
 
-// ---------------------------------------------------------------------------------------------
+std::string boundedWait(const std::function<int()>& poll, const std::function<std::string(int)>& errText,
+                        double timeoutS, const char* what)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long spins = 0;; spins++) {
+        const int st = poll();
+        if (st == 0) return "";
+        if (st != 1) return std::string(what) + ": " + errText(st);
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el > timeoutS) {
+            char buf[160];
+            std::snprintf(buf, sizeof buf, ": timed out after %.1f s (a peer is dead, deadlocked or far behind)", el);
+            return std::string(what) + buf;
+        }
+        // spin briefly (a V-cycle's norm readback is ~1 ms away), then back off
+        if (spins > 2000) std::this_thread::sleep_for(std::chrono::microseconds(spins > 20000 ? 1000 : 50));
+    }
+}
+
 // RCCL over xGMI: halo planes are point-to-point send/recv with the two z-neighbours, grouped so
-// each rank's four operations progress together; the norm is an all-gather of one double.
+// each rank's four operations progress together; the norm is an all-gather of one double. The
+// communicator is non-blocking so that no call can hang the host past its deadline: each call (or
+// group) is settled by polling ncclCommGetAsyncError, and sync() polls it beside hipStreamQuery.
 class RcclComm final : public Comm {
 public:
     RcclComm(int rank, int nranks, const void* uid) : r_(rank), n_(nranks)
     {
+        const char* inj = std::getenv("GS_COMM_INJECT_ERROR");
+        injectAt_ = inj ? std::atol(inj) : 0;
+        timeout_ = commTimeoutS("GS_COMM_TIMEOUT_S", 120.0);
         ncclUniqueId id;
         std::memcpy(&id, uid, sizeof(id));
-        ncclOk(ncclCommInitRank(&c_, nranks, id, rank), "ncclCommInitRank");
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        const ncclResult_t e = ncclCommInitRankConfig(&c_, nranks, id, rank, &cfg);
+        if (e != ncclSuccess && e != ncclInProgress) {
+            if (c_) (void)ncclCommAbort(c_);
+            c_ = nullptr;
+            fail("ncclCommInitRankConfig", ncclGetErrorString(e));
+        }
+        settle("ncclCommInitRankConfig", commTimeoutS("GS_COMM_INIT_TIMEOUT_S", 300.0));
     }
     ~RcclComm() override
     {
@@ -75,38 +92,99 @@ public:
     {
         if (n_ == 1) return;
         const size_t cnt = (size_t)(depth * ldz);
-        ncclOk(ncclGroupStart(), "ncclGroupStart");
+        call(ncclGroupStart(), "ncclGroupStart");
         if (r_ > 0) {
-            ncclOk(ncclSend(field + ldz, cnt, ncclDouble, r_ - 1, c_, s), "ncclSend");
-            ncclOk(ncclRecv(field + (1 - depth) * ldz, cnt, ncclDouble, r_ - 1, c_, s), "ncclRecv");
+            call(ncclSend(field + ldz, cnt, ncclDouble, r_ - 1, c_, s), "ncclSend");
+            call(ncclRecv(field + (1 - depth) * ldz, cnt, ncclDouble, r_ - 1, c_, s), "ncclRecv");
         }
         if (r_ + 1 < n_) {
-            ncclOk(ncclSend(field + (nzl - depth + 1) * ldz, cnt, ncclDouble, r_ + 1, c_, s), "ncclSend");
-            ncclOk(ncclRecv(field + (nzl + 1) * ldz, cnt, ncclDouble, r_ + 1, c_, s), "ncclRecv");
+            call(ncclSend(field + (nzl - depth + 1) * ldz, cnt, ncclDouble, r_ + 1, c_, s), "ncclSend");
+            call(ncclRecv(field + (nzl + 1) * ldz, cnt, ncclDouble, r_ + 1, c_, s), "ncclRecv");
         }
-        ncclOk(ncclGroupEnd(), "ncclGroupEnd");
+        call(ncclGroupEnd(), "ncclGroupEnd");
+        settle("halo exchange", timeout_);
     }
 
     void allgather1(const double* in, double* out, hipStream_t s) override
     {
-        ncclOk(ncclAllGather(in, out, 1, ncclDouble, c_, s), "ncclAllGather");
+        call(ncclAllGather(in, out, 1, ncclDouble, c_, s), "ncclAllGather");
+        settle("ncclAllGather", timeout_);
     }
 
     void gatherPlanes(double* field, int64_t ldz, const std::vector<int64_t>& lo, const std::vector<int64_t>& hi,
                       hipStream_t s) override
     {
-        ncclOk(ncclGroupStart(), "ncclGroupStart");
+        call(ncclGroupStart(), "ncclGroupStart");
         for (int q = 0; q < n_; q++) {
             if (hi[q] < lo[q]) continue;
             double* p = field + lo[q] * ldz;
-            ncclOk(ncclBroadcast(p, p, (size_t)((hi[q] - lo[q] + 1) * ldz), ncclDouble, q, c_, s), "ncclBroadcast");
+            call(ncclBroadcast(p, p, (size_t)((hi[q] - lo[q] + 1) * ldz), ncclDouble, q, c_, s), "ncclBroadcast");
         }
-        ncclOk(ncclGroupEnd(), "ncclGroupEnd");
+        call(ncclGroupEnd(), "ncclGroupEnd");
+        settle("plane gather", timeout_);
+    }
+
+    void sync(hipStream_t s) override
+    {
+        const bool inject = injectNow();
+        const std::string err = boundedWait(
+            [&]() -> int {
+                const hipError_t q = hipStreamQuery(s);
+                const int a = asyncState(inject);
+                if (a > 1) return a;
+                if (q == hipSuccess) return 0;
+                if (q != hipErrorNotReady) return -(int)q;
+                return 1;
+            },
+            [](int st) {
+                return st < 0 ? std::string(hipGetErrorString((hipError_t)-st))
+                              : std::string(ncclGetErrorString((ncclResult_t)(st - 2)));
+            },
+            timeout_, "stream sync");
+        if (!err.empty()) abortAndThrow(err);
     }
 
 private:
+    // 1 in progress, 0 settled, 2 + ncclResult_t for an error
+    int asyncState(bool inject)
+    {
+        ncclResult_t a = ncclSuccess;
+        const ncclResult_t e = ncclCommGetAsyncError(c_, &a);
+        if (e != ncclSuccess) a = e;
+        if (inject) a = ncclInternalError;
+        if (a == ncclSuccess) return 0;
+        if (a == ncclInProgress) return 1;
+        return 2 + (int)a;
+    }
+    void call(ncclResult_t e, const char* what)
+    {
+        if (e != ncclSuccess && e != ncclInProgress) abortAndThrow(std::string(what) + ": " + ncclGetErrorString(e));
+    }
+    // GS_COMM_INJECT_ERROR=k: the k-th settle / sync of this communicator sees ncclInternalError
+    bool injectNow() { return injectAt_ > 0 && ++calls_ == injectAt_; }
+    void settle(const char* what, double timeoutS)
+    {
+        const bool inject = injectNow();
+        const std::string err = boundedWait(
+            [&] { return asyncState(inject); },
+            [](int st) { return std::string(ncclGetErrorString((ncclResult_t)(st - 2))); }, timeoutS, what);
+        if (!err.empty()) abortAndThrow(err);
+    }
+    [[noreturn]] void abortAndThrow(const std::string& msg)
+    {
+        if (c_) (void)ncclCommAbort(c_);
+        c_ = nullptr;
+        fail("RCCL", msg.c_str());
+    }
+    [[noreturn]] void fail(const char* what, const char* msg) const
+    {
+        throw Error(std::string(what) + " " + msg + " (rank " + std::to_string(r_) + " of " + std::to_string(n_) +
+                    "); communicator aborted");
+    }
     int r_, n_;
     ncclComm_t c_ = nullptr;
+    long injectAt_ = 0, calls_ = 0;
+    double timeout_ = 120.0;
 };
 
 std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid)
@@ -138,14 +216,28 @@ public:
     void barrier()
     {
         std::unique_lock<std::mutex> lk(m_);
+        if (aborted_) throw Error("loopback exchange aborted: " + why_);
         const int gen = gen_;
         if (++count_ == n_) {
             count_ = 0;
             gen_++;
             cv_.notify_all();
         } else {
-            cv_.wait(lk, [&] { return gen != gen_; });
+            cv_.wait(lk, [&] { return gen != gen_ || aborted_; });
+            if (gen == gen_) throw Error("loopback exchange aborted: " + why_);
         }
+    }
+    void abort(const std::string& why)
+    {
+        std::lock_guard<std::mutex> lk(m_);
+        if (!aborted_) why_ = why;
+        aborted_ = true;
+        cv_.notify_all();
+    }
+    std::string error()
+    {
+        std::lock_guard<std::mutex> lk(m_);
+        return aborted_ ? why_ : std::string();
     }
     int n_;
     std::vector<Slot> slots_;
@@ -154,7 +246,13 @@ private:
     std::mutex m_;
     std::condition_variable cv_;
     int count_ = 0, gen_ = 0;
+    bool aborted_ = false;
+    std::string why_;
 };
+
+void abortLoopbackHub(LoopbackHub& hub, const std::string& why) { hub.abort(why); }
+std::string loopbackHubError(LoopbackHub& hub) { return hub.error(); }
+void loopbackHubBarrier(LoopbackHub& hub) { hub.barrier(); }
 
 std::shared_ptr<LoopbackHub> makeLoopbackHub(int nranks) { return std::make_shared<LoopbackHub>(nranks); }
 

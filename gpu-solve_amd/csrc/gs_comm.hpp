@@ -11,7 +11,9 @@
 // runs N ranks as N threads on one device with device-to-device copies (tests on a single GPU).
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
@@ -34,16 +36,38 @@ public:
     // every rank holds every rank's planes. Asynchronous on s.
     virtual void gatherPlanes(double* field, int64_t ldz, const std::vector<int64_t>& lo, const std::vector<int64_t>& hi,
                               hipStream_t s) = 0;
+    // Waits until everything enqueued on s has completed. The RCCL communicator bounds the wait and
+    // polls the communicator's asynchronous error state while it waits: a dead or deadlocked peer
+    // becomes a gs::Error (communicator aborted) instead of a hang. The solver's one host sync per
+    // V-cycle (the norm readback) goes through here.
+    virtual void sync(hipStream_t s);
 };
 
 // RCCL (NCCL API); uid is the 128-byte ncclUniqueId created by rank 0 (rcclUniqueId) and shared.
+// The communicator is non-blocking (ncclConfig_t::blocking = 0): initialisation and every grouped
+// call are settled by polling ncclCommGetAsyncError under a deadline (GS_COMM_INIT_TIMEOUT_S, default
+// 300 s; GS_COMM_TIMEOUT_S, default 120 s, also for sync()). On an error or a timeout the communicator
+// is aborted (ncclCommAbort) and gs::Error("RCCL ... (rank r of n)") is thrown. GS_COMM_INJECT_ERROR=k
+// (tests) makes the k-th settle or sync of the communicator see ncclInternalError.
 std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid);
 void rcclUniqueId(void* uid);
+
+// The bounded wait behind RcclComm::sync / settle (host logic, unit-tested on the CPU through
+// gs_debug_bounded_wait). poll() returns 0 done, 1 still pending, or any other value = an error whose
+// text errText(value) gives. Returns "" on completion, else the error / timeout message.
+std::string boundedWait(const std::function<int()>& poll, const std::function<std::string(int)>& errText,
+                        double timeoutS, const char* what);
+double commTimeoutS(const char* env, double dflt);
 
 // Loopback: nranks threads of one process on one device share a hub.
 class LoopbackHub;
 std::shared_ptr<LoopbackHub> makeLoopbackHub(int nranks);
 std::unique_ptr<Comm> makeLoopbackComm(const std::shared_ptr<LoopbackHub>& hub, int rank);
+// A rank that fails calls this: every thread parked in (or later reaching) a hub barrier throws, so
+// all rank threads unwind instead of waiting forever. loopbackHubError: the first message ("" = none).
+void abortLoopbackHub(LoopbackHub& hub, const std::string& why);
+std::string loopbackHubError(LoopbackHub& hub);
+void loopbackHubBarrier(LoopbackHub& hub); // throws once the hub is aborted
 
 // Plane ownership of every level (pure host logic).
 struct SlabPlan {

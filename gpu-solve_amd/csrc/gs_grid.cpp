@@ -2,7 +2,9 @@
 #include "gs_grid.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <iostream>
 #include <string>
@@ -70,6 +72,45 @@ StreamGuard::StreamGuard() { check((int)hipStreamCreateWithFlags(&s, hipStreamNo
 StreamGuard::~StreamGuard()
 {
     if (s) (void)hipStreamDestroy(s);
+}
+
+// ---------------------------------------------------------------------------------------------
+void LevelClock::mark(hipStream_t s, int level, bool begin)
+{
+    if (!on) return;
+    const std::size_t k = segLevel.size();
+    if (begin) {
+        if (ev.size() < 2 * (k + 1)) {
+            for (int j = 0; j < 2; j++) {
+                hipEvent_t e = nullptr;
+                check((int)hipEventCreate(&e), "hipEventCreate");
+                ev.push_back(e);
+            }
+        }
+        segLevel.push_back(level);
+        check((int)hipEventRecord(ev[2 * k], s), "hipEventRecord");
+    } else if (k > 0) {
+        check((int)hipEventRecord(ev[2 * k - 1], s), "hipEventRecord");
+    }
+}
+
+void LevelClock::collect()
+{
+    if (!on) return;
+    for (std::size_t k = 0; k < segLevel.size(); k++) {
+        float ms = 0.f;
+        check((int)hipEventSynchronize(ev[2 * k + 1]), "hipEventSynchronize");
+        check((int)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]), "hipEventElapsedTime");
+        const std::size_t l = (std::size_t)segLevel[k];
+        if (levelMs.size() <= l) levelMs.resize(l + 1, 0.0);
+        levelMs[l] += ms;
+    }
+    segLevel.clear();
+}
+
+LevelClock::~LevelClock()
+{
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -155,6 +196,11 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
             }
     }
     if (mode == NEWTON) newtonF = DeviceField(levels_[0].geom.nx, levels_[0].geom.ny, levels_[0].geom.nz, s);
+    {
+        const char* e = std::getenv("GS_METRICS");
+        clock.on = e && *e && *e != '0';
+        clock.levelMs.assign(nlev, 0.0);
+    }
     // the overlapped sweep splits a level into 3 launches, each with its own partials region
     maxParts = 2 * maxParts + 4096;
     check((int)hipMalloc((void**)&partials_, sizeof(double) * maxParts), "hipMalloc(partials)");
@@ -186,8 +232,15 @@ HipGridData::~HipGridData()
 double HipGridData::readNorm()
 {
     check((int)hipMemcpyAsync(hNorm_, dNorm_, sizeof(double), hipMemcpyDeviceToHost, stream_.s), "hipMemcpyAsync");
-    check((int)hipStreamSynchronize(stream_.s), "hipStreamSynchronize");
+    sync();
     return *hNorm_;
+}
+
+void HipGridData::sync()
+{
+    // distributed: a bounded wait that also polls the communicator's error state (gs_comm.hpp)
+    if (comm_ && comm_->size() > 1) comm_->sync(stream_.s);
+    else check((int)hipStreamSynchronize(stream_.s), "hipStreamSynchronize");
 }
 
 void HipGridData::halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth)
@@ -506,6 +559,7 @@ double HipSolver::speculativeSweep(HipGridData& grid, int* sweeps)
         grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, s);
     }
     if (sweeps) *sweeps = pair ? 2 : 1;
+    grid.clock.mark(s, 0, false); // closes the caller's segment before the norm's host sync
     return finishNorm(grid, n);
 }
 
@@ -523,7 +577,9 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
     const hipStream_t s = grid.stream();
     // levels lc.. run as one gs_coarse_cycle launch (lc == nl: none); the host loops descend to lc
     const std::size_t lc = grid.coarseFrom, last = std::min(lc, nl - 1);
+    const auto tWall = std::chrono::steady_clock::now();
     for (std::size_t i = 0; i < last; i++) {
+        grid.clock.mark(s, (int)i, true);
         std::size_t pre = grid.preSmoothing;
         if (i == 0 && pending && *pending > 0 && pre >= (std::size_t)*pending) {
             grid.getLevel(0).v.swap(grid.getLevel(0).vAlt); // adopt the speculative first sweep(s)
@@ -586,12 +642,16 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
                   "gs_apply_op_add");
             grid.halo(C, C.f, s);
         }
+        grid.clock.mark(s, (int)i, false);
     }
+    grid.clock.mark(s, (int)std::min(lc, nl - 1), true);
     if (lc < nl) coarseCycle(grid, lc);
     else jacobi(grid, nl - 1, grid.preSmoothing + grid.postSmoothing); // coarsest "solve"
+    grid.clock.mark(s, (int)std::min(lc, nl - 1), false);
     for (std::size_t i = last; i > 0; i--) {
         auto& C = grid.getLevel(i);
         auto& F = grid.getLevel(i - 1);
+        grid.clock.mark(s, (int)(i - 1), true);
         materialize(grid, i); // only if the level had no sweep at all
         static const bool noFusedPro = std::getenv("GS_NO_FUSED_PROLONG") != nullptr;
         if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && proWorthIt(grid, i - 1) && proSlabOk(grid, i - 1) &&
@@ -621,6 +681,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
             F.v.swap(F.vAlt);
             F.vZero = false;
             jacobi(grid, i - 1, grid.postSmoothing - 2);
+            grid.clock.mark(s, (int)(i - 1), false);
             continue;
         }
         // v^h += P (v^2h [- restV^2h])   (CpuSolver.cpp:121-132, interpolate + v += e fused)
@@ -629,9 +690,23 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
               "gs_prolong_add");
         grid.halo(F, F.v, s, grid.vDepth(F));
         jacobi(grid, i - 1, grid.postSmoothing);
+        grid.clock.mark(s, (int)(i - 1), false);
     }
-    if (pending && speculationEnabled(grid)) return speculativeSweep(grid, pending);
-    return compResidual(grid, 0, false, true);
+    // the closing norm: the next cycle's first pre-smoothing step (speculative) or a residual pass
+    grid.clock.mark(s, 0, true);
+    double res;
+    if (pending && speculationEnabled(grid)) {
+        res = speculativeSweep(grid, pending); // closes the segment before its host sync
+    } else {
+        res = compResidual(grid, 0, false, true);
+        grid.clock.mark(s, 0, false); // after the norm's host sync: over-counts by the sync latency
+    }
+    if (grid.clock.on) {
+        grid.clock.collect();
+        grid.clock.cycles++;
+        grid.clock.wallMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tWall).count();
+    }
+    return res;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -640,7 +715,9 @@ void NewtonSolver::solve(HipGridData& grid)
 {
     auto& L0 = grid.getLevel(0);
     const hipStream_t s = grid.stream();
-    const bool print = grid.rank() == 0;
+    // the reference prints unconditionally (NewtonSolver.cpp:16,27); printProgress defaults to true,
+    // so GpuSolve-hip does too, and library callers silence it without touching std::cout
+    const bool print = grid.printProgress && grid.rank() == 0;
     check((int)hipMemcpyAsync(grid.newtonF.data(), L0.f.data(), sizeof(double) * L0.f.span(), hipMemcpyDeviceToDevice,
                               s),
           "hipMemcpyAsync");
@@ -698,6 +775,40 @@ void NewtonSolver::findError(HipGridData& grid)
     auto& L0 = grid.getLevel(0);
     // whole local array, ghost planes included: both operands' ghosts are current, so the sum's are
     check(gs_axpy(L0.newtonV.data(), L0.v.data(), 1.0, L0.v.span(), grid.stream()), "gs_axpy");
+}
+
+// "[gs] mlups=... gbps=... pct_peak=... vcycle_ms=... cycles=... level_ms=a,b,..." over the V-cycles
+// timed so far (GS_METRICS). mlups: level-0 smoother updates ((pre+post) x N0 per cycle) per second of
+// V-cycle wall time; gbps: SURVEY.md §8(d)'s compulsory V-cycle traffic model, per level N_l points
+// ((pre+post) x 24 B + 16 B residual/restriction + 16 B prolongation/correction + 2 B coarse, the
+// coarsest level only its sweeps) + 16 B x N0 for the closing norm, per second; pct_peak against
+// 8000 GB/s. level_ms: device time per level and cycle. Does not match runExperiments.py:46's regex.
+std::string metricsLine(const HipGridData& grid)
+{
+    const LevelClock& c = grid.clock;
+    if (c.cycles == 0) return "[gs] no V-cycle timed";
+    const double ms = c.wallMs / c.cycles;
+    const double sweeps = (double)(grid.preSmoothing + grid.postSmoothing);
+    double bytes = 0.0;
+    const std::size_t nl = grid.numLevels();
+    for (std::size_t l = 0; l < nl; l++) {
+        const auto& d = grid.getLevel(l).levelDim;
+        const double n = (double)d[0] * (double)d[1] * (double)d[2];
+        bytes += n * (sweeps * 24.0 + (l + 1 < nl ? 34.0 : 0.0));
+    }
+    const auto& d0 = grid.getLevel(0).levelDim;
+    const double n0 = (double)d0[0] * (double)d0[1] * (double)d0[2];
+    bytes += 16.0 * n0;
+    const double gbps = bytes / (ms * 1e-3) / 1e9;
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "[gs] mlups=%.1f gbps=%.1f pct_peak=%.1f vcycle_ms=%.3f cycles=%d level_ms=",
+                  sweeps * n0 / (ms * 1e-3) / 1e6, gbps, 100.0 * gbps / 8000.0, ms, c.cycles);
+    std::string out = buf;
+    for (std::size_t l = 0; l < c.levelMs.size(); l++) {
+        std::snprintf(buf, sizeof buf, "%s%.4f", l ? "," : "", c.levelMs[l] / c.cycles);
+        out += buf;
+    }
+    return out;
 }
 
 void dumpField(HipGridData& grid, std::size_t level, const std::string& path)

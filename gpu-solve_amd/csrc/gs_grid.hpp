@@ -15,6 +15,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "gpusolve_hip.h"
@@ -56,6 +57,21 @@ struct StreamGuard {
     ~StreamGuard();
 };
 
+// Per-level device time of the V-cycles (GS_METRICS=1 when the grid is created): HIP events around every level's
+// down-leg (smoothing, residual + restriction) and up-leg (prolongation + smoothing) work on the
+// compute stream, read back after each cycle's norm sync. Off: no event is recorded.
+struct LevelClock {
+    bool on = false;
+    int cycles = 0;
+    double wallMs = 0.0;         // host wall time of the V-cycles (norm readbacks included)
+    std::vector<double> levelMs; // device ms per level, summed over cycles
+    std::vector<hipEvent_t> ev;  // ev[2k], ev[2k+1] bracket segment k of the current cycle
+    std::vector<int> segLevel;   // level of segment k
+    void mark(hipStream_t s, int level, bool begin);
+    void collect();              // after a host sync: add this cycle's segments
+    ~LevelClock();
+};
+
 class HipGridData final : public GridParams {
 public:
     struct LevelData {
@@ -95,12 +111,14 @@ public:
     // levels coarseFrom .. numLevels()-1 run as ONE gs_coarse_cycle launch in every V-cycle
     // (numLevels(): none); set from GS_COARSE_POINTS at construction
     std::size_t coarseFrom = 0;
+    LevelClock clock; // per-level timing (GS_METRICS)
 
     // residual-norm plumbing: per-block partials, device scalars, pinned host scalar
     double* partials() const { return partials_; }
     double* dNorm() const { return dNorm_; }
     double* dRankSums() const { return dRankSums_; }
     double readNorm(); // async D2H of dNorm + stream sync: the one host sync per V-cycle
+    void sync();       // stream sync (bounded, error-polling when distributed over RCCL)
 
     // ghost planes of a distributed level's field (no-op otherwise); depth 2 where possible for
     // iterate fields (the fused pair reads two ghost planes of v)
@@ -157,6 +175,9 @@ public:
     static void findError(HipGridData& grid);
     static thread_local std::vector<double>* history;
 };
+
+// The optional machine-readable metrics line of GpuSolve-hip (GS_METRICS=1), see gs_grid.cpp.
+std::string metricsLine(const HipGridData& grid);
 
 // Vector3::dump (src/cpu/Vector3.cpp:56-78) of level `level`'s iterate v (this rank's slab).
 void dumpField(HipGridData& grid, std::size_t level, const std::string& path);

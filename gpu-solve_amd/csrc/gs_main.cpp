@@ -10,7 +10,9 @@
 // Exit codes as the reference: 1 for a missing/non-file config or an invalid mode; a backend
 // error prints "Exception: <what>" to stderr and exits 0 (the reference's GPU-backend behaviour,
 // src/main.cpp:96-111). Added: stencil offsets outside {-1,0,1} (out-of-bounds reads in the
-// reference) are rejected like an invalid mode.
+// reference) are rejected like an invalid mode. With GS_METRICS=1 one more line follows the solve:
+// "[gs] mlups=... gbps=... pct_peak=... vcycle_ms=... cycles=... level_ms=..." (not matched by the
+// reference harness's regex, runExperiments.py:46).
 #include <iostream>
 #include <string>
 
@@ -50,6 +52,7 @@ int main(int argc, char* argv[])
         gs::HipGridData grid(gridParams);
         if (gridParams.mode == gs::GridParams::NEWTON) gs::NewtonSolver::solve(grid);
         else gs::HipSolver::solve(grid);
+        if (grid.clock.on) std::cout << gs::metricsLine(grid) << '\n'; // GS_METRICS=1 (added, optional)
         if (argc > 2) gs::dumpField(grid, 0, argv[2]); // Vector3::dump of the solution (added, optional)
     } catch (std::exception& e) {
         std::cerr << "Exception: " << e.what() << '\n';

@@ -117,6 +117,7 @@ DRIVER_API = {
     "gs_grid_download": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
     "gs_grid_upload": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
     "gs_grid_sync": (C.c_int, [C.c_void_p]),
+    "gs_grid_metrics": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int, dptr, C.c_int]),
     "gs_dump_write": (C.c_int, [dptr, i64, i64, i64, C.c_char_p]),
     "gs_grid_dump": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
     "gs_grid_time_jacobi": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]),
@@ -127,6 +128,8 @@ DRIVER_API = {
     "gs_grid_create_rccl": (C.c_void_p, [C.POINTER(gs_params), C.c_int, C.c_int, C.POINTER(C.c_ubyte)]),
     "gs_zslab_loopback_run": (C.c_int, [C.POINTER(gs_params), C.c_int, i64, C.c_int, C.c_int, dptr, C.c_int,
                                         C.POINTER(C.c_int), dptr]),
+    "gs_debug_bounded_wait": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_char_p, C.c_int]),
+    "gs_debug_loopback_abort": (C.c_int, [C.c_int, C.c_int]),
     "gs_last_error": (C.c_char_p, []),
 }
 

@@ -62,6 +62,10 @@ hipStream_t gs_grid_stream(void* grid);
 int gs_grid_download(void* grid, int level, int field, double* host);
 int gs_grid_upload(void* grid, int level, int field, const double* host);
 int gs_grid_sync(void* grid);
+/* With GS_METRICS=1 in the environment when the grid was created: the "[gs] mlups=... gbps=...
+ * pct_peak=... vcycle_ms=... cycles=... level_ms=..." line GpuSolve-hip prints after its solve (over
+ * the V-cycles run so far), and the device ms per level and V-cycle. Non-zero if metrics are off. */
+int gs_grid_metrics(void* grid, char* line, int cap, double* level_ms, int levels_cap);
 /* Vector3::dump (src/cpu/Vector3.cpp:56-78) of a padded field: header "Px Py Pz" then "x y z value"
  * per point, x outermost, z innermost, values in the iostream default format (%g). path NULL or
  * empty (or not openable): the lines go to stdout without the header, as in the reference.
@@ -95,6 +99,15 @@ void* gs_grid_create_rccl(const gs_params* p, int rank, int nranks, const unsign
  * min_points as in gs_zslab_plan. For testing the distributed path on one GPU. */
 int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, int sweeps, int solve, double* hist,
                           int cap, int* count, double* v_host);
+
+/* ---- failure-detection self-tests (host logic only; no GPU) ----
+ * gs_debug_bounded_wait: the bounded wait that settles every RCCL call and sync (gs_comm.hpp),
+ * driven by a fake poll: scenario 0 completes at poll k, 1 reports ncclInternalError at poll k,
+ * 2 never completes (times out after timeout_s). Returns 0 on completion, 1 with the message in msg.
+ * gs_debug_loopback_abort: nranks threads meet at loopback-hub barriers and failing_rank throws;
+ * returns how many threads unwound (nranks = none left hanging); gs_last_error() = the first error. */
+int gs_debug_bounded_wait(int scenario, int k, double timeout_s, char* msg, int cap);
+int gs_debug_loopback_abort(int nranks, int failing_rank);
 
 const char* gs_last_error(void);
 

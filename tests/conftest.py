@@ -58,3 +58,13 @@ def stencil_from_text(text):
 
 def rel(a, b):
     return abs(a - b) / max(abs(b), 1e-300)
+
+
+@pytest.fixture(scope="session")
+def huge_histories():
+    return load_json("huge_histories.json")
+
+
+@pytest.fixture(scope="session")
+def config3_histories():
+    return load_json("config3_histories.json")

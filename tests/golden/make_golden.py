@@ -106,9 +106,52 @@ def large_cases():
     }
 
 
-def gen_histories(cases, path):
+def config3_cases():
+    """BASELINE config #3 as stated (10 V-cycles) and its converging companion, plus config #4's
+    companion for more than two Newton iterations."""
+    return {
+        "m0_n511_2+2_x10": case(511, maxiter=10),
+        "m0_n512_2+2_x10": case(512, maxiter=10),
+        "m2_n511_2+2_x4": case(511, mode=2, maxiter=4),
+    }
+
+
+def huge_cases():
+    """BASELINE config #5's grid (1024^3) and its companion 1023^3, two linear V-cycles each. The
+    reference holds 6 arrays per level (src/cpu/CpuGridData.cpp:32-39): ~55 GiB at this size, so the
+    probe runs under a virtual-memory cap (it fails with bad_alloc instead of waking the OOM killer)."""
+    return {
+        "m0_n1023_2+2": case(1023, maxiter=2),
+        "m0_n1024_2+2": case(1024, maxiter=2),
+    }
+
+
+def gen_histories(cases, path, vmem_kb=None):
     res = {}
+    if os.path.exists(path) and vmem_kb:  # resumable: the huge cases take minutes each
+        with open(path) as f:
+            res = json.load(f)
     for name, c in cases.items():
+        if name in res:
+            continue
+        if vmem_kb:
+            import resource
+
+            def cap():
+                resource.setrlimit(resource.RLIMIT_AS, (vmem_kb * 1024, vmem_kb * 1024))
+            with tempfile.NamedTemporaryFile("w", suffix=".conf", delete=False) as f:
+                f.write(config_text(c))
+                conf = f.name
+            try:
+                out = subprocess.run([PROBE, "solve", conf], check=True, capture_output=True, text=True,
+                                     preexec_fn=cap).stdout
+            finally:
+                os.unlink(conf)
+            res[name] = {"config": c, "history": parse_history(out)}
+            print(f"  {name}: {res[name]['history']}", flush=True)
+            with open(path, "w") as f:
+                json.dump(res, f, indent=1)
+            continue
         out = run_history(c)
         res[name] = {"config": c, "history": parse_history(out)}
         print(f"  {name}: {len(res[name]['history'])} values", flush=True)
@@ -242,7 +285,15 @@ def main():
     ap.add_argument("--large", action="store_true", help="also the 511^3/512^3 anchors (several minutes)")
     ap.add_argument("--only-large", action="store_true")
     ap.add_argument("--only-dumps", action="store_true")
+    ap.add_argument("--config3", action="store_true", help="only the 10-cycle 511^3/512^3 anchors")
+    ap.add_argument("--huge", action="store_true", help="only the 1023^3/1024^3 anchors (~55 GiB of host RAM)")
     a = ap.parse_args()
+    if a.config3:
+        gen_histories(config3_cases(), os.path.join(HERE, "config3_histories.json"), vmem_kb=60 << 20)
+        return
+    if a.huge:
+        gen_histories(huge_cases(), os.path.join(HERE, "huge_histories.json"), vmem_kb=60 << 20)
+        return
     for exe in (PROBE, REFEXE):
         if not os.path.exists(exe):
             sys.exit(f"{exe} missing: run `make -C oracle ref` (needs /root/reference)")

@@ -1,0 +1,58 @@
+"""BASELINE config #5's grid (1024^3 linear 2+2, Z-slab over 8 GPUs) on ONE MI355X.
+
+1. The single-GPU 1024^3 and 1023^3 solves against the reference's own histories
+   (tests/golden/huge_histories.json: oracle/_ref/ref_probe = src/cpu, run in the build container,
+   ~55 GiB of host RAM), 2 V-cycles each. Every level-0 pass runs the 1024-point-row kernels.
+2. The 8-rank Z-slab solve (gs_zslab_loopback_run: 8 rank threads, 8 slabs of 1024 x 1024 x 128, ghost
+   planes exchanged by device copies under the RCCL communicator's ordering contract, default
+   agglomeration threshold) against the single-GPU 1024^3 solve: level-0 fields bit-identical,
+   histories to 1e-12 (rank partials are summed in rank order). This is the per-rank work of the 8-GPU
+   run: slab pairs, slab residual+restriction, slab prolongation pair, replicated coarse levels.
+Reference operator: /root/reference/src/cpu/CpuSolver.cpp:85-139 (vcycle)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+torch = pytest.importorskip("torch")
+import gpusolve as gsv  # noqa: E402
+from conftest import rel  # noqa: E402
+
+
+@pytest.mark.parametrize("name", ["m0_n1023_2+2", "m0_n1024_2+2"])
+def test_config5_grid_vs_reference(huge_histories, name):
+    c = huge_histories[name]["config"]
+    p = gsv.GridParams(maxiter=c["maxiter"], tol=c["tol"], gridDim=(c["X"], c["Y"], c["Z"]), mode=c["mode"],
+                       preSmoothing=c["pre"], postSmoothing=c["post"], omega=c["omega"], gamma=c["gamma"])
+    with gsv.HipGridData(p) as g:
+        got = gsv.HipSolver.solve(g)
+    ref = huge_histories[name]["history"]
+    assert len(got) == len(ref) == c["maxiter"] + 1
+    for a, b in zip(got, ref):
+        assert rel(a, b) < 1e-9, (name, a, b)
+
+
+def test_config5_eight_slabs_bit_identical_to_one_gpu():
+    n = 1024
+    p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=(n, n, n), mode=0, preSmoothing=2, postSmoothing=2)
+    with gsv.HipGridData(p) as g:
+        ref_h = gsv.HipSolver.solve(g)
+        ref_v = np.empty((n + 2, n + 2, n + 2))  # [z][y][x]
+        assert gsv.driver().gs_grid_download(g.handle, 0, 0, ref_v.ctypes.data_as(gsv._abi.dptr)) == 0
+    torch.cuda.synchronize()
+    d = gsv.driver()
+    ap = p.to_abi()
+    v = np.zeros((n + 2, n + 2, n + 2))
+    hist = (C.c_double * 8)()
+    cnt = C.c_int(0)
+    rc = d.gs_zslab_loopback_run(C.byref(ap), 8, -1, 0, 1, hist, 8, C.byref(cnt), v.ctypes.data_as(gsv._abi.dptr))
+    assert rc == 0, d.gs_last_error().decode()
+    h = list(hist[: cnt.value])
+    assert len(h) == len(ref_h) == 3
+    for a, b in zip(h, ref_h):
+        assert rel(a, b) < 1e-12, (a, b)
+    # interior planes of every slab (the loopback writes planes 1..n; x / y padding included)
+    for z0 in range(1, n + 1, 128):
+        assert np.array_equal(v[z0: z0 + 128], ref_v[z0: z0 + 128]), f"planes {z0}..{z0 + 127}"

@@ -42,6 +42,23 @@ def test_rccl_one_rank_solve_bit_identical(mode):
     np.testing.assert_array_equal(v, ref_v)
 
 
+def test_rccl_injected_error_aborts(monkeypatch):
+    """GS_COMM_INJECT_ERROR=1: the first settle of the non-blocking communicator (its initialisation)
+    sees ncclInternalError; the communicator is aborted and the grid creation fails with the message
+    GpuSolve-hip would print after "Exception: " instead of hanging."""
+    monkeypatch.setenv("GS_COMM_INJECT_ERROR", "1")
+    drv = gsv.driver()
+    uid = (C.c_ubyte * 128)()
+    assert drv.gs_rccl_unique_id(uid) == 0
+    p = gsv.GridParams(maxiter=1, gridDim=(16, 16, 16)).to_abi()
+    assert not drv.gs_grid_create_rccl(C.byref(p), 0, 1, uid)
+    msg = drv.gs_last_error().decode()
+    assert "RCCL" in msg and "internal error" in msg and "rank 0 of 1" in msg and "aborted" in msg, msg
+    monkeypatch.delenv("GS_COMM_INJECT_ERROR")
+    g = rccl_grid(gsv.GridParams(maxiter=1, gridDim=(16, 16, 16)))  # a healthy communicator afterwards
+    g.close()
+
+
 def test_rccl_bad_rank_rejected():
     drv = gsv.driver()
     uid = (C.c_ubyte * 128)()

@@ -129,3 +129,43 @@ def test_example_config_verbatim():
     assert [re.sub(r" Took \d+ms", "", l) for l in lines[3:]] == [
         "newton iter: 0 residual: 12.3816", "newton iter: 1 residual: 0.527004",
         "newton iter: 2 residual: 0.0222718", "newton iter: 3 residual: 0.00093763"]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["m0_n511_2+2_x10", "m0_n512_2+2_x10", "m2_n511_2+2_x4"])
+def test_config3_ten_cycles(config3_histories, name):
+    """BASELINE config #3 as stated (512^3 linear, 10 V-cycles) and its companion 511^3, plus 4 Newton
+    iterations at 511^3 (config #4's companion), against the reference's own histories."""
+    case = config3_histories[name]
+    p = params_from_case(case["config"])
+    with gsv.HipGridData(p) as g:
+        got = gsv.HipSolver.solve(g)
+    ref = case["history"]
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert rel(a, b) < tol_for(p.mode), (name, a, b)
+
+
+def test_executable_metrics_line(tmp_path):
+    """GS_METRICS=1: the reference's stdout unchanged, plus one "[gs] ..." line after the solve that the
+    reference harness regex (runExperiments.py:46) does not match; per-level device ms for every level."""
+    from conftest import load_json
+    case = load_json("stdout.json")["m0_n31_2+2"]
+    conf = tmp_path / "m.conf"
+    conf.write_text(params_from_case(case["config"]).config_text())
+    env = dict(os.environ, GS_METRICS="1")
+    out = subprocess.run([gsv._abi.EXECUTABLE, str(conf)], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    assert _norm_lines(lines[:-1]) == case["stdout"]
+    last = lines[-1]
+    assert last.startswith("[gs] mlups=")
+    kv = dict(t.split("=", 1) for t in last[5:].split())
+    assert float(kv["mlups"]) > 0 and float(kv["gbps"]) > 0 and 0 < float(kv["pct_peak"]) < 100
+    assert int(kv["cycles"]) == case["config"]["maxiter"]
+    nlev = 5  # 31^3: 31, 15, 7, 3, 1
+    ms = [float(x) for x in kv["level_ms"].split(",")]
+    assert len(ms) == nlev and all(x >= 0 for x in ms) and ms[0] > 0
+    pat = re.compile(r"iter: (\d+) residual: ([\d\.e-]+) Took (\d+)ms")
+    assert len(pat.findall(out.stdout)) == case["config"]["maxiter"]
+    assert not pat.search(last)
