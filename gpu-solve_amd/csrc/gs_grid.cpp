@@ -178,7 +178,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         // on the thinnest slab, as the kernel's fill count grows with the plane count
         gs_level thin = L.geom;
         thin.nz = L.minPlanes;
-        L.fusedPairs = !noPairs && gs_jacobi_sweep2_supported(&stencilAbi, &thin) == 2 &&
+        L.fusedPairs = !noPairs && gs_jacobi_sweep2_supported_mode(&stencilAbi, &thin, (int)mode) == 2 &&
                        (!L.distributed || L.minPlanes >= 2);
     }
     // The coarse end of the V-cycle runs as one gs_coarse_cycle launch from the first level of at

@@ -1527,8 +1527,15 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
 // is consumed (the loads stay in flight as before): X-pass values of the two coarse planes under the
 // current fine planes live in registers (W0, W1) and the next coarse plane is prefetched one step
 // ahead; the z-chunk is even, so every fine plane's parity, hence its Y/Z combination, is static.
+//
+// XH (rows of more than 2 * WAVE * WX points): the row is split into column blocks of 2 * WAVE * WX
+// points, one per block. The column just outside a block edge that is interior belongs to the
+// neighbouring block; the edge wave computes what its LDS slot would hold there itself: v of plane z at
+// that column (loads) and sweep 1 of plane z-1 at that column, evaluated lane-parallel one local row per
+// lane (lane j <-> local row j, y-neighbours by lane shifts, x-neighbours loaded) with the same point
+// expression, so every output is bit-identical to two gs_jacobi_sweep calls.
 template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0,
-          int PFD = 1>
+          int PFD = 1, bool XH = false>
 __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* __restrict__ v,
                                                            const double* __restrict__ f, const double* __restrict__ w,
                                                            double* __restrict__ out, double* __restrict__ partials,
@@ -1538,6 +1545,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                                                            int64_t cldy, int64_t cldz)
 {
     static_assert(PRO == 0 || (SPEC && !ZV && RY % 2 == 0), "fused prolongation: per-wave code, even RY");
+    static_assert(!XH || (PRO == 0 && MODE != GS_NEWTON && RY + 2 <= WAVE), "column blocks: LINEAR / NONLINEAR pairs");
     constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
     constexpr int NE = NV + RY; // x-edge values per wave side: v rows 0..RY, sweep-1 rows 1..RY
     __shared__ double red[2 * WXMAX];
@@ -1553,13 +1561,18 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     const int tid = threadIdx.x + WAVE * (threadIdx.y + WX * threadIdx.z);
     for (int i = tid; i < 2 * 2 * (WXMAX + 2) * 2 * NE; i += WAVE * WX * 2) (&edge[0][0][0][0][0])[i] = 0.0;
     __syncthreads();
-    const int x0 = 1 + wx * (2 * WAVE);
+    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+    // XH: column blocks fastest (the two edges a pair of neighbours share are read on one XCD)
+    const int BW = 2 * WAVE * WX; // columns per block
+    const int nh = XH ? (nx + BW - 1) / BW : 1;
+    const int hx = XH ? (int)((tile % gridDim.x) % nh) : 0;
+    const int xb = 1 + hx * BW;
+    const int x0 = xb + wx * (2 * WAVE);
     const int x = x0 + 2 * lane;
     const int xl = min(x, nx + 1);
     const bool bx0 = x > nx, bx1 = x + 1 > nx;
     const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
-    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-    const int y0 = 1 + (int)(tile % gridDim.x) * (2 * RY);
+    const int y0 = 1 + (int)((tile % gridDim.x) / nh) * (2 * RY);
     const int zb = 1 + (int)(tile / gridDim.x) * ZC;
     const int ze = min(zb + ZC - 1, nz);
     const bool mir = wy != 0;
@@ -1575,6 +1588,19 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     }
     auto planeok = [&](int z) { return (z >= 1 && z <= nz) || (z == 0 && zlo) || (z == nz + 1 && zhi); };
     auto at = [&](const double* base, int j, int z) { return base + xl + roff[j + 1] + (int64_t)z * ldz; };
+    // XH edge column xe (wave 0: left of the block, wave WX-1: right of it) when it is interior
+    const bool eL = XH && wx == 0 && hx > 0;
+    const bool eR = XH && wx == WX - 1 && xb + BW <= nx;
+    const bool edg = eL || eR; // wave-uniform
+    const int xe = eL ? xb - 1 : xb + BW;
+    int64_t eroff = 0; // lane j <-> local row j = 0..RY+1
+    bool erowc = false;
+    if (XH) {
+        const int y = yof(min(lane, RY + 1));
+        eroff = (int64_t)min(max(y, 0), ny + 1) * ldy;
+        erowc = y >= 1 && y <= ny;
+    }
+    auto eat = [&](const double* base, int dx, int z) { return base + (xe + dx) + eroff + (int64_t)z * ldz; };
 
     // PFD: prefetch distance in plane steps. 1: two operand slots (this step's, the next one's in
     // flight); 2: four named slots, three live (this step's and the next two in flight), the z loop
@@ -1596,6 +1622,9 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
 #pragma unroll
     for (int j = 0; j < RY; j++) V1p[j] = make_double2(0.0, 0.0);
+    // XH edge column: v at plane z+1 (EA), its x-neighbours (EXm, EXp) and f at plane z, per slot;
+    // EP / EC: v at planes z-1 / z; ES1c: sweep 1 at plane z-1
+    double EA[XH ? NS : 1], EXm[XH ? NS : 1], EXp[XH ? NS : 1], EF[XH ? NS : 1], EP = 0.0, EC = 0.0, ES1c = 0.0;
     auto load_slot = [&](const int s, const int z, const int zv) {
 #pragma unroll
         for (int j = 0; j < NV; j++) {
@@ -1604,11 +1633,23 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             if (MODE == GS_NEWTON) WL[s][j] = ld2(at(w, j, z));
         }
         HL[s] = ldv2<ZV>(at(v, -1, z));
+        if constexpr (XH) {
+            if (edg) {
+                EA[s] = ldv1<ZV>(eat(v, 0, zv));
+                EXm[s] = ldv1<ZV>(eat(v, -1, z));
+                EXp[s] = ldv1<ZV>(eat(v, 1, z));
+                EF[s] = *eat(f, 0, z);
+            }
+        }
     };
 #pragma unroll
     for (int j = 0; j < NV; j++) {
         Vp[j] = ldv2<ZV>(at(v, j, zb - 2));
         Vc[j] = ldv2<ZV>(at(v, j, zb - 1));
+    }
+    if (XH && edg) {
+        EP = ldv1<ZV>(eat(v, 0, zb - 2));
+        EC = ldv1<ZV>(eat(v, 0, zb - 1));
     }
     // ---- fused prolongation (PRO): coarse rows cyb .. cyb+NCR-1 lie under the wave's fine rows ----
     constexpr int NCR = RY / 2 + 2;
@@ -1742,14 +1783,41 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             }
             const double2 vY = yrow[ph][wy ^ 1][wx][0][lane]; // v(z) at local row RY+1
             const double2 sY = yrow[ph][wy ^ 1][wx][1][lane]; // sweep-1(z-1) at local row RY+1
+            if constexpr (XH) {
+                // the edge column beyond an interior block edge: v(z) rows 0..RY, sweep-1(z-1) rows 1..RY
+                if (edg) {
+#pragma unroll
+                    for (int i = 0; i < NE; i++) {
+                        const double e = i < NV ? EC : ES1c;
+                        const int ln = i < NV ? i : i - NV + 1;
+                        const long long b = __double_as_longlong(e);
+                        const int lo = __builtin_amdgcn_readlane((int)b, ln), hi = __builtin_amdgcn_readlane((int)(b >> 32), ln);
+                        const double u = __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+                        if (eL) CL[i] = u;
+                        else CR[i] = u;
+                    }
+                }
+            }
 
             // ---- the two sweeps; wave 1 (mirrored rows) runs its own copy of the code, so the swap of
             // its y-neighbours costs no selects ----
             double2 V1n[NV];
             double2 Acur[RY], Ecur[RY]; // NEWTON terms of sweep 1's own rows (-> Aprev / Eprev)
             const bool pz = planeok(z);
+            double ES1n = 0.0;
             auto sweeps = [&](auto mirc) {
                 const bool M = mirc.get();
+                if constexpr (XH) {
+                    // sweep 1 at plane z on the edge column, local row = lane (rows 1..RY are used)
+                    if (edg) {
+                        const double c = EC;
+                        const double lm = lane_from_left<true>(EC, 0.0), lp = lane_from_right<true>(EC, 0.0);
+                        const double ym = M ? lp : lm, yp = M ? lm : lp;
+                        const double a = op_value<MODE>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP, 0.0);
+                        const double nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
+                        ES1n = (!pz || !erowc) ? c : nv;
+                    }
+                }
                 if constexpr (PRO != 0) {
                     // the corrected iterate: plane z+1 (VL) and the halo row at plane z (HL); with z0
                     // even, ph 0 has z even (z+1 odd: coarse K, K+1) and ph 1 has z odd
@@ -1865,6 +1933,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                 Vp[j] = Vc[j];
                 Vc[j] = VL[cs][j];
             }
+            if constexpr (XH) {
+                EP = EC;
+                EC = EA[cs];
+                ES1c = ES1n;
+            }
             if (PRO && ph == 1) { // next step: coarse planes K+1, K+2
                 if constexpr (RECOMP) {
                     wsl ^= 1;
@@ -1901,19 +1974,40 @@ constexpr int TBY_RY = 2, TBY_RY_NEWTON = 2, TBY_WX = 4, TB_RY_B = 2, TB_WX_B = 
 // waves per SIMD; 0.662 vs 0.673 ms per 512^3 pair, profiles/r01m_summary.md), the other modes and
 // the fused prolongation one (VGPR budget: the LINEAR prolongation pair at distance 2 spills)
 constexpr int tby_pfd(int mode) { return mode == GS_LINEAR ? 2 : 1; }
+// column blocks (XH): LINEAR at distance 2 too (247 VGPRs, no spill); GS_TBX_PFD=1 selects distance 1 (A/B)
+bool tbx_pfd2()
+{
+    static const bool two = !getenv("GS_TBX_PFD") || std::atoi(getenv("GS_TBX_PFD")) != 1;
+    return two;
+}
 
 // Geometry rule of the fused pair: the whole x-row in one block and enough work for >= 512 blocks of
 // 4-plane chunks; the z-chunk is then chosen for >= 1024 blocks (4..64 planes: at 512^3, 64-plane
 // chunks measured 5-8% faster than 32 — fewer re-read chunk-boundary planes).
 // Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU); *y2: the k_tb2y shape.
-int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
-             int mode = GS_LINEAR)
+// Column blocks (k_tb2y XH) for rows of more than 512 points in LINEAR / NONLINEAR mode: 1024-point rows
+// (BASELINE config #5) were k_tb2's one-y-wave shape before; GS_PAIR_XH=0 restores that (A/B).
+bool xh_enabled()
 {
-    if (!S || !L || !canonical_order(S) || L->nx < 1 || L->nx > 2 * WAVE * TB_WX_B || L->ny < 1 || L->nz < 1)
-        return 0;
+    static const bool on = !getenv("GS_PAIR_XH") || std::atoi(getenv("GS_PAIR_XH")) != 0;
+    return on;
+}
+
+// Geometry rule of the fused pair: the whole x-row in one block (or, XH, one column block of 512
+// points) and enough work for >= 512 blocks of 4-plane chunks; the z-chunk is then chosen for >= 1024
+// blocks (4..64 planes: at 512^3, 64-plane chunks measured 5-8% faster than 32 — fewer re-read
+// chunk-boundary planes). Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU);
+// *y2: the k_tb2y whole-row shape, *xh: the k_tb2y column-block shape (neither: k_tb2).
+int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
+             int mode = GS_LINEAR, bool* xh = nullptr)
+{
+    if (!S || !L || !canonical_order(S) || L->nx < 1 || L->ny < 1 || L->nz < 1) return 0;
     const bool two = L->nx <= 2 * WAVE * TBY_WX;
-    const int rows = two ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block
-    const int64_t tiles = (L->ny + rows - 1) / rows;
+    const bool colb = !two && mode != GS_NEWTON && xh_enabled() && L->nx <= (int64_t)1 << 20;
+    if (!two && !colb && L->nx > 2 * WAVE * TB_WX_B) return 0;
+    const int64_t nh = colb ? (L->nx + 2 * WAVE * TBY_WX - 1) / (2 * WAVE * TBY_WX) : 1;
+    const int rows = (two || colb) ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block
+    const int64_t tiles = (L->ny + rows - 1) / rows * nh;
     const int fills = tiles * ((L->nz + 3) / 4) >= 512 ? 2 : 1;
     int64_t c = tiles * L->nz / 1024;
     c = c < 4 ? 4 : (c > 64 ? 64 : c);
@@ -1929,8 +2023,9 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
     c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)
     *zc = (int)c;
     *grid = dim3((unsigned)tiles, (unsigned)((L->nz + c - 1) / c));
-    *block = dim3(WAVE, (unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), two ? 2 : 1);
+    *block = dim3(WAVE, colb ? (unsigned)TBY_WX : (unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), (two || colb) ? 2 : 1);
     if (y2) *y2 = two;
+    if (xh) *xh = colb;
     return fills;
 }
 
@@ -2127,11 +2222,22 @@ int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, doubl
     return launch_pass<0, false>(S, L, mode, omega, gamma, v_in, f, w, v_out, partials, st);
 }
 
-int gs_jacobi_sweep2_supported(const gs_stencil* S, const gs_level* L)
+int gs_jacobi_sweep2_supported_mode(const gs_stencil* S, const gs_level* L, int mode)
 {
     int zc;
     dim3 g, b;
-    return (!bad_level(L) && valid_stencil(S)) ? tb2_plan(S, L, &zc, &g, &b) : 0;
+    if (mode < GS_LINEAR || mode > GS_NEWTON) return 0;
+    return (!bad_level(L) && valid_stencil(S)) ? tb2_plan(S, L, &zc, &g, &b, nullptr, mode) : 0;
+}
+
+int gs_jacobi_sweep2_supported(const gs_stencil* S, const gs_level* L)
+{
+    int r = 2;
+    for (int m = GS_LINEAR; m <= GS_NEWTON; m++) {
+        const int q = gs_jacobi_sweep2_supported_mode(S, L, m);
+        r = q < r ? q : r;
+    }
+    return r;
 }
 
 int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
@@ -2145,9 +2251,10 @@ const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int 
 {
     int zc;
     dim3 g, b;
-    bool y2 = false;
-    if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode)) return "";
+    bool y2 = false, xh = false;
+    if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh)) return "";
     if (y2) return "k_tb2y: 4x2 waves, 2 rows per wave, LDS halo-row exchange, per-wave-row code";
+    if (xh) return "k_tb2y XH: 512-point column blocks of 4x2 waves, edge columns computed lane-parallel";
     return "k_tb2: <= 8 x-waves, 2 rows per wave";
 }
 
@@ -2165,16 +2272,24 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
 {
     int zc;
     dim3 g, b;
-    bool y2 = false;
+    bool y2 = false, xh = false;
     if (!S || bad_level(L) || !valid_stencil(S) || !v_out || !f || v_in == v_out || (!v_in && mode == GS_NONLINEAR) ||
-        (mode == GS_NEWTON && !w) || mode < GS_LINEAR || mode > GS_NEWTON || !tb2_plan(S, L, &zc, &g, &b, &y2, mode))
+        (mode == GS_NEWTON && !w) || mode < GS_LINEAR || mode > GS_NEWTON ||
+        !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh))
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
 #define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
 #define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M)>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TBX(M, Z, P) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
     const bool zv = !v_in;
-    if (y2) {
+    if (xh) {
+        if (mode == GS_LINEAR) {
+            if (zv) GS_TBX(GS_LINEAR, true, 1);
+            else if (tbx_pfd2()) GS_TBX(GS_LINEAR, false, 2);
+            else GS_TBX(GS_LINEAR, false, 1);
+        } else GS_TBX(GS_NONLINEAR, false, 1);
+    } else if (y2) {
         if (mode == GS_LINEAR) {
             if (zv) GS_TBY(GS_LINEAR, true);
             else GS_TBY(GS_LINEAR, false);
@@ -2189,6 +2304,7 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
         else if (zv) GS_TB(GS_NEWTON, true);
         else GS_TB(GS_NEWTON, false);
     }
+#undef GS_TBX
 #undef GS_TBY
 #undef GS_TB
     return launch_status();

@@ -47,6 +47,7 @@ KERNEL_API = {
     "gs_jacobi_sweep_norm": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double, C.c_double,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_jacobi_sweep2_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),
+    "gs_jacobi_sweep2_supported_mode": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int]),
     "gs_jacobi_sweep2": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double, C.c_double,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "gs_jacobi_sweep2_norm": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double,

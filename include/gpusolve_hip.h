@@ -89,12 +89,15 @@ int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, doubl
 
 /* Two fused sweeps, v_out = S(S(v_in)), reading v_in / f once (temporal blocking; bit-identical to
  * two gs_jacobi_sweep calls; v_in = NULL: the zero iterate, as for gs_jacobi_sweep). gs_jacobi_sweep2_supported(S, L): 0 impossible (stencil not in
- * canonical order, nx > 1024), 1 possible, 2 possible and large enough to fill the GPU (the driver
- * uses it only then). zlo / zhi: the plane below local plane 1
+ * canonical order, or, in some mode, nx > 1024), 1 possible, 2 possible and large enough to fill the GPU
+ * (the driver uses it only then). zlo / zhi: the plane below local plane 1
  * (resp. above plane nz) is an internal Z-slab boundary whose two ghost planes (0 and -1, resp.
  * nz+1 and nz+2) of v_in are current; 0 = a level boundary. The x-boundary columns (x = 0 and
  * nx+1) of v_in must be zero, as the reference's are (homogeneous Dirichlet, never written). */
 int gs_jacobi_sweep2_supported(const gs_stencil* S, const gs_level* L);
+/* The same for one mode (rows of more than 512 points: column blocks in LINEAR / NONLINEAR mode, any
+ * row length; NEWTON up to 1024 points). gs_jacobi_sweep2_supported is the minimum over the modes. */
+int gs_jacobi_sweep2_supported_mode(const gs_stencil* S, const gs_level* L, int mode);
 int gs_jacobi_sweep2(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                      const double* v_in, double* v_out, const double* f, const double* w, int zlo, int zhi,
                      hipStream_t stream);

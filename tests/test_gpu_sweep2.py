@@ -55,12 +55,16 @@ def two_sweeps(v0, f0, w0, mode, h):
 
 
 SHAPES = [(1, 1, 1), (2, 5, 3), (5, 4, 33), (127, 9, 17), (128, 8, 8), (129, 13, 40), (257, 6, 10), (500, 7, 9),
-          (512, 4, 5), (513, 5, 6), (1024, 3, 4), (64, 64, 64), (200, 33, 70)]
+          (512, 4, 5), (513, 5, 6), (1024, 3, 4), (64, 64, 64), (200, 33, 70),
+          # rows > 512 points: column blocks (k_tb2y XH) in LINEAR / NONLINEAR mode, k_tb2 in NEWTON mode
+          (700, 9, 11), (1024, 16, 12), (1025, 7, 9), (1536, 5, 6), (2000, 3, 5)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_sweep2_equals_two_sweeps(shape, mode):
+    if shape[0] > 1024 and mode == 2:
+        pytest.skip("NEWTON pairs stop at 1024-point rows")
     rng = np.random.default_rng(abs(hash((shape, mode))) % 2**32)
     nx, ny, nz = shape
     h = 1.0 / (ny + 1)
@@ -69,16 +73,19 @@ def test_sweep2_equals_two_sweeps(shape, mode):
     v, f, w, out = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
                     DevField(nx, ny, nz).from_xyz(w0), DevField(nx, ny, nz))
     L = v.level(h)
-    assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(L)) >= 1
+    assert k().gs_jacobi_sweep2_supported_mode(C.byref(stencil()), C.byref(L), mode) >= 1
     ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, out.ptr, f.ptr, w.ptr, 0, 0, st()))
     np.testing.assert_array_equal(out.to_xyz(), ref)
 
 
+@pytest.mark.parametrize("nx", [130, 1100])
 @pytest.mark.parametrize("lo,hi", [(1, 9), (5, 14), (12, 22), (3, 3), (10, 11)])
 @pytest.mark.parametrize("mode", [0, 2])
-def test_sweep2_on_slab_with_two_ghost_planes(lo, hi, mode):
+def test_sweep2_on_slab_with_two_ghost_planes(lo, hi, mode, nx):
+    if nx > 1024 and mode == 2:
+        pytest.skip("NEWTON pairs stop at 1024-point rows")
     rng = np.random.default_rng(lo * 100 + hi)
-    nx, ny, NZ = 130, 11, 22
+    ny, NZ = 11, 22
     h = 1.0 / (ny + 1)
     v0, f0, w0 = rand_full(rng, nx, ny, NZ), rand_full(rng, nx, ny, NZ, 100.0), rand_full(rng, nx, ny, NZ)
     ref = two_sweeps(v0, f0, w0, mode, h)
@@ -105,18 +112,24 @@ def test_sweep2_on_slab_with_two_ghost_planes(lo, hi, mode):
 def test_sweep2_rejects_unsupported():
     v = DevField(1030, 3, 4)
     L = v.level(0.25)
+    # rows > 1024 points: column blocks in LINEAR / NONLINEAR mode, nothing in NEWTON mode
     assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(L)) == 0
-    rc = k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, DevField(1030, 3, 4).ptr, v.ptr,
-                              None, 0, 0, st())
+    assert k().gs_jacobi_sweep2_supported_mode(C.byref(stencil()), C.byref(L), 0) >= 1
+    assert k().gs_jacobi_sweep2_supported_mode(C.byref(stencil()), C.byref(L), 2) == 0
+    rc = k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 2, 0.8, 1.0, v.ptr, DevField(1030, 3, 4).ptr, v.ptr,
+                              v.ptr, 0, 0, st())
     assert rc == gsv._abi.GS_EINVAL
     big = DevField(512, 512, 64)
     assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(big.level(1 / 513))) == 2
 
 
-@pytest.mark.parametrize("shape", [(5, 4, 33), (129, 13, 40), (512, 4, 5), (300, 9, 7), (1024, 3, 4), (64, 64, 64)])
+@pytest.mark.parametrize("shape", [(5, 4, 33), (129, 13, 40), (512, 4, 5), (300, 9, 7), (1024, 3, 4), (64, 64, 64),
+                                   (1100, 9, 8)])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_sweep2_norm_partials(shape, mode):
     """gs_jacobi_sweep2_norm: same output as the plain pair, and its partials sum to ||f - A v_in||^2."""
+    if shape[0] > 1024 and mode == 2:
+        pytest.skip("NEWTON pairs stop at 1024-point rows")
     rng = np.random.default_rng(sum(shape) * 7 + mode)
     nx, ny, nz = shape
     h = 1.0 / (ny + 1)
@@ -140,7 +153,7 @@ def test_sweep2_norm_partials(shape, mode):
     assert abs(got - want) <= 1e-12 * abs(want)
 
 
-@pytest.mark.parametrize("shape", [(5, 4, 33), (129, 13, 40), (512, 6, 5), (64, 64, 64)])
+@pytest.mark.parametrize("shape", [(5, 4, 33), (129, 13, 40), (512, 6, 5), (64, 64, 64), (1024, 6, 5)])
 @pytest.mark.parametrize("mode", [0, 2])
 def test_zero_iterate_sweeps(shape, mode):
     """v_in = NULL (the coarse levels' v = 0 after restriction) is bit-identical to a zeroed v_in,
@@ -163,7 +176,7 @@ def test_zero_iterate_sweeps(shape, mode):
                                 pb.data_ptr(), st()))
     np.testing.assert_array_equal(a.to_xyz(), b.to_xyz())
     assert torch.equal(pa, pb)
-    if k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(L)) >= 1:
+    if k().gs_jacobi_sweep2_supported_mode(C.byref(stencil()), C.byref(L), mode) >= 1:
         a.from_xyz(np.zeros((nx + 2, ny + 2, nz + 2)))
         b.from_xyz(np.zeros((nx + 2, ny + 2, nz + 2)))
         ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, zero.ptr, a.ptr, f.ptr, w.ptr, 0, 0,
@@ -273,3 +286,18 @@ def test_prolong_fused_pair_rejects():
     assert rc == gsv._abi.GS_EINVAL  # NEWTON needs newtonV
     L2 = DevField(600, 4, 4).level(0.2)
     assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 0) == 0  # rows > 512
+
+
+def test_sweep2_full_1024_plane():
+    """A full 1024 x 1024 plane set (the per-rank slab shape of BASELINE config #5, 4 planes) through
+    the column-block pair, against two single sweeps, bit for bit."""
+    rng = np.random.default_rng(1024)
+    shape = (1024, 1024, 4)
+    h = 1.0 / 1025
+    v0, f0 = rand_full(rng, *shape), rand_full(rng, *shape, 100.0)
+    ref = two_sweeps(v0, f0, np.zeros_like(v0), 0, h)
+    v, f, out = DevField(*shape).from_xyz(v0), DevField(*shape).from_xyz(f0), DevField(*shape)
+    L = v.level(h)
+    assert b"XH" in k().gs_jacobi_sweep2_kernel(C.byref(stencil()), C.byref(L), 0)
+    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, out.ptr, f.ptr, None, 0, 0, st()))
+    np.testing.assert_array_equal(out.to_xyz(), ref)
