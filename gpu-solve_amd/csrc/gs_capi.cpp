@@ -374,6 +374,30 @@ int gs_zslab_plan(const int64_t dims[3], int nranks, int64_t min_points, int max
     return (int)ld.size();
 }
 
+int gs_zslab_schedule(const gs_params* p, int nranks, int rank, int64_t min_points, char* buf, int64_t cap,
+                      int64_t* len)
+{
+    return guarded([&] {
+        if (!p || nranks < 1 || rank < 0 || rank >= nranks) throw gs::Error("gs_zslab_schedule: bad arguments");
+        std::vector<std::string> ops;
+        {
+            auto comm = gs::makeTraceComm(rank, nranks);
+            gs::HipGridData g(toParams(p), comm.get(), min_points, &ops);
+            g.printProgress = false;
+            if (g.mode == gs::GridParams::NEWTON) gs::NewtonSolver::solve(g);
+            else gs::HipSolver::solve(g);
+        }
+        std::string text;
+        for (const auto& o : ops) text += o + "\n";
+        if (len) *len = (int64_t)text.size();
+        if (buf && cap > 0) {
+            const std::size_t n = std::min<std::size_t>(text.size(), (std::size_t)cap - 1);
+            std::memcpy(buf, text.data(), n);
+            buf[n] = 0;
+        }
+    });
+}
+
 int gs_rccl_unique_id(unsigned char uid[128])
 {
     return guarded([&] { gs::rcclUniqueId(uid); });

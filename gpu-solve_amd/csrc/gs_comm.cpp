@@ -346,6 +346,25 @@ private:
     int r_;
 };
 
+class TraceComm final : public Comm {
+public:
+    TraceComm(int rank, int n) : r_(rank), n_(n) {}
+    int rank() const override { return r_; }
+    int size() const override { return n_; }
+    void halo(double*, int64_t, int64_t, int, hipStream_t) override { throw Error("trace communicator: no transport"); }
+    void allgather1(const double*, double*, hipStream_t) override { throw Error("trace communicator: no transport"); }
+    void gatherPlanes(double*, int64_t, const std::vector<int64_t>&, const std::vector<int64_t>&, hipStream_t) override
+    {
+        throw Error("trace communicator: no transport");
+    }
+    void sync(hipStream_t) override {}
+
+private:
+    int r_, n_;
+};
+
+std::unique_ptr<Comm> makeTraceComm(int rank, int nranks) { return std::make_unique<TraceComm>(rank, nranks); }
+
 std::unique_ptr<Comm> makeLoopbackComm(const std::shared_ptr<LoopbackHub>& hub, int rank)
 {
     return std::make_unique<LoopbackComm>(hub, rank);

@@ -59,6 +59,10 @@ std::string boundedWait(const std::function<int()>& poll, const std::function<st
                         double timeoutS, const char* what);
 double commTimeoutS(const char* env, double dflt);
 
+// Rank `rank` of `nranks` without any transport: the communicator of HipGridData's schedule-trace
+// mode, which records exchanges instead of running them.
+std::unique_ptr<Comm> makeTraceComm(int rank, int nranks);
+
 // Loopback: nranks threads of one process on one device share a hub.
 class LoopbackHub;
 std::shared_ptr<LoopbackHub> makeLoopbackHub(int nranks);

@@ -22,10 +22,12 @@ void check(int code, const char* what)
 }
 
 // ---------------------------------------------------------------------------------------------
-DeviceField::DeviceField(int64_t nx, int64_t ny, int64_t nz, hipStream_t s)
+DeviceField::DeviceField(int64_t nx, int64_t ny, int64_t nz, hipStream_t s, bool dry) : dry_(dry)
 {
     int64_t origin = 0;
     check(gs_field_layout(nx, ny, nz, &ldy_, &ldz_, &alloc_, &origin), "gs_field_layout");
+    span_ = ldz_ * (nz + 2);
+    if (dry) return;
     void* p = nullptr;
     check((int)hipMalloc(&p, sizeof(double) * alloc_), "hipMalloc");
     base_ = static_cast<double*>(p);
@@ -49,6 +51,7 @@ DeviceField& DeviceField::operator=(DeviceField&& o) noexcept
         ldz_ = o.ldz_;
         span_ = o.span_;
         alloc_ = o.alloc_;
+        dry_ = o.dry_;
     }
     return *this;
 }
@@ -66,9 +69,13 @@ void DeviceField::swap(DeviceField& o) noexcept
     std::swap(ldz_, o.ldz_);
     std::swap(span_, o.span_);
     std::swap(alloc_, o.alloc_);
+    std::swap(dry_, o.dry_);
 }
 
-StreamGuard::StreamGuard() { check((int)hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate"); }
+StreamGuard::StreamGuard(bool create)
+{
+    if (create) check((int)hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+}
 StreamGuard::~StreamGuard()
 {
     if (s) (void)hipStreamDestroy(s);
@@ -116,9 +123,11 @@ LevelClock::~LevelClock()
 // ---------------------------------------------------------------------------------------------
 // Level hierarchy: L = floor(log2(min dim)) + 1, dims halve per level, h_l = 1/(ny_l+1)
 // (src/cpu/CpuGridData.cpp:19-41). Fields a mode never touches are not allocated.
-HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomeratePoints)
-    : GridParams(grid), comm_(comm)
+HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomeratePoints,
+                         std::vector<std::string>* traceLog)
+    : GridParams(grid), trace(traceLog), comm_(comm), stream_(traceLog == nullptr), commStream_(traceLog == nullptr)
 {
+    const bool dry = traceLog != nullptr;
     const std::size_t mn = std::min(std::min(gridDim[0], gridDim[1]), gridDim[2]);
     if (mn == 0) throw Error("grid dimensions must be positive");
     const int nlev = (int)std::floor(std::log((double)mn) / std::log(2.0)) + 1;
@@ -161,12 +170,12 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         }
         const int64_t nz = L.hi - L.lo + 1;
         L.h = 1.0 / (L.levelDim[1] + 1);
-        L.v = DeviceField(nx, ny, nz, s);
-        L.vAlt = DeviceField(nx, ny, nz, s);
-        L.f = DeviceField(nx, ny, nz, s);
-        if (l + 1 < nlev) L.r = DeviceField(nx, ny, nz, s); // restriction source
-        if (mode == NONLINEAR && l > 0) L.restV = DeviceField(nx, ny, nz, s);
-        if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s);
+        L.v = DeviceField(nx, ny, nz, s, dry);
+        L.vAlt = DeviceField(nx, ny, nz, s, dry);
+        L.f = DeviceField(nx, ny, nz, s, dry);
+        if (l + 1 < nlev) L.r = DeviceField(nx, ny, nz, s, dry); // restriction source
+        if (mode == NONLINEAR && l > 0) L.restV = DeviceField(nx, ny, nz, s, dry);
+        if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s, dry);
         L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), L.lo - 1, L.h};
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
         maxParts = std::max(maxParts, gs_jacobi_sweep2_num_partials(&stencilAbi, &L.geom, (int)mode));
@@ -195,11 +204,18 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
                 coarseFrom = (std::size_t)l;
             }
     }
-    if (mode == NEWTON) newtonF = DeviceField(levels_[0].geom.nx, levels_[0].geom.ny, levels_[0].geom.nz, s);
+    if (mode == NEWTON) newtonF = DeviceField(levels_[0].geom.nx, levels_[0].geom.ny, levels_[0].geom.nz, s, dry);
     {
         const char* e = std::getenv("GS_METRICS");
-        clock.on = e && *e && *e != '0';
+        clock.on = !dry && e && *e && *e != '0';
         clock.levelMs.assign(nlev, 0.0);
+    }
+    if (dry) {
+        dryParts_.assign(16, 0.0); // the partial-sum pointers the solvers pass mark normed launches
+        partials_ = dryParts_.data();
+        rec("rhs", {{"L", 0}}, "f");
+        halo(levels_[0], levels_[0].f, s);
+        return;
     }
     // the overlapped sweep splits a level into 3 launches, each with its own partials region
     maxParts = 2 * maxParts + 4096;
@@ -221,7 +237,7 @@ HipGridData::~HipGridData()
 {
     if (stream_.s) (void)hipStreamSynchronize(stream_.s);
     if (commStream_.s) (void)hipStreamSynchronize(commStream_.s);
-    if (partials_) (void)hipFree(partials_);
+    if (partials_ && !trace) (void)hipFree(partials_);
     if (dNorm_) (void)hipFree(dNorm_);
     if (dRankSums_) (void)hipFree(dRankSums_);
     if (hNorm_) (void)hipHostFree(hNorm_);
@@ -229,8 +245,28 @@ HipGridData::~HipGridData()
     if (evB_) (void)hipEventDestroy(evB_);
 }
 
+void HipGridData::rec(const char* op, std::initializer_list<std::pair<const char*, long long>> kv, const char* field)
+{
+    std::string line = op;
+    if (field) line += std::string(" field=") + field;
+    for (const auto& p : kv) line += " " + std::string(p.first) + "=" + std::to_string(p.second);
+    trace->push_back(line);
+}
+
+const char* HipGridData::fieldName(const LevelData& L, const DeviceField& f)
+{
+    if (&f == &L.v) return "v";
+    if (&f == &L.vAlt) return "vAlt";
+    if (&f == &L.f) return "f";
+    if (&f == &L.r) return "r";
+    if (&f == &L.restV) return "restV";
+    if (&f == &L.newtonV) return "newtonV";
+    return "?";
+}
+
 double HipGridData::readNorm()
 {
+    if (trace) return 1.0; // (no device: the traced norms are placeholders)
     check((int)hipMemcpyAsync(hNorm_, dNorm_, sizeof(double), hipMemcpyDeviceToHost, stream_.s), "hipMemcpyAsync");
     sync();
     return *hNorm_;
@@ -238,6 +274,7 @@ double HipGridData::readNorm()
 
 void HipGridData::sync()
 {
+    if (trace) return;
     // distributed: a bounded wait that also polls the communicator's error state (gs_comm.hpp)
     if (comm_ && comm_->size() > 1) comm_->sync(stream_.s);
     else check((int)hipStreamSynchronize(stream_.s), "hipStreamSynchronize");
@@ -245,12 +282,15 @@ void HipGridData::sync()
 
 void HipGridData::halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth)
 {
-    if (L.distributed && nranks() > 1) comm_->halo(fld.data(), fld.ldz(), L.geom.nz, depth, s);
+    if (!(L.distributed && nranks() > 1)) return;
+    if (trace) rec("halo", {{"L", (long long)levelIndex(L)}, {"depth", depth}}, fieldName(L, fld));
+    else comm_->halo(fld.data(), fld.ldz(), L.geom.nz, depth, s);
 }
 
 void HipGridData::gather(LevelData& L, DeviceField& fld)
 {
-    comm_->gatherPlanes(fld.data(), fld.ldz(), L.ranksLo, L.ranksHi, stream_.s);
+    if (trace) rec("gather", {{"L", (long long)levelIndex(L)}}, fieldName(L, fld));
+    else comm_->gatherPlanes(fld.data(), fld.ldz(), L.ranksLo, L.ranksHi, stream_.s);
 }
 
 gs_level HipGridData::ownedGeom(const LevelData& L, int64_t* off) const
@@ -284,6 +324,10 @@ int64_t sweepPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64
     sub.nz = z2 - z1 + 1;
     sub.z0 += z1 - 1;
     const int64_t off = (z1 - 1) * L.geom.ldz;
+    if (g.trace) {
+        g.rec("sweep", {{"L", (long long)g.levelIndex(L)}, {"z1", z1}, {"z2", z2}, {"vzero", L.vZero}, {"norm", partials != nullptr}});
+        return partials ? 1 : 0;
+    }
     check(gs_jacobi_sweep_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.vZero ? nullptr : L.v.data() + off,
                                L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
                                partials, s),
@@ -305,6 +349,11 @@ int64_t pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_
     const bool dist = L.distributed && g.nranks() > 1;
     const int zlo = z1 > 1 || (dist && g.rank() > 0);
     const int zhi = z2 < L.geom.nz || (dist && g.rank() + 1 < g.nranks());
+    if (g.trace) {
+        g.rec("pair", {{"L", (long long)g.levelIndex(L)}, {"z1", z1}, {"z2", z2}, {"zlo", zlo}, {"zhi", zhi},
+                       {"vzero", L.vZero}, {"norm", partials != nullptr}});
+        return partials ? 1 : 0;
+    }
     check(gs_jacobi_sweep2_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.vZero ? nullptr : L.v.data() + off,
                                 L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
                                 zlo, zhi, partials, s),
@@ -327,6 +376,10 @@ void proPlanes(HipGridData& g, HipGridData::LevelData& F, HipGridData::LevelData
     const bool dist = F.distributed && g.nranks() > 1;
     const int zlo = z1 > 1 || (dist && g.rank() > 0);
     const int zhi = z2 < F.geom.nz || (dist && g.rank() + 1 < g.nranks());
+    if (g.trace) {
+        g.rec("pro", {{"L", (long long)g.levelIndex(F)}, {"z1", z1}, {"z2", z2}, {"zlo", zlo}, {"zhi", zhi}});
+        return;
+    }
     check(gs_jacobi_sweep2_prolong(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, F.v.data() + off, C.v.data(),
                                    nullptr, &C.geom, F.vAlt.data() + off, F.f.data() + off,
                                    F.newtonV ? F.newtonV.data() + off : nullptr, zlo, zhi, s),
@@ -347,7 +400,12 @@ void restrictTo(HipGridData& g, const DeviceField& src, std::size_t l, DeviceFie
     const hipStream_t s = g.stream();
     int64_t off = 0;
     const gs_level cg = g.ownedGeom(C, &off);
-    if (cg.nz > 0)
+    if (g.trace) {
+        if (cg.nz > 0)
+            g.rec("restrict", {{"L", (long long)l}, {"c1", cg.z0 + 1}, {"c2", cg.z0 + cg.nz}, {"two", b != nullptr}},
+                  (std::string(HipGridData::fieldName(F, src)) + ">" + HipGridData::fieldName(C, a) +
+                   (b ? std::string(",") + HipGridData::fieldName(C, *b) : std::string())).c_str());
+    } else if (cg.nz > 0)
         check(gs_restrict2(src.data(), &F.geom, a.data() + off, b ? b->data() + off : nullptr, &cg, s), "gs_restrict");
     if (transitionLevel(g, l + 1)) {
         g.gather(C, a);
@@ -359,6 +417,23 @@ void restrictTo(HipGridData& g, const DeviceField& src, std::size_t l, DeviceFie
 }
 
 } // namespace
+
+// The overlapped exchange: the comm stream waits for the boundary planes (fork), the compute stream
+// for the exchange before the next sweep (join; recorded after the exchange, waited on after the
+// interior launch). Nothing to order in trace mode.
+void HipSolver::forkComm(HipGridData& grid)
+{
+    if (grid.trace) return;
+    check((int)hipEventRecord(grid.evA_, grid.stream()), "hipEventRecord");
+    check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
+}
+
+void HipSolver::joinComm(HipGridData& grid, bool wait)
+{
+    if (grid.trace) return;
+    if (!wait) check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+    else check((int)hipStreamWaitEvent(grid.stream(), grid.evB_, 0), "hipStreamWaitEvent");
+}
 
 bool HipSolver::speculationEnabled(const HipGridData& grid)
 {
@@ -396,6 +471,10 @@ void HipSolver::solve(HipGridData& grid)
 double HipSolver::finishNorm(HipGridData& grid, int64_t nparts)
 {
     const hipStream_t s = grid.stream();
+    if (grid.trace) {
+        grid.rec("norm", {{"allgather", grid.nranks() > 1 && grid.getLevel(0).distributed}});
+        return grid.readNorm();
+    }
     if (grid.nranks() > 1 && grid.getLevel(0).distributed) {
         check(gs_sumsq_finish(grid.partials(), nparts, grid.dNorm(), 1, s), "gs_sumsq_finish");
         grid.comm()->allgather1(grid.dNorm(), grid.dRankSums(), s);
@@ -413,10 +492,13 @@ double HipSolver::compResidual(HipGridData& grid, std::size_t l, bool storeR, bo
     materialize(grid, l);
     auto& L = grid.getLevel(l);
     const hipStream_t s = grid.stream();
-    check(gs_residual(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(), L.f.data(),
-                      L.newtonV ? L.newtonV.data() : nullptr, storeR ? L.r.data() : nullptr,
-                      norm ? grid.partials() : nullptr, s),
-          "gs_residual");
+    if (grid.trace)
+        grid.rec("residual", {{"L", (long long)l}, {"store", storeR}, {"norm", norm}});
+    else
+        check(gs_residual(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(), L.f.data(),
+                          L.newtonV ? L.newtonV.data() : nullptr, storeR ? L.r.data() : nullptr,
+                          norm ? grid.partials() : nullptr, s),
+              "gs_residual");
     if (storeR) grid.halo(L, L.r, s);
     if (!norm) return 0.0;
     return finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L.geom));
@@ -477,17 +559,17 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
         } else if (grid.overlapHalo && nz >= 2 * b + 1) {
             run(1, b);
             run(nz - b + 1, nz);
-            check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
-            check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
-            grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, grid.commStream());
-            check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+            forkComm(grid);
+            grid.halo(L, L.vAlt, grid.commStream(), depth);
+            joinComm(grid, false);
             run(b + 1, nz - b);
-            check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
+            joinComm(grid, true);
         } else {
             run(1, nz);
-            grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, s);
+            grid.halo(L, L.vAlt, s, depth);
         }
         L.v.swap(L.vAlt);
+        if (grid.trace) grid.rec("swap", {{"L", (long long)l}});
         L.vZero = false;
         sweeps -= pair ? 2 : 1;
     }
@@ -498,6 +580,7 @@ void HipSolver::materialize(HipGridData& grid, std::size_t l)
 {
     auto& L = grid.getLevel(l);
     if (!L.vZero) return;
+    if (grid.trace) grid.rec("zero", {{"L", (long long)l}}, "v");
     L.v.zero(grid.stream());
     L.vZero = false;
 }
@@ -516,13 +599,19 @@ void HipSolver::coarseCycle(HipGridData& grid, std::size_t from)
                                 L.restV ? L.restV.data() : nullptr, L.newtonV ? L.newtonV.data() : nullptr,
                                 L.geom, j == 0 ? (L.vZero ? 1 : 0) : (grid.mode != GridParams::NONLINEAR ? 1 : 0)};
     }
-    check(gs_coarse_cycle(&grid.stencilAbi, lv, n, (int)grid.mode, grid.omega, grid.gamma, (int)grid.preSmoothing,
-                          (int)grid.postSmoothing, grid.stream()),
-          "gs_coarse_cycle");
+    if (grid.trace)
+        grid.rec("coarse", {{"from", (long long)from}, {"vzero", lv[0].v_zero}});
+    else
+        check(gs_coarse_cycle(&grid.stencilAbi, lv, n, (int)grid.mode, grid.omega, grid.gamma, (int)grid.preSmoothing,
+                              (int)grid.postSmoothing, grid.stream()),
+              "gs_coarse_cycle");
     const bool odd = ((grid.preSmoothing + grid.postSmoothing) & 1) != 0; // every level swept pre+post times
     for (int j = 0; j < n; j++) {
         auto& L = grid.getLevel(from + j);
-        if (odd) L.v.swap(L.vAlt);
+        if (odd) {
+            L.v.swap(L.vAlt);
+            if (grid.trace) grid.rec("swap", {{"L", (long long)(from + j)}});
+        }
         L.vZero = false;
     }
 }
@@ -548,15 +637,14 @@ double HipSolver::speculativeSweep(HipGridData& grid, int* sweeps)
     } else if (grid.overlapHalo && nz >= 2 * b + 1) {
         run(1, b);
         run(nz - b + 1, nz);
-        check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
-        check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
-        grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, grid.commStream());
-        check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+        forkComm(grid);
+        grid.halo(L, L.vAlt, grid.commStream(), depth);
+        joinComm(grid, false);
         run(b + 1, nz - b);
-        check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
+        joinComm(grid, true);
     } else {
         run(1, nz);
-        grid.comm()->halo(L.vAlt.data(), L.vAlt.ldz(), nz, depth, s);
+        grid.halo(L, L.vAlt, s, depth);
     }
     if (sweeps) *sweeps = pair ? 2 : 1;
     grid.clock.mark(s, 0, false); // closes the caller's segment before the norm's host sync
@@ -583,6 +671,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
         std::size_t pre = grid.preSmoothing;
         if (i == 0 && pending && *pending > 0 && pre >= (std::size_t)*pending) {
             grid.getLevel(0).v.swap(grid.getLevel(0).vAlt); // adopt the speculative first sweep(s)
+            if (grid.trace) grid.rec("swap", {{"L", 0}});
             pre -= (std::size_t)*pending;
             *pending = 0;
         }
@@ -596,9 +685,12 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
             materialize(grid, i);
             const double* w = L.newtonV ? L.newtonV.data() : nullptr;
             if (!(L.distributed && grid.nranks() > 1)) {
-                check(gs_residual_restrict(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(),
-                                           L.f.data(), w, C.f.data(), nullptr, &C.geom, s),
-                      "gs_residual_restrict");
+                if (grid.trace)
+                    grid.rec("resrestrict", {{"L", (long long)i}, {"c1", 1}, {"c2", C.geom.nz}, {"zhi", 0}});
+                else
+                    check(gs_residual_restrict(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(),
+                                               L.f.data(), w, C.f.data(), nullptr, &C.geom, s),
+                          "gs_residual_restrict");
                 fused = true;
             } else {
                 // Z-slab: this rank's coarse planes from its fine slab, whose top ghost planes are current
@@ -615,7 +707,9 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
                 slabOk = slabOk && grid.vDepth(L) == 2 &&
                          gs_residual_restrict_slab_supported(&grid.stencilAbi, &L.geom) != 0;
                 if (slabOk) {
-                    if (cg.nz > 0)
+                    if (cg.nz > 0 && grid.trace)
+                        grid.rec("resrestrict", {{"L", (long long)i}, {"c1", cg.z0 + 1}, {"c2", cg.z0 + cg.nz}, {"zhi", zhi}});
+                    else if (cg.nz > 0)
                         check(gs_residual_restrict_slab(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma,
                                                         L.v.data(), L.f.data(), w, C.f.data() + off, nullptr, &cg,
                                                         zhi, s),
@@ -633,13 +727,20 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
         if (grid.mode != GridParams::NONLINEAR) {
             // v^2h = 0 (CpuSolver.cpp:114-116): not stored; the first sweep on the level reads no v
             static const bool noZeroGuess = std::getenv("GS_NO_ZERO_GUESS") != nullptr;
-            if (noZeroGuess) C.v.zero(s);
-            else C.vZero = true;
+            if (noZeroGuess) {
+                if (grid.trace) grid.rec("zero", {{"L", (long long)(i + 1)}}, "v");
+                C.v.zero(s);
+            } else {
+                C.vZero = true;
+            }
         } else {
             // FAS: restV = v^2h = R v^h, then f^2h += A^2h(restV)  (CpuSolver.cpp:104-113)
             restrictTo(grid, L.v, i, C.restV, &C.v, true);
-            check(gs_apply_op_add(&grid.stencilAbi, &C.geom, grid.gamma, C.restV.data(), C.f.data(), s),
-                  "gs_apply_op_add");
+            if (grid.trace)
+                grid.rec("applyadd", {{"L", (long long)(i + 1)}});
+            else
+                check(gs_apply_op_add(&grid.stencilAbi, &C.geom, grid.gamma, C.restV.data(), C.f.data(), s),
+                      "gs_apply_op_add");
             grid.halo(C, C.f, s);
         }
         grid.clock.mark(s, (int)i, false);
@@ -668,26 +769,29 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
                 const int64_t zt = nz % 2 == 0 ? nz - 1 : nz - 2; // odd start: 2 or 3 top planes
                 proPlanes(grid, F, C, 1, 2, s);
                 proPlanes(grid, F, C, zt, nz, s);
-                check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
-                check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
-                grid.comm()->halo(F.vAlt.data(), F.vAlt.ldz(), nz, grid.vDepth(F), grid.commStream());
-                check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+                forkComm(grid);
+                grid.halo(F, F.vAlt, grid.commStream(), grid.vDepth(F));
+                joinComm(grid, false);
                 proPlanes(grid, F, C, 3, zt - 1, s);
-                check((int)hipStreamWaitEvent(s, grid.evB_, 0), "hipStreamWaitEvent");
+                joinComm(grid, true);
             } else {
                 proPlanes(grid, F, C, 1, nz, s);
-                grid.comm()->halo(F.vAlt.data(), F.vAlt.ldz(), nz, grid.vDepth(F), s);
+                grid.halo(F, F.vAlt, s, grid.vDepth(F));
             }
             F.v.swap(F.vAlt);
+            if (grid.trace) grid.rec("swap", {{"L", (long long)(i - 1)}});
             F.vZero = false;
             jacobi(grid, i - 1, grid.postSmoothing - 2);
             grid.clock.mark(s, (int)(i - 1), false);
             continue;
         }
         // v^h += P (v^2h [- restV^2h])   (CpuSolver.cpp:121-132, interpolate + v += e fused)
-        check(gs_prolong_add(C.v.data(), grid.mode == GridParams::NONLINEAR ? C.restV.data() : nullptr, &C.geom,
-                             F.v.data(), &F.geom, s),
-              "gs_prolong_add");
+        if (grid.trace)
+            grid.rec("prolongadd", {{"L", (long long)(i - 1)}, {"sub", grid.mode == GridParams::NONLINEAR}});
+        else
+            check(gs_prolong_add(C.v.data(), grid.mode == GridParams::NONLINEAR ? C.restV.data() : nullptr, &C.geom,
+                                 F.v.data(), &F.geom, s),
+                  "gs_prolong_add");
         grid.halo(F, F.v, s, grid.vDepth(F));
         jacobi(grid, i - 1, grid.postSmoothing);
         grid.clock.mark(s, (int)(i - 1), false);
@@ -718,9 +822,12 @@ void NewtonSolver::solve(HipGridData& grid)
     // the reference prints unconditionally (NewtonSolver.cpp:16,27); printProgress defaults to true,
     // so GpuSolve-hip does too, and library callers silence it without touching std::cout
     const bool print = grid.printProgress && grid.rank() == 0;
-    check((int)hipMemcpyAsync(grid.newtonF.data(), L0.f.data(), sizeof(double) * L0.f.span(), hipMemcpyDeviceToDevice,
-                              s),
-          "hipMemcpyAsync");
+    if (grid.trace)
+        grid.rec("copy", {{"L", 0}}, "f>newtonF");
+    else
+        check((int)hipMemcpyAsync(grid.newtonF.data(), L0.f.data(), sizeof(double) * L0.f.span(),
+                                  hipMemcpyDeviceToDevice, s),
+              "hipMemcpyAsync");
     const double initialResidual = compF(grid);
     if (history) history->push_back(initialResidual);
     if (print) std::cout << "Inital newton residual: " << initialResidual << '\n';
@@ -729,6 +836,7 @@ void NewtonSolver::solve(HipGridData& grid)
         if (print) Timer::start();
         // The reference recomputes compF here (NewtonSolver.cpp:21); f^0 already holds exactly that
         // value from the previous compF and nothing wrote it since, so the pass is skipped.
+        if (grid.trace) grid.rec("zero", {{"L", 0}}, "v");
         L0.v.zero(s);
         findError(grid);
         const double res = compF(grid);
@@ -745,9 +853,12 @@ void NewtonSolver::solve(HipGridData& grid)
 double NewtonSolver::compF(HipGridData& grid)
 {
     auto& L0 = grid.getLevel(0);
-    check(gs_newton_F(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), grid.newtonF.data(), L0.f.data(),
-                      grid.partials(), grid.stream()),
-          "gs_newton_F");
+    if (grid.trace)
+        grid.rec("newtonF", {{"L", 0}});
+    else
+        check(gs_newton_F(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), grid.newtonF.data(),
+                          L0.f.data(), grid.partials(), grid.stream()),
+              "gs_newton_F");
     grid.halo(L0, L0.f, grid.stream());
     return HipSolver::finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L0.geom));
 }
@@ -774,7 +885,8 @@ void NewtonSolver::findError(HipGridData& grid)
 
     auto& L0 = grid.getLevel(0);
     // whole local array, ghost planes included: both operands' ghosts are current, so the sum's are
-    check(gs_axpy(L0.newtonV.data(), L0.v.data(), 1.0, L0.v.span(), grid.stream()), "gs_axpy");
+    if (grid.trace) grid.rec("axpy", {{"L", 0}}, "newtonV+=v");
+    else check(gs_axpy(L0.newtonV.data(), L0.v.data(), 1.0, L0.v.span(), grid.stream()), "gs_axpy");
 }
 
 // "[gs] mlups=... gbps=... pct_peak=... vcycle_ms=... cycles=... level_ms=a,b,..." over the V-cycles

@@ -14,6 +14,7 @@
 #include <array>
 #include <cstddef>
 #include <cstdint>
+#include <initializer_list>
 #include <memory>
 #include <string>
 #include <vector>
@@ -30,7 +31,8 @@ void check(int code, const char* what); // throws gs::Error with gs_strerror(cod
 class DeviceField {
 public:
     DeviceField() = default;
-    DeviceField(int64_t nx, int64_t ny, int64_t nz, hipStream_t s); // zero-filled
+    DeviceField(int64_t nx, int64_t ny, int64_t nz, hipStream_t s, bool dry = false); // zero-filled
+    // dry: the layout without device memory (schedule tracing, HipGridData's trace mode)
     ~DeviceField();
     DeviceField(const DeviceField&) = delete;
     DeviceField& operator=(const DeviceField&) = delete;
@@ -41,7 +43,7 @@ public:
     int64_t ldy() const { return ldy_; }
     int64_t ldz() const { return ldz_; }
     int64_t span() const { return span_; } // elements from origin covering every padded point
-    explicit operator bool() const { return base_ != nullptr; }
+    explicit operator bool() const { return base_ != nullptr || dry_; }
     void zero(hipStream_t s);
     void swap(DeviceField& o) noexcept;
 
@@ -49,11 +51,12 @@ private:
     double* base_ = nullptr;
     double* origin_ = nullptr;
     int64_t ldy_ = 0, ldz_ = 0, span_ = 0, alloc_ = 0;
+    bool dry_ = false;
 };
 
 struct StreamGuard {
     hipStream_t s = nullptr;
-    StreamGuard();
+    explicit StreamGuard(bool create = true);
     ~StreamGuard();
 };
 
@@ -93,7 +96,12 @@ public:
     };
 
     // comm == nullptr or comm->size() == 1: the single-GPU path. The grid does not own comm.
-    explicit HipGridData(const GridParams& grid, Comm* comm = nullptr, int64_t agglomeratePoints = -1);
+    // trace != nullptr: schedule-trace mode — no device is touched; every kernel launch, ghost
+    // exchange, gather, norm reduction, swap and zeroing the solvers would issue is appended to *trace
+    // as one "op key=value ..." line instead (gs_zslab_schedule; replayed by tests/test_zslab_cpu.py
+    // with the oracle's arithmetic on gloo ranks).
+    explicit HipGridData(const GridParams& grid, Comm* comm = nullptr, int64_t agglomeratePoints = -1,
+                         std::vector<std::string>* trace = nullptr);
     ~HipGridData();
 
     LevelData& getLevel(std::size_t l) { return levels_[l]; }
@@ -112,6 +120,10 @@ public:
     // (numLevels(): none); set from GS_COARSE_POINTS at construction
     std::size_t coarseFrom = 0;
     LevelClock clock; // per-level timing (GS_METRICS)
+    std::vector<std::string>* trace = nullptr; // schedule-trace mode (see the constructor)
+    void rec(const char* op, std::initializer_list<std::pair<const char*, long long>> kv, const char* field = nullptr);
+    std::size_t levelIndex(const LevelData& L) const { return (std::size_t)(&L - levels_.data()); }
+    static const char* fieldName(const LevelData& L, const DeviceField& f);
 
     // residual-norm plumbing: per-block partials, device scalars, pinned host scalar
     double* partials() const { return partials_; }
@@ -139,6 +151,7 @@ private:
     double* dRankSums_ = nullptr;
     double* hNorm_ = nullptr;
     hipEvent_t evA_ = nullptr, evB_ = nullptr;
+    std::vector<double> dryParts_;
     friend class HipSolver;
 };
 
@@ -163,6 +176,8 @@ public:
     // the V-cycle below level `from` (its f set) in one gs_coarse_cycle launch
     static void coarseCycle(HipGridData& grid, std::size_t from);
     static double finishNorm(HipGridData& grid, int64_t nparts);
+    static void forkComm(HipGridData& grid);
+    static void joinComm(HipGridData& grid, bool wait);
 
     // solve() records its residual history here when non-null (initial, then one per V-cycle)
     static thread_local std::vector<double>* history;

@@ -125,6 +125,7 @@ DRIVER_API = {
     "gs_grid_time_vcycles": (C.c_int, [C.c_void_p, C.c_int, dptr, dptr]),
     "gs_zslab_plan": (C.c_int, [C.POINTER(i64), C.c_int, i64, C.c_int, C.POINTER(C.c_int), C.POINTER(i64),
                                 C.POINTER(i64)]),
+    "gs_zslab_schedule": (C.c_int, [C.POINTER(gs_params), C.c_int, C.c_int, i64, C.c_char_p, i64, C.POINTER(i64)]),
     "gs_rccl_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
     "gs_grid_create_rccl": (C.c_void_p, [C.POINTER(gs_params), C.c_int, C.c_int, C.POINTER(C.c_ubyte)]),
     "gs_zslab_loopback_run": (C.c_int, [C.POINTER(gs_params), C.c_int, i64, C.c_int, C.c_int, dptr, C.c_int,

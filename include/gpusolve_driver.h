@@ -86,6 +86,14 @@ int gs_grid_time_vcycles(void* grid, int cycles, double* ms, double* last_residu
  * level count (at most max_levels entries are written). */
 int gs_zslab_plan(const int64_t dims[3], int nranks, int64_t min_points, int max_levels, int* distributed,
                   int64_t* lo, int64_t* hi);
+/* The Z-slab schedule of rank `rank` of `nranks` for the solve of p (construction, initial norm,
+ * p->maxiter V-cycles / Newton iterations), produced by the driver's own V-cycle code in its trace mode
+ * (no device touched): one line per kernel launch, ghost exchange, gather, norm reduction, swap and
+ * zeroing, "op field=.. key=value ..." (ops: rhs pair sweep pro swap zero halo gather norm residual
+ * resrestrict restrict prolongadd applyadd coarse copy newtonF axpy; L = level, z1..z2 = local planes,
+ * c1..c2 = global coarse planes). Writes at most cap-1 bytes + NUL; *len = the full length. */
+int gs_zslab_schedule(const gs_params* p, int nranks, int rank, int64_t min_points, char* buf, int64_t cap,
+                      int64_t* len);
 /* 128-byte RCCL unique id (rank 0 creates it, every rank passes the same bytes). */
 int gs_rccl_unique_id(unsigned char uid[128]);
 /* Grid whose levels are Z-slab partitioned over an RCCL communicator (one GPU per rank; the

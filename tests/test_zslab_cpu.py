@@ -3,10 +3,10 @@
 1. the ownership plan (gs_zslab_plan, the driver's own host code) covers every plane exactly once
    on every level, honours the "coarse plane zc belongs to the owner of fine plane 2 zc" rule, and
    keeps every stencil / transfer read inside [lo-1, hi+1] (one ghost plane);
-2. a world_size-2 torch.distributed (gloo) run of the slab protocol — sweeps on slabs with one
-   ghost plane, ghost exchange after every write, rank-ordered norm — reproduces the single-domain
-   oracle bit for bit. The per-slab arithmetic is the oracle's; the schedule mirrors
-   HipSolver::jacobi / finishNorm.
+2. the driver's own Z-slab schedule (gs_zslab_schedule: HipSolver in trace mode, every launch, plane
+   range, ghost exchange, gather and norm reduction of gs_grid.cpp) replayed on world_size 2 / 3
+   torch.distributed (gloo) ranks with the oracle's point arithmetic (tests/zslab_exec.py) reproduces
+   the single-domain oracle solve bit for bit.
 """
 import ctypes as C
 import os
@@ -80,75 +80,91 @@ def _free_port():
     return p
 
 
-def _slab_worker(rank, world, port, dims, sweeps, q):
+def _replay_worker(rank, world, port, params, min_points, q, mutation=None):
+    """One gloo rank: replay this rank's schedule from the driver (gs_zslab_schedule) on its slab."""
+    import zslab_exec as X
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    nx, ny, nz = dims
-    _, distributed, own = plan(dims, world)
-    lo, hi = own[0][rank]
-    h = 1.0 / (ny + 1)
-    f_full = O.rhs(nx, ny, nz, O.LINEAR)
-    rng = np.random.default_rng(1)
-    v_full = O.zeros(nx, ny, nz)
-    v_full[1:-1, 1:-1, 1:-1] = rng.uniform(-1, 1, (nx, ny, nz))
-    # slab with one ghost plane each side (reference layout: z is the last axis)
-    v = np.ascontiguousarray(v_full[:, :, lo - 1: hi + 2])
-    f = np.ascontiguousarray(f_full[:, :, lo - 1: hi + 2])
-    nzl = hi - lo + 1
-
-    def halo(a):
-        reqs = []
-        recv_lo = torch.zeros(a.shape[0] * a.shape[1], dtype=torch.float64)
-        recv_hi = torch.zeros_like(recv_lo)
-        if rank > 0:
-            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(a[:, :, 1]).ravel()), rank - 1))
-            reqs.append(dist.irecv(recv_lo, rank - 1))
-        if rank + 1 < world:
-            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(a[:, :, nzl]).ravel()), rank + 1))
-            reqs.append(dist.irecv(recv_hi, rank + 1))
-        for r_ in reqs:
-            r_.wait()
-        if rank > 0:
-            a[:, :, 0] = recv_lo.numpy().reshape(a.shape[0], a.shape[1])
-        if rank + 1 < world:
-            a[:, :, nzl + 1] = recv_hi.numpy().reshape(a.shape[0], a.shape[1])
-
-    for _ in range(sweeps):
-        v = O.jacobi(v, f, h, O.LINEAR, 0.8, 1.0, 1)  # one sweep on the slab (ghosts are read-only)
-        halo(v)
-    _, n = O.residual(v, f, h, O.LINEAR)
-    part = torch.tensor([n * n], dtype=torch.float64)
-    allp = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
-    dist.all_gather(allp, part)
-    total = 0.0
-    for t in allp:  # rank order, as HipSolver::finishNorm
-        total += t.item()
-    q.put((rank, lo, hi, v[:, :, 1: nzl + 1].copy(), float(np.sqrt(total))))
-    dist.destroy_process_group()
+    try:
+        ops = X.schedule(params, world, rank, min_points)
+        if mutation:
+            ops = X.mutate(ops, mutation)
+        R = X.Rank(params, rank, world, min_points)
+        R.run(ops)
+        lo, hi, v = R.owned_v()
+        q.put((rank, lo, hi, v, R.history, sorted({op for op, _ in ops})))
+    except Exception as e:  # reported to the parent, which fails the test
+        import traceback
+        q.put((rank, None, None, None, traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()
 
 
-def test_gloo_two_rank_slab_sweeps():
-    dims, sweeps, world = (23, 18, 30), 4, 2
+REPLAY_CASES = [
+    # fused pairs, slab residual+restriction, fused prolongation pair on slabs, gather + coarse cycle
+    ((64, 256, 64), 2, -1, 2, 2),
+    # single sweeps (levels too small for pairs), unfused prolongation
+    ((40, 36, 64), 2, 0, 2, 2),
+    # odd smoothing counts: a pair plus a single sweep; odd coarse-cycle count (its result in vAlt)
+    ((64, 256, 64), 2, -1, 3, 2),
+    # three ranks, uneven slabs
+    ((48, 256, 70), 3, -1, 2, 2),
+]
+
+
+def _replay(dims, world, min_points, pre, post, cycles=2, mutation=None):
+    import gpusolve as gsv
+    params = gsv.GridParams(maxiter=cycles, tol=0.0, gridDim=dims, mode=0, preSmoothing=pre, postSmoothing=post)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_slab_worker, args=(r, world, port, dims, sweeps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_replay_worker, args=(r, world, port, params, min_points, q, mutation))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
+    for r in res:
+        assert r[1] is not None, r[4]
+    for p in procs:
         assert p.exitcode == 0
-    nx, ny, nz = dims
-    f_full = O.rhs(nx, ny, nz, O.LINEAR)
-    rng = np.random.default_rng(1)
-    v_full = O.zeros(nx, ny, nz)
-    v_full[1:-1, 1:-1, 1:-1] = rng.uniform(-1, 1, (nx, ny, nz))
-    ref = O.jacobi(v_full, f_full, 1.0 / (ny + 1), O.LINEAR, 0.8, 1.0, sweeps)
-    _, ref_norm = O.residual(ref, f_full, 1.0 / (ny + 1), O.LINEAR)
-    got = O.zeros(nx, ny, nz)
-    for rank, lo, hi, slab, norm in res:
-        got[:, :, lo: hi + 1] = slab
-        assert abs(norm - ref_norm) <= 1e-13 * ref_norm
-    np.testing.assert_array_equal(got, ref)
+    og = O.Grid(dims, mode=O.LINEAR, maxiter=cycles, pre=pre, post=post)
+    ref_hist = og.solve()
+    ref_v = og.field(0, "v").copy()  # (a view into the oracle grid, which dies with og)
+    got = np.full_like(ref_v, np.nan)
+    got[:, :, 0] = ref_v[:, :, 0]
+    got[:, :, -1] = ref_v[:, :, -1]
+    ops_seen = set()
+    hists = []
+    for rank, lo, hi, v, hist, ops in res:
+        got[:, :, lo: hi + 1] = v
+        ops_seen |= set(ops)
+        hists.append(hist)
+    return got, ref_v, hists, ref_hist, ops_seen
+
+
+@pytest.mark.parametrize("dims,world,min_points,pre,post", REPLAY_CASES)
+def test_gloo_replay_of_driver_schedule(dims, world, min_points, pre, post):
+    """The Z-slab schedule the driver itself issues (HipSolver in trace mode, gs_grid.cpp), replayed on
+    `world` gloo ranks with the oracle's point arithmetic: level-0 fields bit-identical to the
+    single-domain oracle solve and the residual history to 1e-12. A changed exchange order, plane
+    range or ghost depth in gs_grid.cpp that breaks the decomposition fails here, on the CPU."""
+    got, ref_v, hists, ref_hist, ops_seen = _replay(dims, world, min_points, pre, post)
+    for hist in hists:
+        assert len(hist) == len(ref_hist)
+        for a, b in zip(hist, ref_hist):
+            assert abs(a - b) <= 1e-12 * abs(b), (a, b)
+    np.testing.assert_array_equal(got, ref_v)
+    if dims == (64, 256, 64) and pre == 2:
+        assert {"pair", "pro", "resrestrict", "halo", "gather", "coarse"} <= ops_seen, ops_seen
+
+
+@pytest.mark.parametrize("mutation", ["halo", "depth", "range"])
+def test_gloo_replay_catches_a_broken_schedule(mutation):
+    """The same replay with one deliberate schedule defect must NOT reproduce the oracle."""
+    got, ref_v, hists, ref_hist, _ = _replay((64, 256, 64), 2, -1, 2, 2, mutation=mutation)
+    same_field = np.array_equal(got, ref_v)
+    same_hist = all(abs(a - b) <= 1e-12 * abs(b) for a, b in zip(hists[0], ref_hist))
+    assert not (same_field and same_hist), "a broken schedule went unnoticed"
