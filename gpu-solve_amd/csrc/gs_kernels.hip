@@ -41,6 +41,7 @@ struct Coef {
     double alpha;  // h*h / s0          (CpuSolver.cpp:145)
     double preFac; // s0 / (h*h)        (CpuSolver.cpp:144)
     int fastdiv;   // 2^-120 <= hh <= 1: div_hh may take its 3-operation path
+    int unit;      // s[1..6] == -1 and |s[0]| >= 1: the unit-neighbour stencil sum applies (stencil_sum<true>)
     int64_t off[7]; // generic kernel: linear element offsets of the 7 entries
 };
 
@@ -75,6 +76,9 @@ Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamm
     k.alpha = k.hh / S->s[0];
     k.preFac = S->s[0] / k.hh;
     k.fastdiv = k.hh >= 0x1p-120 && k.hh <= 1.0;
+    static const bool noUnit = getenv("GS_NO_UNIT_STENCIL") != nullptr;
+    k.unit = !noUnit && (S->s[0] >= 1.0 || S->s[0] <= -1.0);
+    for (int i = 1; i < 7; i++) k.unit = k.unit && S->s[i] == -1.0;
     return k;
 }
 
@@ -150,10 +154,26 @@ __device__ __forceinline__ void div_hh_row(const Coef& k, double (&q)[2])
     }
 }
 
-// stencil sum in config order (before the division by h^2) — CpuSolver.cpp:56-62
+// stencil sum in config order (before the division by h^2) — CpuSolver.cpp:56-62.
+// UN (Coef::unit: the six neighbour weights are exactly -1, |s0| >= 1 — every reference config): the
+// same value in 7 instead of 14 operations, bit for bit. s += (-1) * x is s - x exactly (the product
+// by -1 is a sign flip, and IEEE subtraction is the addition of the negation), and the first term
+// 0.0 + s0 * c equals fma(s0, c, 0.0): both round the product once and add an exact zero, and with
+// |s0| >= 1 a non-zero product never underflows to a signed zero (the one case where they differ).
+template <bool UN = false>
 __device__ __forceinline__ double stencil_sum(const Coef& k, double c, double xp, double xm, double yp, double ym,
                                               double zp, double zm)
 {
+    if constexpr (UN) {
+        double s = __builtin_fma(k.s[0], c, 0.0);
+        s = s - xp;
+        s = s - xm;
+        s = s - yp;
+        s = s - ym;
+        s = s - zp;
+        s = s - zm;
+        return s;
+    }
     double s = 0.0;
     s += k.s[0] * c;
     s += k.s[1] * xp;
@@ -181,18 +201,11 @@ __device__ __forceinline__ double op_finish(const Coef& k, double q, double c, d
 }
 
 // stencil sum in config order, then /h^2 and the non-linear term  — CpuSolver.cpp:56-76
-template <int MODE>
+template <int MODE, bool UN = false>
 __device__ __forceinline__ double op_value(const Coef& k, double c, double xp, double xm, double yp, double ym,
                                            double zp, double zm, double w)
 {
-    double s = 0.0;
-    s += k.s[0] * c;
-    s += k.s[1] * xp;
-    s += k.s[2] * xm;
-    s += k.s[3] * yp;
-    s += k.s[4] * ym;
-    s += k.s[5] * zp;
-    s += k.s[6] * zm;
+    double s = stencil_sum<UN>(k, c, xp, xm, yp, ym, zp, zm);
     s = div_hh(k, s);
     if (MODE == GS_NEWTON) {
         const double ew = exp(w);
@@ -353,7 +366,7 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb)
 }
 
 template <int MODE, int KIND, bool ADD, int RY, int W, bool DPP, bool NT = false, bool XCD = false, bool NTV = false,
-          bool ZV = false>
+          bool ZV = false, bool UN = false>
 __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict__ v, const double* __restrict__ f,
                                                  const double* __restrict__ w, double* __restrict__ out,
                                                  double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
@@ -439,10 +452,10 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
                 constexpr bool NS = MODE == GS_NEWTON && KIND == 0;
                 const double Ax = NS ? k.gamma * (1 + wx) : 0.0, Ay = NS ? k.gamma * (1 + wy) : 0.0;
                 const double Ex = NS ? exp(wx) : 0.0, Ey = NS ? exp(wy) : 0.0;
-                const double a0 = NS ? newton_op(div_hh(k, stencil_sum(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x)), c.x, Ax, Ex)
-                                     : op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
-                const double a1 = NS ? newton_op(div_hh(k, stencil_sum(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)), c.y, Ay, Ey)
-                                     : op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
+                const double a0 = NS ? newton_op(div_hh(k, stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x)), c.x, Ax, Ex)
+                                     : op_value<MODE, UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
+                const double a1 = NS ? newton_op(div_hh(k, stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)), c.y, Ay, Ey)
+                                     : op_value<MODE, UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
                 double r0 = 0.0, r1 = 0.0; // residual of the input iterate
                 if (KIND != 2 || ADD) {
                     r0 = FL[cs][r].x - a0;
@@ -780,7 +793,7 @@ constexpr int RR2_WXMAX = 8, RR2_NR2_LOG2_POINTS = 26;
 
 // NR: coarse rows per block (1: fine rows 2Y-1..2Y+1 computed; 2: 2Y-1..2Y+3, the shared row 2Y+1 and three
 // of the seven v rows once instead of twice)
-template <int MODE, bool PF, int NR = 1> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
+template <int MODE, bool PF, int NR = 1, bool UN = false> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
 __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* __restrict__ v,
                                                          const double* __restrict__ f, const double* __restrict__ w,
                                                          double* __restrict__ ca,
@@ -900,8 +913,8 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             const double xm0 = lane_from_left<true>(c.y, CL[j]);
             const double xp1 = lane_from_right<true>(c.x, CR[j]);
             const double w0 = MODE == GS_NEWTON ? W[j].x : 0.0, w1 = MODE == GS_NEWTON ? W[j].y : 0.0;
-            const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, Vp[j].x, Vm[j].x, w0);
-            const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, Vp[j].y, Vm[j].y, w1);
+            const double a0 = op_value<MODE, UN>(k, c.x, c.y, xm0, yp.x, ym.x, Vp[j].x, Vm[j].x, w0);
+            const double a1 = op_value<MODE, UN>(k, c.y, xp1, c.x, yp.y, ym.y, Vp[j].y, Vm[j].y, w1);
             const bool ok = pin && rowc[j + 1];
             R[j] = make_double2((ok && okx0) ? F[j].x - a0 : 0.0, (ok && okx1) ? F[j].y - a1 : 0.0);
         }
@@ -1535,7 +1548,7 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
 // lane (lane j <-> local row j, y-neighbours by lane shifts, x-neighbours loaded) with the same point
 // expression, so every output is bit-identical to two gs_jacobi_sweep calls.
 template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0,
-          int PFD = 1, bool XH = false>
+          int PFD = 1, bool XH = false, bool UN = false>
 __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* __restrict__ v,
                                                            const double* __restrict__ f, const double* __restrict__ w,
                                                            double* __restrict__ out, double* __restrict__ partials,
@@ -1813,7 +1826,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         const double c = EC;
                         const double lm = lane_from_left<true>(EC, 0.0), lp = lane_from_right<true>(EC, 0.0);
                         const double ym = M ? lp : lm, yp = M ? lm : lp;
-                        const double a = op_value<MODE>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP, 0.0);
+                        const double a = op_value<MODE, UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP, 0.0);
                         const double nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
                         ES1n = (!pz || !erowc) ? c : nv;
                     }
@@ -1834,8 +1847,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                     const double2 ym = M ? lp : lm, yp = M ? lm : lp;
                     const double xm0 = lane_from_left<true>(c.y, CL[j]);
                     const double xp1 = lane_from_right<true>(c.x, CR[j]);
-                    double q[2] = {stencil_sum(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
-                                   stencil_sum(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
+                    double q[2] = {stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
+                                   stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
                     div_hh_row<MODE>(k, q);
                     double a0, a1, n0, n1;
                     if constexpr (MODE == GS_NEWTON) {
@@ -1875,8 +1888,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         const double2 ym = M ? lp : lm, yp = M ? lm : lp;
                         const double xm0 = lane_from_left<true>(c.y, CL[NV + j - 1]);
                         const double xp1 = lane_from_right<true>(c.x, CR[NV + j - 1]);
-                        double q[2] = {stencil_sum(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
-                                       stencil_sum(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
+                        double q[2] = {stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
+                                       stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
                         div_hh_row<MODE>(k, q);
                         double o0, o1;
                         if constexpr (MODE == GS_NEWTON) {
@@ -2077,7 +2090,8 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
     const PassPlan plan = pass_plan(S, L);
     if (plan.rb) {
         const dim3 g = plan.grid, b(WAVE, RB_W);
-#define GS_RB(M, Z) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, true, RB_NT, false, false, Z>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz, plan.zc)
+#define GS_RBU(M, Z, U) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, true, RB_NT, false, false, Z, U>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz, plan.zc)
+#define GS_RB(M, Z) do { if (k.unit) GS_RBU(M, Z, true); else GS_RBU(M, Z, false); } while (0)
         if (!v) {
             if constexpr (KIND == 0 && !ADD) {
                 if (mode == GS_LINEAR) GS_RB(GS_LINEAR, true);
@@ -2087,6 +2101,7 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
         else if (mode == GS_NONLINEAR) GS_RB(GS_NONLINEAR, false);
         else GS_RB(GS_NEWTON, false);
 #undef GS_RB
+#undef GS_RBU
     } else {
         const dim3 g = plan.grid, b(GN_BX, GN_BY);
 #define GS_GN(M) hipLaunchKernelGGL((k_generic<M, KIND, ADD>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
@@ -2280,8 +2295,10 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
 #define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
-#define GS_TBY(M, Z) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M)>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
-#define GS_TBX(M, Z, P) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TBY1(M, Z, U) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M), false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TBY(M, Z) do { if (k.unit) GS_TBY1(M, Z, true); else GS_TBY1(M, Z, false); } while (0)
+#define GS_TBX1(M, Z, P, U) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TBX(M, Z, P) do { if (k.unit) GS_TBX1(M, Z, P, true); else GS_TBX1(M, Z, P, false); } while (0)
     const bool zv = !v_in;
     if (xh) {
         if (mode == GS_LINEAR) {
@@ -2305,7 +2322,9 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
         else GS_TB(GS_NEWTON, false);
     }
 #undef GS_TBX
+#undef GS_TBX1
 #undef GS_TBY
+#undef GS_TBY1
 #undef GS_TB
     return launch_status();
 }
@@ -2341,10 +2360,12 @@ int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, d
     coarse_v += czoff * cl->ldz;
     if (coarse_sub) coarse_sub += czoff * cl->ldz;
     const Coef k = make_coef(S, L, omega, gamma);
-#define GS_TBP(M, P) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, false, true, P, 1>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz)
+#define GS_TBP1(M, P, U) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, false, true, P, 1, false, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz)
+#define GS_TBP(M, P) do { if (k.unit) GS_TBP1(M, P, true); else GS_TBP1(M, P, false); } while (0)
     if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1);
     else GS_TBP(GS_LINEAR, 1);
 #undef GS_TBP
+#undef GS_TBP1
     return launch_status();
 }
 
@@ -2433,12 +2454,14 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         const dim3 g((unsigned)rows, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
-#define GS_RR2(M, N) hipLaunchKernelGGL((k_rr2<M, false, N>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
+#define GS_RR2U(M, N, U) hipLaunchKernelGGL((k_rr2<M, false, N, U>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
+#define GS_RR2(M, N) do { if (k.unit) GS_RR2U(M, N, true); else GS_RR2U(M, N, false); } while (0)
         if (mode == GS_LINEAR && nr == 2) GS_RR2(GS_LINEAR, 2);
         else if (mode == GS_LINEAR) GS_RR2(GS_LINEAR, 1);
         else if (mode == GS_NONLINEAR) GS_RR2(GS_NONLINEAR, 1);
         else GS_RR2(GS_NEWTON, 1);
 #undef GS_RR2
+#undef GS_RR2U
         return launch_status();
     }
     StencilOffsets so;

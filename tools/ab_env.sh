@@ -9,6 +9,6 @@ for rep in 1 2; do
   for val in "$A" "$B"; do
     echo "[$(date +%T)] $VAR=$val rep $rep"
     env "$VAR=$val" timeout -k 10 300 python bench.py --cpu-sweeps 0 --newton-iters 0 "$@" > "$OUT/${VAR}_${val}_$rep.json" 2> "$OUT/${VAR}_${val}_$rep.err" || { tail -20 "$OUT/${VAR}_${val}_$rep.err"; exit 1; }
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; v=d.get('vcycle') or {}; print(sys.argv[2], 'value', d['value'], 'kernel_ms', r['kernel_ms'], 'frac', r['frac'], 'vcycle_ms', v.get('ms'), r['kernel'][:40])" "$OUT/${VAR}_${val}_$rep.json" "$VAR=$val"
+    python tools/bench_brief.py "$OUT/${VAR}_${val}_$rep.json"
   done
 done
