@@ -5,27 +5,28 @@
 set -o pipefail
 TAG=${1:-r01}
 STEPS=${2:-20}
+WARM=${3:-5}   # the driver runs bench.py --steps 20 --warmup 5
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
 
 step pytest-gpu
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
 tail -2 "$OUT/pytest_gpu.log"
 
 step kbench
 timeout -k 10 500 python tools/kbench.py --bw --pairs --zc 0 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 || { tail -20 "$OUT/kbench.log"; exit 1; }
 
 step bench
-timeout -k 10 600 python bench.py --steps "$STEPS" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
+timeout -k 10 600 python bench.py --steps "$STEPS" --warmup "$WARM" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
 
 # kernel statistics of the bench's timed smoother alone (no V-cycles: every launch of the pair kernel
 # is a level-0 launch, so its average is the bench's kernel_ms)
 step rocprof-kernel-trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python bench.py --steps "$STEPS" --cpu-sweeps 0 --newton-iters 0 --vcycles 0 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail -20 "$OUT/bench_prof.err"; exit 1; }
+    python bench.py --steps "$STEPS" --warmup "$WARM" --cpu-sweeps 0 --newton-iters 0 --vcycles 0 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail -20 "$OUT/bench_prof.err"; exit 1; }
 
 # the V-cycle's kernels (tools/vc_breakdown.py reads the trace)
 step rocprof-vcycle
