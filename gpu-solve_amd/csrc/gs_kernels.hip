@@ -2446,6 +2446,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         // NONLINEAR / NEWTON: one row (VGPR budget). GS_RR_NR=1|2 forces the choice (A/B, tests).
         static const int nr_env = getenv("GS_RR_NR") ? std::atoi(getenv("GS_RR_NR")) : 0;
         const bool big = fl->nx * fl->ny * fl->nz >= ((int64_t)1 << RR2_NR2_LOG2_POINTS);
+        // (NEWTON with two rows spills 19 VGPRs: 40.5 vs 38.9 ms per 512^3 Newton iteration, gpurun_out/rrn)
         const int nr = mode == GS_LINEAR && (nr_env == 2 || (nr_env == 0 && big)) ? 2 : 1;
         const int64_t rows = (cl->ny + nr - 1) / nr; // blocks along y
         const int64_t chunks = (2048 + rows - 1) / rows;
