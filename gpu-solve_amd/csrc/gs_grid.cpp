@@ -125,7 +125,8 @@ LevelClock::~LevelClock()
 // (src/cpu/CpuGridData.cpp:19-41). Fields a mode never touches are not allocated.
 HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomeratePoints,
                          std::vector<std::string>* traceLog)
-    : GridParams(grid), trace(traceLog), comm_(comm), stream_(traceLog == nullptr), commStream_(traceLog == nullptr)
+    : GridParams(grid), trace(traceLog), comm_(comm), stream_(traceLog == nullptr), commStream_(traceLog == nullptr),
+      bndStream_(traceLog == nullptr && comm != nullptr && comm->size() > 1)
 {
     const bool dry = traceLog != nullptr;
     const std::size_t mn = std::min(std::min(gridDim[0], gridDim[1]), gridDim[2]);
@@ -225,6 +226,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
     check((int)hipHostMalloc((void**)&hNorm_, sizeof(double), hipHostMallocDefault), "hipHostMalloc");
     check((int)hipEventCreateWithFlags(&evA_, hipEventDisableTiming), "hipEventCreate");
     check((int)hipEventCreateWithFlags(&evB_, hipEventDisableTiming), "hipEventCreate");
+    check((int)hipEventCreateWithFlags(&evC_, hipEventDisableTiming), "hipEventCreate");
     // level-0 right-hand side on the device (src/cpu/CpuGridData.cpp:44-78), h = 1/(Y+1) (main.cpp:84);
     // a slab evaluates it at its global plane indices (geom.z0)
     check(gs_rhs_init(&levels_[0].geom, levels_[0].f.data(), (int)mode, 1.0 / (gridDim[1] + 1), gamma, s),
@@ -237,12 +239,14 @@ HipGridData::~HipGridData()
 {
     if (stream_.s) (void)hipStreamSynchronize(stream_.s);
     if (commStream_.s) (void)hipStreamSynchronize(commStream_.s);
+    if (bndStream_.s) (void)hipStreamSynchronize(bndStream_.s);
     if (partials_ && !trace) (void)hipFree(partials_);
     if (dNorm_) (void)hipFree(dNorm_);
     if (dRankSums_) (void)hipFree(dRankSums_);
     if (hNorm_) (void)hipHostFree(hNorm_);
     if (evA_) (void)hipEventDestroy(evA_);
     if (evB_) (void)hipEventDestroy(evB_);
+    if (evC_) (void)hipEventDestroy(evC_);
 }
 
 void HipGridData::rec(const char* op, std::initializer_list<std::pair<const char*, long long>> kv, const char* field)
@@ -418,14 +422,24 @@ void restrictTo(HipGridData& g, const DeviceField& src, std::size_t l, DeviceFie
 
 } // namespace
 
-// The overlapped exchange: the comm stream waits for the boundary planes (fork), the compute stream
-// for the exchange before the next sweep (join; recorded after the exchange, waited on after the
-// interior launch). Nothing to order in trace mode.
+// The overlapped exchange of a Z-slab sweep: the boundary planes run on their own stream (forked
+// from the compute stream), the exchange on the comm stream after them, and the interior planes on
+// the compute stream concurrently with both; the compute stream waits for the exchange (join,
+// recorded after it, waited on after the interior launch) before the next sweep. The boundary and
+// interior launches write disjoint planes of vAlt and only read v. Nothing to order in trace mode.
+hipStream_t HipSolver::forkBoundary(HipGridData& grid)
+{
+    if (grid.trace) return grid.stream();
+    check((int)hipEventRecord(grid.evA_, grid.stream()), "hipEventRecord");
+    check((int)hipStreamWaitEvent(grid.bndStream_.s, grid.evA_, 0), "hipStreamWaitEvent");
+    return grid.bndStream_.s;
+}
+
 void HipSolver::forkComm(HipGridData& grid)
 {
     if (grid.trace) return;
-    check((int)hipEventRecord(grid.evA_, grid.stream()), "hipEventRecord");
-    check((int)hipStreamWaitEvent(grid.commStream(), grid.evA_, 0), "hipStreamWaitEvent");
+    check((int)hipEventRecord(grid.evC_, grid.bndStream_.s), "hipEventRecord");
+    check((int)hipStreamWaitEvent(grid.commStream(), grid.evC_, 0), "hipStreamWaitEvent");
 }
 
 void HipSolver::joinComm(HipGridData& grid, bool wait)
@@ -550,22 +564,23 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
     while (sweeps > 0) {
         const bool pair = L.fusedPairs && sweeps >= 2;
         const int64_t b = pair ? 2 : depth; // outermost planes whose ghost copies the neighbours need
-        auto run = [&](int64_t z1, int64_t z2) {
-            if (pair) pairPlanes(grid, L, z1, z2, s);
-            else sweepPlanes(grid, L, z1, z2, s);
+        auto run = [&](int64_t z1, int64_t z2, hipStream_t st) {
+            if (pair) pairPlanes(grid, L, z1, z2, st);
+            else sweepPlanes(grid, L, z1, z2, st);
         };
         if (!dist) {
-            run(1, nz);
+            run(1, nz, s);
         } else if (grid.overlapHalo && nz >= 2 * b + 1) {
-            run(1, b);
-            run(nz - b + 1, nz);
+            const hipStream_t bs = forkBoundary(grid);
+            run(1, b, bs);
+            run(nz - b + 1, nz, bs);
             forkComm(grid);
             grid.halo(L, L.vAlt, grid.commStream(), depth);
             joinComm(grid, false);
-            run(b + 1, nz - b);
+            run(b + 1, nz - b, s);
             joinComm(grid, true);
         } else {
-            run(1, nz);
+            run(1, nz, s);
             grid.halo(L, L.vAlt, s, depth);
         }
         L.v.swap(L.vAlt);
@@ -629,21 +644,22 @@ double HipSolver::speculativeSweep(HipGridData& grid, int* sweeps)
     const bool pair = L.fusedPairs && grid.preSmoothing >= 2;
     const int depth = grid.vDepth(L);
     const int64_t b = pair ? 2 : depth;
-    auto run = [&](int64_t z1, int64_t z2) {
-        n += pair ? pairPlanes(grid, L, z1, z2, s, P + n) : sweepPlanes(grid, L, z1, z2, s, P + n);
+    auto run = [&](int64_t z1, int64_t z2, hipStream_t st) {
+        n += pair ? pairPlanes(grid, L, z1, z2, st, P + n) : sweepPlanes(grid, L, z1, z2, st, P + n);
     };
     if (!(L.distributed && grid.nranks() > 1)) {
-        run(1, nz);
+        run(1, nz, s);
     } else if (grid.overlapHalo && nz >= 2 * b + 1) {
-        run(1, b);
-        run(nz - b + 1, nz);
+        const hipStream_t bs = forkBoundary(grid);
+        run(1, b, bs);
+        run(nz - b + 1, nz, bs);
         forkComm(grid);
         grid.halo(L, L.vAlt, grid.commStream(), depth);
         joinComm(grid, false);
-        run(b + 1, nz - b);
+        run(b + 1, nz - b, s);
         joinComm(grid, true);
     } else {
-        run(1, nz);
+        run(1, nz, s);
         grid.halo(L, L.vAlt, s, depth);
     }
     if (sweeps) *sweeps = pair ? 2 : 1;
@@ -767,8 +783,9 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
                 proPlanes(grid, F, C, 1, nz, s);
             } else if (grid.overlapHalo && nz >= 5) {
                 const int64_t zt = nz % 2 == 0 ? nz - 1 : nz - 2; // odd start: 2 or 3 top planes
-                proPlanes(grid, F, C, 1, 2, s);
-                proPlanes(grid, F, C, zt, nz, s);
+                const hipStream_t bs = forkBoundary(grid);
+                proPlanes(grid, F, C, 1, 2, bs);
+                proPlanes(grid, F, C, zt, nz, bs);
                 forkComm(grid);
                 grid.halo(F, F.vAlt, grid.commStream(), grid.vDepth(F));
                 joinComm(grid, false);

@@ -146,11 +146,12 @@ private:
     Comm* comm_ = nullptr;
     StreamGuard stream_;
     StreamGuard commStream_;
+    StreamGuard bndStream_; // boundary planes of an overlapped Z-slab sweep (distributed grids only)
     double* partials_ = nullptr;
     double* dNorm_ = nullptr;
     double* dRankSums_ = nullptr;
     double* hNorm_ = nullptr;
-    hipEvent_t evA_ = nullptr, evB_ = nullptr;
+    hipEvent_t evA_ = nullptr, evB_ = nullptr, evC_ = nullptr;
     std::vector<double> dryParts_;
     friend class HipSolver;
 };
@@ -176,6 +177,7 @@ public:
     // the V-cycle below level `from` (its f set) in one gs_coarse_cycle launch
     static void coarseCycle(HipGridData& grid, std::size_t from);
     static double finishNorm(HipGridData& grid, int64_t nparts);
+    static hipStream_t forkBoundary(HipGridData& grid);
     static void forkComm(HipGridData& grid);
     static void joinComm(HipGridData& grid, bool wait);
 
