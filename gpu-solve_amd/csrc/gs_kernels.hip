@@ -1994,10 +1994,6 @@ bool tbx_pfd2()
     return two;
 }
 
-// Geometry rule of the fused pair: the whole x-row in one block and enough work for >= 512 blocks of
-// 4-plane chunks; the z-chunk is then chosen for >= 1024 blocks (4..64 planes: at 512^3, 64-plane
-// chunks measured 5-8% faster than 32 — fewer re-read chunk-boundary planes).
-// Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU); *y2: the k_tb2y shape.
 // Column blocks (k_tb2y XH) for rows of more than 512 points in LINEAR / NONLINEAR mode: 1024-point rows
 // (BASELINE config #5) were k_tb2's one-y-wave shape before; GS_PAIR_XH=0 restores that (A/B).
 bool xh_enabled()
@@ -2007,7 +2003,7 @@ bool xh_enabled()
 }
 
 // Geometry rule of the fused pair: the whole x-row in one block (or, XH, one column block of 512
-// points) and enough work for >= 512 blocks of 4-plane chunks; the z-chunk is then chosen for >= 1024
+// points) and enough work for >= 128 blocks of 4-plane chunks; the z-chunk is then chosen for >= 1024
 // blocks (4..64 planes: at 512^3, 64-plane chunks measured 5-8% faster than 32 — fewer re-read
 // chunk-boundary planes). Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU);
 // *y2: the k_tb2y whole-row shape, *xh: the k_tb2y column-block shape (neither: k_tb2).
@@ -2021,7 +2017,12 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
     const int64_t nh = colb ? (L->nx + 2 * WAVE * TBY_WX - 1) / (2 * WAVE * TBY_WX) : 1;
     const int rows = (two || colb) ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block
     const int64_t tiles = (L->ny + rows - 1) / rows * nh;
-    const int fills = tiles * ((L->nz + 3) / 4) >= 512 ? 2 : 1;
+    // the block count (of 4-plane chunks) from which the pair is the level's smoother: 128 takes 64^3
+    // (256 blocks: ZV pair + prolongation pair 23.5 us vs 4 one-point sweeps + prolongation 24.7 us) and
+    // leaves 32^3 (64 blocks: 25.2 vs 23.9 us) to the one-point kernel (gpurun_out/pmb, r02);
+    // GS_PAIR_MIN_BLOCKS overrides it (A/B)
+    static const int64_t minBlocks = getenv("GS_PAIR_MIN_BLOCKS") ? std::atoll(getenv("GS_PAIR_MIN_BLOCKS")) : 128;
+    const int fills = tiles * ((L->nz + 3) / 4) >= minBlocks ? 2 : 1;
     int64_t c = tiles * L->nz / 1024;
     c = c < 4 ? 4 : (c > 64 ? 64 : c);
     // levels of >= 2^26 points: chunks for ~512 blocks, up to 128 planes (one 8-wave block per CU, two
