@@ -14,7 +14,9 @@ Multi-GPU (torchrun, one process per GPU): the grid is Z-slab partitioned over R
 planes exchanged every sweep on a second stream while the interior planes are swept; weak scaling
 with 512^3 lattice points per rank: N=2 -> 512x512x1024, N=4 -> 512x1024x1024 (every rank's slab has
 the single-GPU run's 512-point rows, so the per-rank kernels are the N=1 ones), N=8 -> 1024^3
-(BASELINE config #5: 1024-point rows, the 8-wave-row pair k_tb2); other N -> 512x512x(512N).
+(BASELINE config #5: 1024-point rows, the column-block pair); other N -> 512x512x(512N). Every
+rank runs the same number of sweeps (the untimed ramp's length is agreed across ranks), since each
+sweep's ghost exchange pairs with the neighbours'.
 
 Roofline: the smoother is HBM-bound (0.5 flop/B per sweep); algorithmic bytes per launch = 24 B
 per lattice point (read v, read f, write the result) x 512^3, for a single sweep
@@ -237,6 +239,19 @@ def newton_timing(n, iters):
             "residuals": hist}
 
 
+def ramp_sweeps(run, ramp_ms, any_rank, chunk=40):
+    """Untimed ramp: `run(chunk)` (launch + wait) until `ramp_ms` of wall time has passed on EVERY rank.
+    `any_rank(flag)` is the OR of flag over all ranks, so all ranks run the same number of chunks — a
+    rank that ran one chunk more than its neighbour would post a ghost exchange nobody answers.
+    Returns (sweeps run, wall ms)."""
+    tw = time.perf_counter()
+    done = 0
+    while any_rank((time.perf_counter() - tw) * 1e3 < ramp_ms):
+        run(chunk)
+        done += chunk
+    return done, (time.perf_counter() - tw) * 1e3
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,14 +283,20 @@ def main():
     fused = drv.gs_grid_level_fused(grid.handle, 0) == 1
     # untimed ramp: the requested warm-up sweeps, then more until at least --ramp-ms of smoother launches
     # have run (cold launches run ~25 % slower: BENCH_r01 timed them inside a 7.8 ms window)
-    tw = time.perf_counter()
-    sweeps(a.warmup)
-    grid.sync()
-    ramp = 0
-    while (time.perf_counter() - tw) * 1e3 < a.ramp_ms:
-        sweeps(40)
+    def any_rank(flag):
+        if world == 1:
+            return flag
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item() > 0
+
+    def run(k):
+        sweeps(k)
         grid.sync()
-        ramp += 40
+
+    tw = time.perf_counter()
+    run(a.warmup)
+    ramp, _ = ramp_sweeps(run, max(0.0, a.ramp_ms - (time.perf_counter() - tw) * 1e3), any_rank)
     warmup_ms = (time.perf_counter() - tw) * 1e3
     barrier()
     torch.cuda.synchronize()
