@@ -2019,7 +2019,8 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
     const int64_t tiles = (L->ny + rows - 1) / rows * nh;
     // the block count (of 4-plane chunks) from which the pair is the level's smoother: 128 takes 64^3
     // (256 blocks: ZV pair + prolongation pair 23.5 us vs 4 one-point sweeps + prolongation 24.7 us) and
-    // leaves 32^3 (64 blocks: 25.2 vs 23.9 us) to the one-point kernel (gpurun_out/pmb, r02);
+    // leaves 32^3 (64 blocks: 25.2 vs 23.9 us) to the one-point kernel (rocprofv3 V-cycle traces, r02:
+    // tools/rr_ab_session.sh pmb GS_PAIR_MIN_BLOCKS 512 128);
     // GS_PAIR_MIN_BLOCKS overrides it (A/B)
     static const int64_t minBlocks = getenv("GS_PAIR_MIN_BLOCKS") ? std::atoll(getenv("GS_PAIR_MIN_BLOCKS")) : 128;
     const int fills = tiles * ((L->nz + 3) / 4) >= minBlocks ? 2 : 1;
