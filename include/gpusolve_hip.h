@@ -124,6 +124,19 @@ int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, d
                              const double* v_in, const double* coarse_v, const double* coarse_sub,
                              const gs_level* coarse, double* v_out, const double* f, const double* w, int zlo,
                              int zhi, hipStream_t stream);
+/* The first pre-smoothing pair of a 2-sweep pre-smoothing, the residual of its result and the full
+ * weighting in one pass: v_out = S(S(v_in)), coarse_a (and coarse_b if not NULL) = R(f - A(v_out)) on
+ * the coarse interior, partials (may be NULL) = gs_jacobi_sweep2_restrict_num_partials per-block sums
+ * of r^2 of f - A(v_in). Bit-identical to gs_jacobi_sweep2 followed by gs_residual_restrict (the norm
+ * in this kernel's block order). Replaces CpuSolver.cpp:94-99 (jacobi(pre = 2), compResidual,
+ * restrict). Supported (gs_jacobi_sweep2_restrict_supported != 0) for LINEAR levels with the unit
+ * 7-point stencil (canonical order, neighbour weights -1, |s0| >= 1), rows <= 512 points, z0 = 0, and
+ * coarse = fine / 2 per axis; GS_EINVAL otherwise. */
+int gs_jacobi_sweep2_restrict_supported(const gs_stencil* S, const gs_level* fine, const gs_level* coarse, int mode);
+int gs_jacobi_sweep2_restrict(const gs_stencil* S, const gs_level* fine, double omega, const double* v_in,
+                              double* v_out, const double* f, double* partials, double* coarse_a, double* coarse_b,
+                              const gs_level* coarse, hipStream_t stream);
+int64_t gs_jacobi_sweep2_restrict_num_partials(const gs_stencil* S, const gs_level* fine, const gs_level* coarse);
 /* Which fused-pair kernel (and shape) gs_jacobi_sweep2 launches for this level and mode ("" if none). */
 const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int mode);
 
