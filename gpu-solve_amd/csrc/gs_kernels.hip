@@ -2645,10 +2645,9 @@ static bool prr_plan(const gs_stencil* S, const gs_level* fl, const gs_level* cl
 
 int gs_jacobi_sweep2_restrict_supported(const gs_stencil* S, const gs_level* fl, const gs_level* cl, int mode)
 {
-    static const bool off = getenv("GS_NO_PAIR_RESTRICT") != nullptr;
     int zc;
     dim3 g, b;
-    return !off && prr_plan(S, fl, cl, mode, &zc, &g, &b) ? 1 : 0;
+    return prr_plan(S, fl, cl, mode, &zc, &g, &b) ? 1 : 0;
 }
 
 int64_t gs_jacobi_sweep2_restrict_num_partials(const gs_stencil* S, const gs_level* fl, const gs_level* cl)
