@@ -340,9 +340,10 @@ int gs_grid_time_vcycles(void* grid, int cycles, double* ms, double* last_residu
         gs::check((int)hipStreamSynchronize(g.stream()), "hipStreamSynchronize");
         const auto t0 = std::chrono::steady_clock::now();
         double r = 0;
-        for (int c = 0; c < cycles; c++) r = gs::HipSolver::vcycleSpeculative(g, &pending);
-        if (pending) { // drop the speculative sweep: v stays the last cycle's result
-        }
+        gs::HipSolver::runCycles(g, &pending, (std::size_t)std::max(cycles, 0), [&](std::size_t, double res) {
+            r = res;
+            return false;
+        }); // (a speculative sweep left in vAlt is dropped: v stays the last cycle's result)
         const auto t1 = std::chrono::steady_clock::now();
         if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         if (last_residual) *last_residual = r;

@@ -30,6 +30,7 @@ void ncclOk(ncclResult_t e, const char* what)
 
 // ---------------------------------------------------------------------------------------------
 void Comm::sync(hipStream_t s) { hipOk(hipStreamSynchronize(s), "hipStreamSynchronize"); }
+void Comm::syncEvent(hipEvent_t e) { hipOk(hipEventSynchronize(e), "hipEventSynchronize"); }
 
 double commTimeoutS(const char* env, double dflt)
 {
@@ -126,10 +127,21 @@ public:
 
     void sync(hipStream_t s) override
     {
+        wait([&] { return hipStreamQuery(s); }, "stream sync");
+    }
+    void syncEvent(hipEvent_t e) override
+    {
+        wait([&] { return hipEventQuery(e); }, "event sync");
+    }
+
+private:
+    // a bounded wait for `query` (hipStreamQuery / hipEventQuery) that polls the async error state
+    void wait(const std::function<hipError_t()>& query, const char* what)
+    {
         const bool inject = injectNow();
         const std::string err = boundedWait(
             [&]() -> int {
-                const hipError_t q = hipStreamQuery(s);
+                const hipError_t q = query();
                 const int a = asyncState(inject);
                 if (a > 1) return a;
                 if (q == hipSuccess) return 0;
@@ -140,11 +152,10 @@ public:
                 return st < 0 ? std::string(hipGetErrorString((hipError_t)-st))
                               : std::string(ncclGetErrorString((ncclResult_t)(st - 2)));
             },
-            timeout_, "stream sync");
+            timeout_, what);
         if (!err.empty()) abortAndThrow(err);
     }
 
-private:
     // 1 in progress, 0 settled, 2 + ncclResult_t for an error
     int asyncState(bool inject)
     {
@@ -358,6 +369,7 @@ public:
         throw Error("trace communicator: no transport");
     }
     void sync(hipStream_t) override {}
+    void syncEvent(hipEvent_t) override {}
 
 private:
     int r_, n_;

@@ -41,6 +41,8 @@ public:
     // becomes a gs::Error (communicator aborted) instead of a hang. The solver's one host sync per
     // V-cycle (the norm readback) goes through here.
     virtual void sync(hipStream_t s);
+    // The same wait for one event (work enqueued on the stream after it is not waited for).
+    virtual void syncEvent(hipEvent_t e);
 };
 
 // RCCL (NCCL API); uid is the 128-byte ncclUniqueId created by rank 0 (rcclUniqueId) and shared.

@@ -227,6 +227,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
     check((int)hipEventCreateWithFlags(&evA_, hipEventDisableTiming), "hipEventCreate");
     check((int)hipEventCreateWithFlags(&evB_, hipEventDisableTiming), "hipEventCreate");
     check((int)hipEventCreateWithFlags(&evC_, hipEventDisableTiming), "hipEventCreate");
+    check((int)hipEventCreateWithFlags(&evNorm_, hipEventDisableTiming), "hipEventCreate");
     // level-0 right-hand side on the device (src/cpu/CpuGridData.cpp:44-78), h = 1/(Y+1) (main.cpp:84);
     // a slab evaluates it at its global plane indices (geom.z0)
     check(gs_rhs_init(&levels_[0].geom, levels_[0].f.data(), (int)mode, 1.0 / (gridDim[1] + 1), gamma, s),
@@ -247,6 +248,7 @@ HipGridData::~HipGridData()
     if (evA_) (void)hipEventDestroy(evA_);
     if (evB_) (void)hipEventDestroy(evB_);
     if (evC_) (void)hipEventDestroy(evC_);
+    if (evNorm_) (void)hipEventDestroy(evNorm_);
 }
 
 void HipGridData::rec(const char* op, std::initializer_list<std::pair<const char*, long long>> kv, const char* field)
@@ -273,6 +275,22 @@ double HipGridData::readNorm()
     if (trace) return 1.0; // (no device: the traced norms are placeholders)
     check((int)hipMemcpyAsync(hNorm_, dNorm_, sizeof(double), hipMemcpyDeviceToHost, stream_.s), "hipMemcpyAsync");
     sync();
+    return *hNorm_;
+}
+
+void HipGridData::readNormBegin()
+{
+    if (trace) return;
+    check((int)hipMemcpyAsync(hNorm_, dNorm_, sizeof(double), hipMemcpyDeviceToHost, stream_.s), "hipMemcpyAsync");
+    check((int)hipEventRecord(evNorm_, stream_.s), "hipEventRecord");
+}
+
+double HipGridData::readNormEnd()
+{
+    if (trace) return 1.0;
+    // distributed: a bounded wait that also polls the communicator's error state (gs_comm.hpp)
+    if (comm_ && comm_->size() > 1) comm_->syncEvent(evNorm_);
+    else check((int)hipEventSynchronize(evNorm_), "hipEventSynchronize");
     return *hNorm_;
 }
 
@@ -467,22 +485,27 @@ void HipSolver::solve(HipGridData& grid)
     const double initialResidual = spec ? speculativeSweep(grid, &pending) : compResidual(grid, 0, false, true);
     if (history) history->push_back(initialResidual);
     if (print) std::cout << "Inital residual: " << initialResidual << '\n';
-
-    for (std::size_t i = 0; i < grid.maxiter; i++) {
-        if (print) Timer::start();
-        const double res = spec ? vcycleSpeculative(grid, &pending) : vcycle(grid);
+    if (print) Timer::start();
+    auto onNorm = [&](std::size_t i, double res) {
         if (history) history->push_back(res);
         if (print) {
             std::cout << "iter: " << i << " residual: " << res << ' ';
-            Timer::stop();
+            Timer::stop(); // "Took Nms": from the previous norm to this one (the cycles overlap)
+            Timer::start();
         }
-        if (res <= initialResidual / (1.0 / grid.tol)) return;
+        return res <= initialResidual / (1.0 / grid.tol);
+    };
+    if (spec) {
+        runCycles(grid, &pending, grid.maxiter, onNorm);
+    } else {
+        for (std::size_t i = 0; i < grid.maxiter; i++)
+            if (onNorm(i, vcycle(grid))) break;
     }
 }
 
 // Global ||.|| from this rank's per-block partials: fixed-order sums per rank, then over ranks in
 // rank order, so every rank (and every run) gets the same bits.
-double HipSolver::finishNorm(HipGridData& grid, int64_t nparts)
+double HipSolver::finishNorm(HipGridData& grid, int64_t nparts, bool wait)
 {
     const hipStream_t s = grid.stream();
     if (grid.trace) {
@@ -496,7 +519,9 @@ double HipSolver::finishNorm(HipGridData& grid, int64_t nparts)
     } else {
         check(gs_sumsq_finish(grid.partials(), nparts, grid.dNorm(), 0, s), "gs_sumsq_finish");
     }
-    return grid.readNorm();
+    if (wait) return grid.readNorm();
+    grid.readNormBegin();
+    return std::nan("");
 }
 
 // compResidual (src/cpu/CpuSolver.cpp:45-83): r is written only when a restriction consumes it,
@@ -634,7 +659,7 @@ void HipSolver::coarseCycle(HipGridData& grid, std::size_t from)
 // The first pre-smoothing step of the next cycle, run into vAlt (v untouched) with the norm of the
 // residual of v: a fused pair when level 0 smooths in pairs and pre-smoothing has two sweeps, else
 // one sweep. *sweeps = how many sweeps vAlt holds.
-double HipSolver::speculativeSweep(HipGridData& grid, int* sweeps)
+double HipSolver::speculativeSweep(HipGridData& grid, int* sweeps, bool wait)
 {
     auto& L = grid.getLevel(0);
     const hipStream_t s = grid.stream();
@@ -664,7 +689,7 @@ double HipSolver::speculativeSweep(HipGridData& grid, int* sweeps)
     }
     if (sweeps) *sweeps = pair ? 2 : 1;
     grid.clock.mark(s, 0, false); // closes the caller's segment before the norm's host sync
-    return finishNorm(grid, n);
+    return finishNorm(grid, n, wait);
 }
 
 void HipSolver::restrict(HipGridData& grid, const DeviceField& src, std::size_t srcLevel, DeviceField& dst)
@@ -674,14 +699,65 @@ void HipSolver::restrict(HipGridData& grid, const DeviceField& src, std::size_t 
 
 double HipSolver::vcycle(HipGridData& grid) { return vcycleSpeculative(grid, nullptr); }
 
-// src/cpu/CpuSolver.cpp:85-139
-double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
+// The up-leg of level i-1 from level i (CpuSolver.cpp:121-135): v^(i-1) += P v^i, post-smoothing.
+void HipSolver::upLeg(HipGridData& grid, std::size_t i)
+{
+    const hipStream_t s = grid.stream();
+    auto& C = grid.getLevel(i);
+    auto& F = grid.getLevel(i - 1);
+    grid.clock.mark(s, (int)(i - 1), true);
+    materialize(grid, i); // only if the level had no sweep at all
+    static const bool noFusedPro = std::getenv("GS_NO_FUSED_PROLONG") != nullptr;
+    if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && proWorthIt(grid, i - 1) && proSlabOk(grid, i - 1) &&
+        gs_jacobi_sweep2_prolong_supported(&grid.stencilAbi, &F.geom, (int)grid.mode)) {
+        // the first two post-smoothing sweeps of v^h + P v^2h in one pass (the corrected
+        // iterate is never stored), then the remaining ones. On a Z-slab each rank corrects its
+        // ghost planes itself, from the coarse planes under them, and the pair's outermost planes
+        // go first so that their exchange overlaps the interior (as in jacobi())
+        materialize(grid, i - 1);
+        const int64_t nz = F.geom.nz;
+        if (!(F.distributed && grid.nranks() > 1)) {
+            proPlanes(grid, F, C, 1, nz, s);
+        } else if (grid.overlapHalo && nz >= 5) {
+            const int64_t zt = nz % 2 == 0 ? nz - 1 : nz - 2; // odd start: 2 or 3 top planes
+            const hipStream_t bs = forkBoundary(grid);
+            proPlanes(grid, F, C, 1, 2, bs);
+            proPlanes(grid, F, C, zt, nz, bs);
+            forkComm(grid);
+            grid.halo(F, F.vAlt, grid.commStream(), grid.vDepth(F));
+            joinComm(grid, false);
+            proPlanes(grid, F, C, 3, zt - 1, s);
+            joinComm(grid, true);
+        } else {
+            proPlanes(grid, F, C, 1, nz, s);
+            grid.halo(F, F.vAlt, s, grid.vDepth(F));
+        }
+        F.v.swap(F.vAlt);
+        if (grid.trace) grid.rec("swap", {{"L", (long long)(i - 1)}});
+        F.vZero = false;
+        jacobi(grid, i - 1, grid.postSmoothing - 2);
+        grid.clock.mark(s, (int)(i - 1), false);
+        return;
+    }
+    // v^h += P (v^2h [- restV^2h])   (CpuSolver.cpp:121-132, interpolate + v += e fused)
+    if (grid.trace)
+        grid.rec("prolongadd", {{"L", (long long)(i - 1)}, {"sub", grid.mode == GridParams::NONLINEAR}});
+    else
+        check(gs_prolong_add(C.v.data(), grid.mode == GridParams::NONLINEAR ? C.restV.data() : nullptr, &C.geom,
+                             F.v.data(), &F.geom, s),
+              "gs_prolong_add");
+    grid.halo(F, F.v, s, grid.vDepth(F));
+    jacobi(grid, i - 1, grid.postSmoothing);
+    grid.clock.mark(s, (int)(i - 1), false);
+}
+
+// src/cpu/CpuSolver.cpp:85-139, in two halves (see gs_grid.hpp)
+void HipSolver::cycleDown(HipGridData& grid, int* pending)
 {
     const std::size_t nl = grid.numLevels();
     const hipStream_t s = grid.stream();
     // levels lc.. run as one gs_coarse_cycle launch (lc == nl: none); the host loops descend to lc
     const std::size_t lc = grid.coarseFrom, last = std::min(lc, nl - 1);
-    const auto tWall = std::chrono::steady_clock::now();
     for (std::size_t i = 0; i < last; i++) {
         grid.clock.mark(s, (int)i, true);
         std::size_t pre = grid.preSmoothing;
@@ -765,63 +841,31 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
     if (lc < nl) coarseCycle(grid, lc);
     else jacobi(grid, nl - 1, grid.preSmoothing + grid.postSmoothing); // coarsest "solve"
     grid.clock.mark(s, (int)std::min(lc, nl - 1), false);
-    for (std::size_t i = last; i > 0; i--) {
-        auto& C = grid.getLevel(i);
-        auto& F = grid.getLevel(i - 1);
-        grid.clock.mark(s, (int)(i - 1), true);
-        materialize(grid, i); // only if the level had no sweep at all
-        static const bool noFusedPro = std::getenv("GS_NO_FUSED_PROLONG") != nullptr;
-        if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && proWorthIt(grid, i - 1) && proSlabOk(grid, i - 1) &&
-            gs_jacobi_sweep2_prolong_supported(&grid.stencilAbi, &F.geom, (int)grid.mode)) {
-            // the first two post-smoothing sweeps of v^h + P v^2h in one pass (the corrected
-            // iterate is never stored), then the remaining ones. On a Z-slab each rank corrects its
-            // ghost planes itself, from the coarse planes under them, and the pair's outermost planes
-            // go first so that their exchange overlaps the interior (as in jacobi())
-            materialize(grid, i - 1);
-            const int64_t nz = F.geom.nz;
-            if (!(F.distributed && grid.nranks() > 1)) {
-                proPlanes(grid, F, C, 1, nz, s);
-            } else if (grid.overlapHalo && nz >= 5) {
-                const int64_t zt = nz % 2 == 0 ? nz - 1 : nz - 2; // odd start: 2 or 3 top planes
-                const hipStream_t bs = forkBoundary(grid);
-                proPlanes(grid, F, C, 1, 2, bs);
-                proPlanes(grid, F, C, zt, nz, bs);
-                forkComm(grid);
-                grid.halo(F, F.vAlt, grid.commStream(), grid.vDepth(F));
-                joinComm(grid, false);
-                proPlanes(grid, F, C, 3, zt - 1, s);
-                joinComm(grid, true);
-            } else {
-                proPlanes(grid, F, C, 1, nz, s);
-                grid.halo(F, F.vAlt, s, grid.vDepth(F));
-            }
-            F.v.swap(F.vAlt);
-            if (grid.trace) grid.rec("swap", {{"L", (long long)(i - 1)}});
-            F.vZero = false;
-            jacobi(grid, i - 1, grid.postSmoothing - 2);
-            grid.clock.mark(s, (int)(i - 1), false);
-            continue;
-        }
-        // v^h += P (v^2h [- restV^2h])   (CpuSolver.cpp:121-132, interpolate + v += e fused)
-        if (grid.trace)
-            grid.rec("prolongadd", {{"L", (long long)(i - 1)}, {"sub", grid.mode == GridParams::NONLINEAR}});
-        else
-            check(gs_prolong_add(C.v.data(), grid.mode == GridParams::NONLINEAR ? C.restV.data() : nullptr, &C.geom,
-                                 F.v.data(), &F.geom, s),
-                  "gs_prolong_add");
-        grid.halo(F, F.v, s, grid.vDepth(F));
-        jacobi(grid, i - 1, grid.postSmoothing);
-        grid.clock.mark(s, (int)(i - 1), false);
-    }
+    for (std::size_t i = last; i > 1; i--) upLeg(grid, i);
+}
+
+double HipSolver::cycleUp0(HipGridData& grid, int* pending, bool wait)
+{
+    const std::size_t nl = grid.numLevels();
+    const hipStream_t s = grid.stream();
+    if (std::min(grid.coarseFrom, nl - 1) >= 1) upLeg(grid, 1);
     // the closing norm: the next cycle's first pre-smoothing step (speculative) or a residual pass
     grid.clock.mark(s, 0, true);
     double res;
     if (pending && speculationEnabled(grid)) {
-        res = speculativeSweep(grid, pending); // closes the segment before its host sync
+        res = speculativeSweep(grid, pending, wait); // closes the segment before its host sync
     } else {
         res = compResidual(grid, 0, false, true);
         grid.clock.mark(s, 0, false); // after the norm's host sync: over-counts by the sync latency
     }
+    return res;
+}
+
+double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
+{
+    const auto tWall = std::chrono::steady_clock::now();
+    cycleDown(grid, pending);
+    const double res = cycleUp0(grid, pending, true);
     if (grid.clock.on) {
         grid.clock.collect();
         grid.clock.cycles++;
@@ -830,8 +874,47 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
     return res;
 }
 
-// ---------------------------------------------------------------------------------------------
-// src/cpu/NewtonSolver.cpp:10-44
+// Overlapping cycle i+1's cycleDown with the wait for cycle i's norm is exact only if that work
+// leaves level 0's iterate alone: every pre-smoothing sweep is the speculative step's (pre ==
+// pending), level 0 is not part of the coarse-cycle launch, and no per-level clock is running.
+bool HipSolver::pipelinable(const HipGridData& grid, int pending)
+{
+    static const bool off = std::getenv("GS_NO_PIPELINE") != nullptr;
+    return !off && !grid.clock.on && speculationEnabled(grid) && pending > 0 &&
+           (std::size_t)pending == grid.preSmoothing && std::min(grid.coarseFrom, grid.numLevels() - 1) >= 1;
+}
+
+std::size_t HipSolver::runCycles(HipGridData& grid, int* pending, std::size_t maxCycles,
+                                 const std::function<bool(std::size_t, double)>& onNorm)
+{
+    // (cycle-invariant: every closing speculative step leaves the same number of sweeps pending)
+    const bool pipe = pipelinable(grid, *pending);
+    bool downDone = false; // this cycle's cycleDown was enqueued during the previous cycle's wait
+    for (std::size_t i = 0; i < maxCycles; i++) {
+        if (!pipe) {
+            if (onNorm(i, vcycleSpeculative(grid, pending))) return i + 1;
+            continue;
+        }
+        if (!downDone) cycleDown(grid, pending);
+        cycleUp0(grid, pending, false); // cycle i's closing norm in flight; *pending = its sweeps
+        const int next = *pending;
+        const bool ahead = i + 1 < maxCycles;
+        if (ahead) cycleDown(grid, pending); // adopts the speculative sweeps: *pending = 0
+        const double res = grid.readNormEnd();
+        if (onNorm(i, res)) {
+            if (ahead) { // undo the adoption: level 0 holds cycle i's iterate, vAlt the speculation
+                auto& L0 = grid.getLevel(0);
+                L0.v.swap(L0.vAlt);
+                if (grid.trace) grid.rec("swap", {{"L", 0}});
+                *pending = next;
+            }
+            return i + 1;
+        }
+        downDone = ahead;
+    }
+    return maxCycles;
+}
+
 void NewtonSolver::solve(HipGridData& grid)
 {
     auto& L0 = grid.getLevel(0);

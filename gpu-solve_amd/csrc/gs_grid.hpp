@@ -17,6 +17,7 @@
 #include <initializer_list>
 #include <memory>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "gpusolve_hip.h"
@@ -130,6 +131,10 @@ public:
     double* dNorm() const { return dNorm_; }
     double* dRankSums() const { return dRankSums_; }
     double readNorm(); // async D2H of dNorm + stream sync: the one host sync per V-cycle
+    // the same in two halves: the D2H copy + an event now, the (bounded) wait for the event later, so
+    // that more work can be enqueued in between
+    void readNormBegin();
+    double readNormEnd();
     void sync();       // stream sync (bounded, error-polling when distributed over RCCL)
 
     // ghost planes of a distributed level's field (no-op otherwise); depth 2 where possible for
@@ -151,7 +156,7 @@ private:
     double* dNorm_ = nullptr;
     double* dRankSums_ = nullptr;
     double* hNorm_ = nullptr;
-    hipEvent_t evA_ = nullptr, evB_ = nullptr, evC_ = nullptr;
+    hipEvent_t evA_ = nullptr, evB_ = nullptr, evC_ = nullptr, evNorm_ = nullptr;
     std::vector<double> dryParts_;
     friend class HipSolver;
 };
@@ -169,14 +174,30 @@ public:
     // or a fused pair), run into vAlt without swapping; *pending = how many sweeps vAlt holds (0:
     // none), and the next cycle adopts them.
     static double vcycleSpeculative(HipGridData& grid, int* pending);
-    // level-0 sweep or pair v -> vAlt (no swap) + norm of f - A v; *sweeps = sweeps run
-    static double speculativeSweep(HipGridData& grid, int* sweeps);
+    // vcycleSpeculative in two halves: cycleDown enqueues everything that leaves level 0's iterate
+    // untouched (adopting the pending speculative sweeps, every down-leg, the coarse end, the up-legs
+    // of levels >= 1); cycleUp0 enqueues level 0's up-leg and the closing norm, and waits for the norm
+    // only if `wait` (else the caller collects it with grid.readNormEnd()).
+    static void cycleDown(HipGridData& grid, int* pending);
+    static double cycleUp0(HipGridData& grid, int* pending, bool wait);
+    // Up to maxCycles V-cycles with the host's wait for cycle i's norm overlapped with cycle i+1's
+    // cycleDown (when pipelinable): onNorm(i, res) gets each closing norm in order and returns true
+    // to stop — the early-enqueued work then only wrote coarse levels and scratch, and the adoption
+    // of the speculative level-0 sweeps is undone, so level 0 holds cycle i's iterate exactly as
+    // without the overlap. *pending: the speculative sweeps vAlt holds on entry and on return.
+    static std::size_t runCycles(HipGridData& grid, int* pending, std::size_t maxCycles,
+                                 const std::function<bool(std::size_t, double)>& onNorm);
+    static bool pipelinable(const HipGridData& grid, int pending);
+    static void upLeg(HipGridData& grid, std::size_t level); // level-1 -> level-1 up-leg (from `level`)
+    // level-0 sweep or pair v -> vAlt (no swap) + norm of f - A v; *sweeps = sweeps run; !wait: the
+    // norm is left in flight (grid.readNormEnd())
+    static double speculativeSweep(HipGridData& grid, int* sweeps, bool wait = true);
     static bool speculationEnabled(const HipGridData& grid);
     static void jacobi(HipGridData& grid, std::size_t level, std::size_t sweeps);
     static void materialize(HipGridData& grid, std::size_t level); // store a pending v = 0
     // the V-cycle below level `from` (its f set) in one gs_coarse_cycle launch
     static void coarseCycle(HipGridData& grid, std::size_t from);
-    static double finishNorm(HipGridData& grid, int64_t nparts);
+    static double finishNorm(HipGridData& grid, int64_t nparts, bool wait = true);
     static hipStream_t forkBoundary(HipGridData& grid);
     static void forkComm(HipGridData& grid);
     static void joinComm(HipGridData& grid, bool wait);
