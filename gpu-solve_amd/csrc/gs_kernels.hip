@@ -15,6 +15,10 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "gpusolve_hip.h"
 
 namespace {
@@ -2260,6 +2264,59 @@ bool xh_enabled()
 // blocks (4..64 planes: at 512^3, 64-plane chunks measured 5-8% faster than 32 — fewer re-read
 // chunk-boundary planes). Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU);
 // *y2: the k_tb2y whole-row shape, *xh: the k_tb2y column-block shape (neither: k_tb2).
+// Blocks of `threads` threads kernel `fn` keeps resident on the whole GPU (occupancy x CUs, cached).
+int64_t resident_blocks(const void* fn, int threads)
+{
+    static std::mutex m;
+    static std::map<std::pair<const void*, int>, int64_t> cache;
+    std::lock_guard<std::mutex> lk(m);
+    const auto key = std::make_pair(fn, threads);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int per = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, 0) != hipSuccess || per < 1) per = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    (void)hipGetLastError();
+    return cache[key] = (int64_t)per * cus;
+}
+
+// Round-aware chunking for levels whose grid is a few rounds of resident blocks: the chunk length c
+// in [lo, hi] (even if `even`) maximising (blocks / (rounds x capacity)) x c / (c + halo) — whole
+// rounds, long chunks (each recomputes ~halo planes) — among those that still fill the GPU.
+// GS_FIT_ROUNDS=0 keeps the callers' rules (A/B). Returns 0 for "keep".
+int fit_chunk(int64_t tiles, int64_t planes, int64_t cap, int lo, int hi, bool even, double halo)
+{
+    static const bool off = getenv("GS_FIT_ROUNDS") && atoi(getenv("GS_FIT_ROUNDS")) == 0;
+    if (off || tiles < 1 || planes < 1 || cap < 1) return 0;
+    double best = -1.0;
+    int bc = 0;
+    for (int c = lo; c <= hi; c++) {
+        if (even && (c & 1)) continue;
+        const int64_t blocks = tiles * ((planes + c - 1) / c);
+        if (blocks < cap && bc != 0) continue; // would leave CUs idle where a shorter chunk does not
+        const int64_t rounds = (blocks + cap - 1) / cap;
+        const double score = (double)blocks / (double)(rounds * cap) * c / (c + halo);
+        if (score > best) {
+            best = score;
+            bc = c;
+        }
+    }
+    return bc;
+}
+
+// refit a plan's z-chunk (grid.y) for kernel `fn` at `threads` threads
+template <class K>
+void refit_chunks(K* fn, int threads, int64_t planes, int lo, int hi, bool even, double halo, int* zc, dim3* g)
+{
+    const int c = fit_chunk(g->x, planes, resident_blocks((const void*)fn, threads), lo, hi, even, halo);
+    if (c > 0) {
+        *zc = c;
+        g->y = (unsigned)((planes + c - 1) / c);
+    }
+}
+
 int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
              int mode = GS_LINEAR, bool* xh = nullptr)
 {
@@ -2550,7 +2607,13 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
 #define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
-#define GS_TBY1(M, Z, U) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M), false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+    // zero-iterate pairs (the first sweep of a coarse level, v = 0: the lightest variant, three blocks per
+    // CU) below 2^26 points: chunks fitted to whole rounds of resident blocks (256^3: 61 vs 71 us; the
+    // same rule measured no better for the other pairs and worse for k_rr2, r02 tools/fit_session.sh)
+    const bool refit = !v_in && !partials && (int64_t)L->nx * L->ny * L->nz < ((int64_t)1 << 26);
+#define GS_TBY1(M, Z, U) do { \
+        if (refit) refit_chunks(&k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M), false, U>, (int)(b.x * b.y * b.z), nz, 4, 64, true, 2.0, &zc, &g); \
+        hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M), false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0); } while (0)
 #define GS_TBY(M, Z) do { if (k.unit) GS_TBY1(M, Z, true); else GS_TBY1(M, Z, false); } while (0)
 #define GS_TBX1(M, Z, P, U) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
 #define GS_TBX(M, Z, P) do { if (k.unit) GS_TBX1(M, Z, P, true); else GS_TBX1(M, Z, P, false); } while (0)
