@@ -169,3 +169,29 @@ def test_executable_metrics_line(tmp_path):
     pat = re.compile(r"iter: (\d+) residual: ([\d\.e-]+) Took (\d+)ms")
     assert len(pat.findall(out.stdout)) == case["config"]["maxiter"]
     assert not pat.search(last)
+
+
+@pytest.mark.parametrize("mode,pre,dims", [(0, 2, (64, 64, 64)), (0, 1, (40, 36, 33)), (1, 2, (63, 63, 63))])
+def test_early_stop_level0_exact(mode, pre, dims):
+    """A tol that stops the loop after the 3rd V-cycle: by then the 4th cycle's down-leg is already
+    enqueued (HipSolver::runCycles overlaps it with the wait for the 3rd norm), so the stop must undo
+    the adoption of the speculative sweeps. Level 0's iterate and the history must be the oracle's
+    (bit-identical fields in LINEAR mode)."""
+    full = O.Grid(dims, mode=mode, maxiter=8, pre=pre, post=2)
+    h = full.solve()
+    tol = (h[2] * h[3]) ** 0.5 / h[0]  # between the 2nd and 3rd cycle's ratios
+    og = O.Grid(dims, mode=mode, maxiter=8, tol=tol, pre=pre, post=2)
+    oh = og.solve()
+    assert len(oh) == 4
+    p = gsv.GridParams(maxiter=8, tol=tol, gridDim=dims, mode=mode, preSmoothing=pre, postSmoothing=2)
+    with gsv.HipGridData(p) as g:
+        hist = gsv.HipSolver.solve(g)
+        v = g.field(0, "v")
+    assert len(hist) == 4
+    ref = og.field(0, "v")
+    if mode == 0:
+        np.testing.assert_array_equal(v, ref)
+    else:
+        assert np.abs(v - ref).max() <= 1e-10 * np.abs(ref).max()
+    for a, b in zip(hist, oh):
+        assert rel(a, b) < (1e-12 if mode == 0 else 1e-9)
