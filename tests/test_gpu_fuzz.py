@@ -1,0 +1,70 @@
+"""Seeded random solves against the CPU oracle (pinned to the reference, tests/test_oracle_golden.py):
+grid shapes from 2 to 70 points per axis (power-of-two and odd, flat and long), all three modes,
+0..3 pre / post sweeps, omega and gamma drawn from the reference's usable range. Level 0's iterate
+must be bit-identical in LINEAR mode and within 1e-10 (ocml vs glibc exp) otherwise; the histories
+within 1e-12 / 1e-9. Every case exercises a different mix of fused pairs, single sweeps, zero-iterate
+sweeps, one-point small-level kernels, the coarse-cycle launch and the overlapped solve loop."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import gpusolve as gsv  # noqa: E402
+import oracle as O  # noqa: E402
+from conftest import rel  # noqa: E402
+
+
+CANON = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
+
+
+def cases(n=150, seed=20261016):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        dims = tuple(int(rng.choice([rng.integers(2, 71), 2 ** rng.integers(1, 7)])) for _ in range(3))
+        mode = int(rng.integers(0, 3))
+        pre, post = int(rng.integers(0, 4)), int(rng.integers(0, 4))
+        if pre + post == 0:
+            post = 1
+        omega = float(np.round(rng.uniform(0.5, 0.95), 3))
+        gamma = float(np.round(rng.uniform(0.0, 1.5), 3)) if mode else 1.0
+        # one case in five: a non-unit stencil (general stencil sums); one in ten: entries permuted
+        # (the generic kernels), keeping the weights attached to their offsets
+        values, offsets = [6.0, -1, -1, -1, -1, -1, -1], list(CANON)
+        u = rng.uniform()
+        if u < 0.2:
+            values = [float(np.round(6 + rng.uniform(0, 2), 2))] + [float(np.round(-rng.uniform(0.8, 1.2), 2))
+                                                                    for _ in range(6)]
+        if u < 0.1:
+            perm = [0] + list(1 + rng.permutation(6))
+            values, offsets = [values[j] for j in perm], [offsets[j] for j in perm]
+        out.append((i, dims, mode, pre, post, omega, gamma, tuple(values), tuple(offsets)))
+    return out
+
+
+@pytest.mark.parametrize("case", cases(), ids=lambda c: f"c{c[0]}-{'x'.join(map(str, c[1]))}-m{c[2]}-{c[3]}+{c[4]}")
+def test_random_solve_vs_oracle(case):
+    _, dims, mode, pre, post, omega, gamma, values, offsets = case
+    maxiter = 2
+    og = O.Grid(dims, mode=mode, maxiter=maxiter, omega=omega, gamma=gamma, pre=pre, post=post,
+                stencil=O.Stencil.make(values, offsets))
+    oh = og.solve()
+    name = "newtonV" if mode == 2 else "v"
+    ref = og.field(0, name).copy()
+    p = gsv.GridParams(maxiter=maxiter, tol=0.0, gridDim=dims, mode=mode, preSmoothing=pre, postSmoothing=post,
+                       omega=omega, gamma=gamma, stencil=gsv.Stencil(list(values), list(offsets)))
+    with gsv.HipGridData(p) as g:
+        hist = gsv.NewtonSolver.solve(g) if mode == 2 else gsv.HipSolver.solve(g)
+        v = g.field(0, name)
+    assert len(hist) == len(oh)
+    fin = np.isfinite(ref)
+    assert np.array_equal(fin, np.isfinite(v)), "non-finite values at different points"
+    if mode == 0:
+        assert v.tobytes() == ref.tobytes() or np.array_equal(v, ref, equal_nan=True)
+    else:
+        scale = max(np.abs(ref[fin]).max(), 1e-300) if fin.any() else 1.0
+        assert np.abs(v[fin] - ref[fin]).max() <= 1e-10 * scale
+    for a, b in zip(hist, oh):
+        if np.isfinite(a) or np.isfinite(b):
+            assert rel(a, b) < (1e-12 if mode == 0 else 1e-9), (a, b)
