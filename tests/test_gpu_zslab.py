@@ -94,3 +94,32 @@ def test_fused_prolong_slabs_match_single_gpu(dims, nranks, min_points, pre, pos
     for a, b in zip(h, ref_h):
         assert rel(a, b) < 1e-12, (a, b)
     np.testing.assert_array_equal(v[:, :, 1:-1], ref_v[:, :, 1:-1])
+
+
+def zslab_cases(n=30, seed=7):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        nranks = int(rng.integers(2, 6))
+        dims = (int(rng.integers(8, 200)), int(rng.integers(8, 300)), int(rng.integers(4 * nranks, 140)))
+        mode = int(rng.choice([0, 0, 1, 2]))
+        pre, post = int(rng.integers(1, 4)), int(rng.integers(1, 4))
+        min_points = int(rng.choice([-1, 0, 4096]))
+        out.append((i, dims, nranks, mode, pre, post, min_points))
+    return out
+
+
+@pytest.mark.parametrize("case", zslab_cases(), ids=lambda c: f"z{c[0]}-{'x'.join(map(str, c[1]))}-r{c[2]}-m{c[3]}")
+def test_zslab_random_vs_single(case):
+    """Seeded random shapes, rank counts (2-5, uneven slabs), modes, smoothing counts and agglomeration
+    thresholds: the loopback Z-slab solve against the single-GPU one, fields bit for bit."""
+    _, dims, nranks, mode, pre, post, min_points = case
+    p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=mode, preSmoothing=pre, postSmoothing=post)
+    h1, v1 = single(p, 0, True)
+    hn, vn = loopback(p, nranks, min_points, 0, True)
+    a, b = np.ascontiguousarray(vn[:, :, 1:-1]), np.ascontiguousarray(v1[:, :, 1:-1])
+    assert a.tobytes() == b.tobytes() or np.array_equal(a, b, equal_nan=True)
+    assert len(hn) == len(h1)
+    for a, b in zip(hn, h1):
+        if np.isfinite(a) or np.isfinite(b):
+            assert rel(a, b) < 1e-12
