@@ -161,6 +161,27 @@ def test_gloo_replay_of_driver_schedule(dims, world, min_points, pre, post):
         assert {"pair", "pro", "resrestrict", "halo", "gather", "coarse"} <= ops_seen, ops_seen
 
 
+def _random_replay_cases(n=4, seed=11):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        world = int(rng.integers(2, 4))
+        dims = (int(rng.integers(8, 48)), int(rng.integers(8, 200)), int(rng.integers(6 * world, 72)))
+        out.append((dims, world, int(rng.choice([-1, 0, 4096])), int(rng.integers(1, 4)), int(rng.integers(1, 4))))
+    return out
+
+
+@pytest.mark.parametrize("dims,world,min_points,pre,post", _random_replay_cases())
+def test_gloo_replay_random_shapes(dims, world, min_points, pre, post):
+    """Seeded random shapes, rank counts, thresholds and smoothing counts through the same replay."""
+    got, ref_v, hists, ref_hist, _ = _replay(dims, world, min_points, pre, post)
+    for hist in hists:
+        assert len(hist) == len(ref_hist)
+        for a, b in zip(hist, ref_hist):
+            assert abs(a - b) <= 1e-12 * abs(b), (a, b)
+    np.testing.assert_array_equal(got, ref_v)
+
+
 @pytest.mark.parametrize("mutation", ["halo", "depth", "range"])
 def test_gloo_replay_catches_a_broken_schedule(mutation):
     """The same replay with one deliberate schedule defect must NOT reproduce the oracle."""
