@@ -270,9 +270,20 @@ const char* HipGridData::fieldName(const LevelData& L, const DeviceField& f)
     return "?";
 }
 
+// Trace mode has no device: the norms are placeholders (1.0, never a stop), except that
+// GS_TRACE_STOP_AFTER=k makes the norm closing cycle k read 0.0, so that the loop stops there and the
+// schedule records an early stop (tests replay it: the undo of the overlapped next cycle's adoption).
+double HipGridData::traceNorm()
+{
+    const char* e = std::getenv("GS_TRACE_STOP_AFTER"); // read per call: tests switch it
+    const long stopAfter = e ? std::strtol(e, nullptr, 10) : -1;
+    const long read = traceNorms_++; // 0: the initial norm, i + 1: cycle i's closing norm
+    return (stopAfter >= 0 && read == stopAfter + 1) ? 0.0 : 1.0;
+}
+
 double HipGridData::readNorm()
 {
-    if (trace) return 1.0; // (no device: the traced norms are placeholders)
+    if (trace) return traceNorm();
     check((int)hipMemcpyAsync(hNorm_, dNorm_, sizeof(double), hipMemcpyDeviceToHost, stream_.s), "hipMemcpyAsync");
     sync();
     return *hNorm_;
@@ -287,7 +298,7 @@ void HipGridData::readNormBegin()
 
 double HipGridData::readNormEnd()
 {
-    if (trace) return 1.0;
+    if (trace) return traceNorm();
     // distributed: a bounded wait that also polls the communicator's error state (gs_comm.hpp)
     if (comm_ && comm_->size() > 1) comm_->syncEvent(evNorm_);
     else check((int)hipEventSynchronize(evNorm_), "hipEventSynchronize");
@@ -510,7 +521,7 @@ double HipSolver::finishNorm(HipGridData& grid, int64_t nparts, bool wait)
     const hipStream_t s = grid.stream();
     if (grid.trace) {
         grid.rec("norm", {{"allgather", grid.nranks() > 1 && grid.getLevel(0).distributed}});
-        return grid.readNorm();
+        return wait ? grid.readNorm() : std::nan(""); // (!wait: readNormEnd reads it)
     }
     if (grid.nranks() > 1 && grid.getLevel(0).distributed) {
         check(gs_sumsq_finish(grid.partials(), nparts, grid.dNorm(), 1, s), "gs_sumsq_finish");

@@ -158,6 +158,8 @@ private:
     double* hNorm_ = nullptr;
     hipEvent_t evA_ = nullptr, evB_ = nullptr, evC_ = nullptr, evNorm_ = nullptr;
     std::vector<double> dryParts_;
+    long traceNorms_ = 0;
+    double traceNorm();
     friend class HipSolver;
 };
 

@@ -80,9 +80,11 @@ def _free_port():
     return p
 
 
-def _replay_worker(rank, world, port, params, min_points, q, mutation=None):
+def _replay_worker(rank, world, port, params, min_points, q, mutation=None, stop_after=None):
     """One gloo rank: replay this rank's schedule from the driver (gs_zslab_schedule) on its slab."""
     import zslab_exec as X
+    if stop_after is not None:  # the traced loop stops after cycle `stop_after` (HipGridData::traceNorm)
+        os.environ["GS_TRACE_STOP_AFTER"] = str(stop_after)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -113,13 +115,14 @@ REPLAY_CASES = [
 ]
 
 
-def _replay(dims, world, min_points, pre, post, cycles=2, mutation=None):
+def _replay(dims, world, min_points, pre, post, cycles=2, mutation=None, stop_after=None):
     import gpusolve as gsv
     params = gsv.GridParams(maxiter=cycles, tol=0.0, gridDim=dims, mode=0, preSmoothing=pre, postSmoothing=post)
+    ran = cycles if stop_after is None else stop_after + 1
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_replay_worker, args=(r, world, port, params, min_points, q, mutation))
+    procs = [ctx.Process(target=_replay_worker, args=(r, world, port, params, min_points, q, mutation, stop_after))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -130,7 +133,7 @@ def _replay(dims, world, min_points, pre, post, cycles=2, mutation=None):
         assert r[1] is not None, r[4]
     for p in procs:
         assert p.exitcode == 0
-    og = O.Grid(dims, mode=O.LINEAR, maxiter=cycles, pre=pre, post=post)
+    og = O.Grid(dims, mode=O.LINEAR, maxiter=ran, pre=pre, post=post)
     ref_hist = og.solve()
     ref_v = og.field(0, "v").copy()  # (a view into the oracle grid, which dies with og)
     got = np.full_like(ref_v, np.nan)
@@ -177,6 +180,20 @@ def test_gloo_replay_random_shapes(dims, world, min_points, pre, post):
     got, ref_v, hists, ref_hist, _ = _replay(dims, world, min_points, pre, post)
     for hist in hists:
         assert len(hist) == len(ref_hist)
+        for a, b in zip(hist, ref_hist):
+            assert abs(a - b) <= 1e-12 * abs(b), (a, b)
+    np.testing.assert_array_equal(got, ref_v)
+
+
+@pytest.mark.parametrize("stop_after", [0, 1])
+def test_gloo_replay_early_stop(stop_after):
+    """A loop that stops after cycle `stop_after` of 4 while the next cycle's down-leg is already
+    enqueued (HipSolver::runCycles): the recorded schedule contains that down-leg and the undo of the
+    adoption of the speculative pair; replayed, level 0 must equal the oracle's after stop_after + 1
+    cycles, bit for bit."""
+    got, ref_v, hists, ref_hist, _ = _replay((64, 256, 64), 2, -1, 2, 2, cycles=4, stop_after=stop_after)
+    for hist in hists:
+        assert len(hist) == len(ref_hist) == stop_after + 2
         for a, b in zip(hist, ref_hist):
             assert abs(a - b) <= 1e-12 * abs(b), (a, b)
     np.testing.assert_array_equal(got, ref_v)
