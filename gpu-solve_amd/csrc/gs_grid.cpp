@@ -774,6 +774,7 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
         std::size_t pre = grid.preSmoothing;
         if (i == 0 && pending && *pending > 0 && pre >= (std::size_t)*pending) {
             grid.getLevel(0).v.swap(grid.getLevel(0).vAlt); // adopt the speculative first sweep(s)
+            grid.getLevel(0).vZero = false;
             if (grid.trace) grid.rec("swap", {{"L", 0}});
             pre -= (std::size_t)*pending;
             *pending = 0;
@@ -947,8 +948,9 @@ void NewtonSolver::solve(HipGridData& grid)
         if (print) Timer::start();
         // The reference recomputes compF here (NewtonSolver.cpp:21); f^0 already holds exactly that
         // value from the previous compF and nothing wrote it since, so the pass is skipped.
-        if (grid.trace) grid.rec("zero", {{"L", 0}}, "v");
-        L0.v.zero(s);
+        // v = 0 (NewtonSolver.cpp:22), not stored: the inner solve's first (speculative) sweep is a
+        // zero-iterate kernel that reads no v; anything else that reads v materializes it first
+        L0.vZero = true;
         findError(grid);
         const double res = compF(grid);
         if (history) history->push_back(res);
