@@ -188,6 +188,50 @@ def single_sweep_timing(grid, dims, k):
             "achieved_GBps": round(gbps, 1), "frac": round(gbps / PEAK_GBPS, 4)}
 
 
+def vcycle_level0_kernels(grid, k):
+    """The V-cycle's two other level-0 passes timed alone with HIP events on the grid's own fields
+    (after the V-cycles: level 1's f is scratch, the prolongation pair writes a spare buffer): the
+    fused residual + restriction (16 B/point read + 1 B coarse write) and the prolongation pair (24 B
+    + 1 B coarse read). Algorithmic bytes per point / average launch time, as `roofline`."""
+    import ctypes as C
+    from gpusolve.devfield import DevField
+    kl, drv = gsv.kernels(), gsv.driver()
+    L0, L1 = grid.getLevel(0).geom, grid.getLevel(1).geom
+    S = grid.params.stencil.to_abi()
+    p = grid.params
+    v, f = drv.gs_grid_field(grid.handle, 0, 0), drv.gs_grid_field(grid.handle, 0, 3)
+    cv, cf = drv.gs_grid_field(grid.handle, 1, 0), drv.gs_grid_field(grid.handle, 1, 3)
+    out = DevField(L0.nx, L0.ny, L0.nz)
+    st = grid.stream()
+    stream = torch.cuda.ExternalStream(st)
+    pts = float(L0.nx) * L0.ny * L0.nz
+
+    def rr():
+        assert kl.gs_residual_restrict(C.byref(S), C.byref(L0), 0, p.gamma, v, f, None, cf, None, C.byref(L1), st) == 0
+
+    def pro():
+        assert kl.gs_jacobi_sweep2_prolong(C.byref(S), C.byref(L0), 0, p.omega, p.gamma, v, cv, None, C.byref(L1),
+                                           out.ptr, f, None, 0, 0, st) == 0
+
+    res = {}
+    for name, fn, bpp in (("residual_restrict", rr, 17.0), ("prolong_pair", pro, 25.0)):
+        for _ in range(2):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(k):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / k
+        gbps = bpp * pts / (ms * 1e-3) / 1e9
+        res[name] = {"ms": round(ms, 4), "bytes_per_point": bpp, "achieved_GBps": round(gbps, 1),
+                     "frac": round(gbps / PEAK_GBPS, 4)}
+    res["kernels"] = "k_rr2 (residual + full weighting), k_tb2y PRO (prolongation + correction + 2 sweeps)"
+    del out
+    return res
+
+
 def triad_ceiling(n):
     """This GPU's achievable rate for the smoother's byte pattern (2 streamed reads + 1 streamed write,
     24 B per element) on arrays of the level's size — the best of a few grid sizes of the streaming
@@ -344,6 +388,8 @@ def main():
             dist.all_reduce(vt, op=dist.ReduceOp.MAX)
         vc = {"ms": round(vt.item(), 3), "cycles": a.vcycles,
               "config": f"{dims[0]}x{dims[1]}x{dims[2]} linear 2+2, norm readback included", "first_residual": res}
+        if world == 1:  # the other two level-0 passes of the V-cycle, each alone
+            vc["level0_kernels"] = vcycle_level0_kernels(grid, max(4, min(a.steps, 20)))
 
     newton = None
     if world == 1 and a.newton_iters > 0:
