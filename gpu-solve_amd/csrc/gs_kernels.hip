@@ -797,7 +797,7 @@ constexpr int RR2_WXMAX = 8, RR2_NR2_LOG2_POINTS = 26;
 
 // NR: coarse rows per block (1: fine rows 2Y-1..2Y+1 computed; 2: 2Y-1..2Y+3, the shared row 2Y+1 and three
 // of the seven v rows once instead of twice)
-template <int MODE, bool PF, int NR = 1, bool UN = false> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
+template <int MODE, bool PF, int NR = 1, bool UN = false, bool NTU = false> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
 __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* __restrict__ v,
                                                          const double* __restrict__ f, const double* __restrict__ w,
                                                          double* __restrict__ ca,
@@ -843,10 +843,13 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
         const int p = 2 * Z;
 #pragma unroll
         for (int j = 0; j < RR; j++) {
-            VA[s][j] = ld2(at(v, j + 1, p + 1));
-            VB[s][j] = ld2(at(v, j + 1, p + 2));
-            F0[s][j] = ld2(at(f, j + 1, p));
-            F1[s][j] = ld2(at(f, j + 1, p + 1));
+            // NTU: rows no neighbouring block reads (v: 2Y+1 .. 2Y+2NR-3, f: 2Y .. 2Y+2NR-2) bypass L2
+            // retention, leaving it to the shared halo rows
+            const bool uv = NTU && j >= 2 && j <= RR - 3, uf = NTU && j >= 1 && j <= RR - 2;
+            VA[s][j] = uv ? ld2s<true>(at(v, j + 1, p + 1)) : ld2(at(v, j + 1, p + 1));
+            VB[s][j] = uv ? ld2s<true>(at(v, j + 1, p + 2)) : ld2(at(v, j + 1, p + 2));
+            F0[s][j] = uf ? ld2s<true>(at(f, j + 1, p)) : ld2(at(f, j + 1, p));
+            F1[s][j] = uf ? ld2s<true>(at(f, j + 1, p + 1)) : ld2(at(f, j + 1, p + 1));
             if (MODE == GS_NEWTON) {
                 W0[s][j] = ld2(at(w, j + 1, p));
                 W1[s][j] = ld2(at(w, j + 1, p + 1));
@@ -2821,7 +2824,12 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         const dim3 g((unsigned)rows, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
-#define GS_RR2U(M, N, U) hipLaunchKernelGGL((k_rr2<M, false, N, U>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
+        // two-row blocks: the rows no neighbouring block reads are non-temporal loads (0.490 vs 0.505 ms at
+        // 512^3, r02 tools/rr_ab_session.sh rrntu); GS_RR_NTU=0 keeps them cached (A/B)
+        static const bool ntu_on = !getenv("GS_RR_NTU") || atoi(getenv("GS_RR_NTU")) != 0;
+        const bool ntu = ntu_on && nr == 2;
+#define GS_RR2V(M, N, U, T) hipLaunchKernelGGL((k_rr2<M, false, N, U, T>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
+#define GS_RR2U(M, N, U) do { if (ntu) GS_RR2V(M, N, U, true); else GS_RR2V(M, N, U, false); } while (0)
 #define GS_RR2(M, N) do { if (k.unit) GS_RR2U(M, N, true); else GS_RR2U(M, N, false); } while (0)
         if (mode == GS_LINEAR && nr == 2) GS_RR2(GS_LINEAR, 2);
         else if (mode == GS_LINEAR) GS_RR2(GS_LINEAR, 1);
@@ -2829,6 +2837,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         else GS_RR2(GS_NEWTON, 1);
 #undef GS_RR2
 #undef GS_RR2U
+#undef GS_RR2V
         return launch_status();
     }
     StencilOffsets so;
