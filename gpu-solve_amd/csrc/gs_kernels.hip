@@ -851,8 +851,8 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             F0[s][j] = uf ? ld2s<true>(at(f, j + 1, p)) : ld2(at(f, j + 1, p));
             F1[s][j] = uf ? ld2s<true>(at(f, j + 1, p + 1)) : ld2(at(f, j + 1, p + 1));
             if (MODE == GS_NEWTON) {
-                W0[s][j] = ld2(at(w, j + 1, p));
-                W1[s][j] = ld2(at(w, j + 1, p + 1));
+                W0[s][j] = uf ? ld2s<true>(at(w, j + 1, p)) : ld2(at(w, j + 1, p));
+                W1[s][j] = uf ? ld2s<true>(at(w, j + 1, p + 1)) : ld2(at(w, j + 1, p + 1));
             }
         }
         H0[s][0] = ld2(at(v, 0, p));
@@ -2826,8 +2826,8 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
         // two-row blocks: the rows no neighbouring block reads are non-temporal loads (0.490 vs 0.505 ms at
         // 512^3, r02 tools/rr_ab_session.sh rrntu); GS_RR_NTU=0 keeps them cached (A/B)
-        static const bool ntu_on = !getenv("GS_RR_NTU") || atoi(getenv("GS_RR_NTU")) != 0;
-        const bool ntu = ntu_on && nr == 2;
+        static const int ntu_env = getenv("GS_RR_NTU") ? atoi(getenv("GS_RR_NTU")) : 1;
+        const bool ntu = ntu_env == 2 || (ntu_env == 1 && nr == 2);
 #define GS_RR2V(M, N, U, T) hipLaunchKernelGGL((k_rr2<M, false, N, U, T>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
 #define GS_RR2U(M, N, U) do { if (ntu) GS_RR2V(M, N, U, true); else GS_RR2V(M, N, U, false); } while (0)
 #define GS_RR2(M, N) do { if (k.unit) GS_RR2U(M, N, true); else GS_RR2U(M, N, false); } while (0)
