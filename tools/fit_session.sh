@@ -1,3 +1,6 @@
+#!/bin/bash
+# A/B of the round-fitted zero-iterate pair chunks (GS_FIT_ROUNDS 0/1) through gpurun: GPU tests,
+# bench V-cycle / Newton, and a rocprofv3 V-cycle breakdown per setting.   tools/fit_session.sh
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/fit; mkdir -p $O

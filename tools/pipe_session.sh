@@ -1,3 +1,6 @@
+#!/bin/bash
+# A/B of the overlapped solve loop (GS_NO_PIPELINE unset / set) through gpurun: GPU tests, bench
+# V-cycle / Newton, and a rocprofv3 V-cycle breakdown.   tools/pipe_session.sh
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/pipe; mkdir -p $O

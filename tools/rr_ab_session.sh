@@ -10,7 +10,7 @@ for val in "$A" "$B"; do
   env "$VAR=$val" timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_solver.py -x -q --timeout 200 --timeout-method thread > $O/pytest_$val.log 2>&1 || { tail -30 $O/pytest_$val.log; exit 1; }
   tail -1 $O/pytest_$val.log
 done
-bash tools/ab_env.sh $TAG $VAR "$A" "$B" --steps 20 --vcycles 50 || exit 1
+bash tools/ab_multi.sh $TAG $VAR "$A $B" 2 --vcycles 50 || exit 1
 for val in "$A" "$B"; do
   env "$VAR=$val" timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/prof_$val -o run -- python bench.py --steps 20 --vcycles 5 --cpu-sweeps 0 --newton-iters 0 > $O/prof_$val.log 2>&1 || exit 1
   echo "== $VAR=$val"; python tools/vc_breakdown.py $(find $O/prof_$val -name '*kernel_trace.csv' -print -quit) 6

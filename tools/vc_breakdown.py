@@ -1,3 +1,5 @@
+"""The last complete V-cycle of a rocprofv3 kernel trace (between the last two k_sumsq_finish launches),
+kernel time per (name, grid) and the wall span:   python tools/vc_breakdown.py <kernel_trace.csv> [top]"""
 import csv, collections, sys
 rows=list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r:int(r['Start_Timestamp']))
