@@ -10,6 +10,12 @@
 //
 // Layout: x unit-stride, z slowest (include/gpusolve_hip.h), so Z-slabs are contiguous planes and
 // a wave64 row load along x is one coalesced 1 KiB (dwordx4 per lane) access.
+// Timing-only experiment builds (tools/pro_exp_build.sh + tools/pro_exp.py; never the product): 1 = the fused prolongation
+// pair without the correction arithmetic, 2 = also without the coarse loads, 3 = LINEAR pairs at one
+// plane step of prefetch
+#ifndef GS_PRO_EXP
+#define GS_PRO_EXP 0
+#endif
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -1776,7 +1782,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             const int cs = PFD == 1 ? ph ^ 1 : ph4; // slot holding this step's operands
             if (PFD == 1) load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
             else load_slot((ph4 + 2) & 3, min(z + 2, nz + 1), min(z + 3, nz + 2));
-            if (PRO && ph == 0) craw((z >> 1) + 2); // consumed at the end of the next step
+            if (PRO && GS_PRO_EXP < 2 && ph == 0) craw((z >> 1) + 2); // consumed at the end of the next step
             // ---- publish: x-edge columns (v(z) rows 0..RY, sweep-1(z-1) rows 1..RY) and the y-edge row
             if (lane == 0) {
 #pragma unroll
@@ -1838,7 +1844,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         ES1n = (!pz || !erowc) ? c : nv;
                     }
                 }
-                if constexpr (PRO != 0) {
+                if constexpr (PRO != 0 && GS_PRO_EXP == 0) {
                     // the corrected iterate: plane z+1 (VL) and the halo row at plane z (HL); with z0
                     // even, ph 0 has z even (z+1 odd: coarse K, K+1) and ph 1 has z odd
 #pragma unroll
@@ -1958,7 +1964,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                 EC = EA[cs];
                 ES1c = ES1n;
             }
-            if (PRO && ph == 1) { // next step: coarse planes K+1, K+2
+            if (PRO && GS_PRO_EXP < 2 && ph == 1) { // next step: coarse planes K+1, K+2
                 if constexpr (RECOMP) {
                     wsl ^= 1;
                 } else {
@@ -2246,7 +2252,7 @@ constexpr int TBY_RY = 2, TBY_RY_NEWTON = 2, TBY_WX = 4, TB_RY_B = 2, TB_WX_B = 
 // prefetch distance of k_tb2y (plane steps): LINEAR keeps two steps in flight (215 VGPRs, still two
 // waves per SIMD; 0.662 vs 0.673 ms per 512^3 pair, profiles/r01m_summary.md), the other modes and
 // the fused prolongation one (VGPR budget: the LINEAR prolongation pair at distance 2 spills)
-constexpr int tby_pfd(int mode) { return mode == GS_LINEAR ? 2 : 1; }
+constexpr int tby_pfd(int mode) { return mode == GS_LINEAR && GS_PRO_EXP != 3 ? 2 : 1; }
 // column blocks (XH): LINEAR at distance 2 too (247 VGPRs, no spill); GS_TBX_PFD=1 selects distance 1 (A/B)
 bool tbx_pfd2()
 {

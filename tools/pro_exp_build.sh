@@ -1,0 +1,11 @@
+#!/bin/bash
+# Timing-only builds of the kernel library with GS_PRO_EXP=1..3 (gs_kernels.hip) into
+# gpu-solve_amd/build/exp/ (git-ignored; travels to the GPU box). Run here, then tools/pro_exp.py there.
+set -e
+H=$(dirname "$0")/../gpu-solve_amd
+mkdir -p $H/build/exp
+for e in ${@:-1 2 3}; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -I$H/../include -I$H/csrc \
+    -DGS_PRO_EXP=$e -shared -Wl,-Bsymbolic $H/csrc/gs_kernels.hip -o $H/build/exp/libgs_exp$e.so &
+done
+wait
