@@ -2326,6 +2326,22 @@ void refit_chunks(K* fn, int threads, int64_t planes, int lo, int hi, bool even,
     }
 }
 
+// compute units of the current device (cached per device)
+int64_t device_cus()
+{
+    static std::mutex m;
+    static std::map<int, int64_t> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(m);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    (void)hipGetLastError();
+    return cache[dev] = cus;
+}
+
 int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
              int mode = GS_LINEAR, bool* xh = nullptr)
 {
@@ -2353,6 +2369,18 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
     if (big_chunks && L->nx * L->ny * L->nz >= ((int64_t)1 << 26)) {
         const int64_t b = tiles * L->nz / 512;
         c = b < 64 ? 64 : (b > 128 ? 128 : b);
+        // k_tb2y shapes whose tiles fit the CUs: chunks long enough for ONE round of blocks (every
+        // k_tb2y variant at this size runs one 8-wave block per CU). 512^3: 256 blocks of 256 planes,
+        // pair 0.587 vs 0.602 ms, V-cycle 2.16 vs 2.18 ms (tools/ab_multi.sh; 170- and 192-plane
+        // chunks, i.e. uneven rounds, are far slower). GS_PAIR_ONE_ROUND=0 keeps the rule above (A/B).
+        static const bool one_round = !getenv("GS_PAIR_ONE_ROUND") || std::atoi(getenv("GS_PAIR_ONE_ROUND")) != 0;
+        const int64_t cus = device_cus();
+        if (one_round && (two || colb) && tiles <= cus) {
+            const int64_t per = cus / tiles; // chunks per tile
+            int64_t c1 = (L->nz + per - 1) / per;
+            c1 += c1 & 1;
+            if (c1 > c) c = c1;
+        }
     }
     c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)
     *zc = (int)c;
