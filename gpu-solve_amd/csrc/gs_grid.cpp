@@ -72,9 +72,14 @@ void DeviceField::swap(DeviceField& o) noexcept
     std::swap(dry_, o.dry_);
 }
 
-StreamGuard::StreamGuard(bool create)
+StreamGuard::StreamGuard(bool create, bool high)
 {
-    if (create) check((int)hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    if (!create) return;
+    int least = 0, greatest = 0;
+    if (high && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        check((int)hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest), "hipStreamCreateWithPriority");
+    else
+        check((int)hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
 }
 StreamGuard::~StreamGuard()
 {
@@ -125,8 +130,10 @@ LevelClock::~LevelClock()
 // (src/cpu/CpuGridData.cpp:19-41). Fields a mode never touches are not allocated.
 HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomeratePoints,
                          std::vector<std::string>* traceLog)
-    : GridParams(grid), trace(traceLog), comm_(comm), stream_(traceLog == nullptr), commStream_(traceLog == nullptr),
-      bndStream_(traceLog == nullptr && comm != nullptr && comm->size() > 1)
+    : GridParams(grid), trace(traceLog), comm_(comm), stream_(traceLog == nullptr),
+      // the exchange path at high priority: when the interior sweep's blocks retire, the dispatcher
+      // hands the freed CUs to the boundary planes and the ghost exchange first
+      commStream_(traceLog == nullptr, true), bndStream_(traceLog == nullptr && comm != nullptr && comm->size() > 1, true)
 {
     const bool dry = traceLog != nullptr;
     const std::size_t mn = std::min(std::min(gridDim[0], gridDim[1]), gridDim[2]);

@@ -57,7 +57,8 @@ private:
 
 struct StreamGuard {
     hipStream_t s = nullptr;
-    explicit StreamGuard(bool create = true);
+    // high: the device's greatest stream priority (the exchange path: boundary planes, ghost copies)
+    explicit StreamGuard(bool create = true, bool high = false);
     ~StreamGuard();
 };
 

@@ -2372,10 +2372,14 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
         // k_tb2y shapes whose tiles fit the CUs: chunks long enough for ONE round of blocks (every
         // k_tb2y variant at this size runs one 8-wave block per CU). 512^3: 256 blocks of 256 planes,
         // pair 0.587 vs 0.602 ms, V-cycle 2.16 vs 2.18 ms (tools/ab_multi.sh; 170- and 192-plane
-        // chunks, i.e. uneven rounds, are far slower). GS_PAIR_ONE_ROUND=0 keeps the rule above (A/B).
+        // chunks, i.e. uneven rounds, are far slower). Only for plane ranges from the level's first plane
+        // (z0 = 0: whole single-GPU levels): the interior launch of an overlapped Z-slab sweep keeps two
+        // rounds, so that the ghost exchange running beside it (RCCL kernels on the comm stream) finds
+        // free CUs halfway through instead of waiting for every block of the interior to retire.
+        // GS_PAIR_ONE_ROUND=0 keeps the rule above (A/B).
         static const bool one_round = !getenv("GS_PAIR_ONE_ROUND") || std::atoi(getenv("GS_PAIR_ONE_ROUND")) != 0;
         const int64_t cus = device_cus();
-        if (one_round && (two || colb) && tiles <= cus) {
+        if (one_round && (two || colb) && tiles <= cus && L->z0 == 0) {
             const int64_t per = cus / tiles; // chunks per tile
             int64_t c1 = (L->nz + per - 1) / per;
             c1 += c1 & 1;
