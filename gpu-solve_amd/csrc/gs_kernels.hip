@@ -2342,6 +2342,14 @@ int64_t device_cus()
     return cache[dev] = cus;
 }
 
+// chunk length (planes) of pair launches over plane ranges past a slab's first plane; 0: the rules
+// for whole levels. Read at every call (tools/exchange_probe.py varies it in one process).
+int slab_zc()
+{
+    const char* e = getenv("GS_SLAB_ZC");
+    return e && *e ? std::atoi(e) : 0;
+}
+
 int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
              int mode = GS_LINEAR, bool* xh = nullptr)
 {
@@ -2384,6 +2392,13 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
             int64_t c1 = (L->nz + per - 1) / per;
             c1 += c1 & 1;
             if (c1 > c) c = c1;
+        }
+        // plane ranges past a slab's first plane (the interior launch of an overlapped Z-slab sweep):
+        // GS_SLAB_ZC-plane chunks, so that blocks retire often and the ghost exchange's kernels
+        // (RCCL's need a whole SIMD's registers) find a free CU soon after they are enqueued
+        if (L->z0 != 0) {
+            const int sz = slab_zc();
+            if (sz > 0) c = sz;
         }
     }
     c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)
@@ -2523,6 +2538,32 @@ __global__ __launch_bounds__(256) void k_bw(double* __restrict__ out, const doub
         }
     }
     if (KIND == 0 && acc == -1.2345e300) *sink = acc; // keeps the loads alive
+}
+
+// A copy with the resource footprint of RCCL's gfx950 transport kernels (ncclDevKernel_Generic: 256
+// VGPRs, 37664 B of LDS per 256-thread workgroup): the clobber of v255 makes the allocator reserve
+// every VGPR. Stands in for the ghost exchange in tools/exchange_probe.py (when does a workgroup
+// that needs a whole SIMD's registers get a CU while the interior pair holds the GPU?).
+__global__ __launch_bounds__(256) void k_fatcopy(double* __restrict__ out, const double* __restrict__ a, int64_t n2)
+{
+    __shared__ double pad[4708];
+    asm volatile("" ::: "v255");
+    for (int i = threadIdx.x; i < 4708; i += 256) pad[i] = 0.0;
+    __syncthreads();
+    const double z = pad[(threadIdx.x * 17) % 4708];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const double2 x = ld2s<true>(a + 2 * i);
+        st2s<true>(out + 2 * i, x.x + z, x.y + z);
+    }
+}
+
+// One wave that sleeps `iters` x s_sleep(127) (~3.4 us each at 2.4 GHz) and touches no memory: a delay
+// on a stream, e.g. between the boundary planes and the interior launch of an overlapped Z-slab sweep
+// so that the exchange's kernels are dispatched first (tools/exchange_probe.py).
+__global__ __launch_bounds__(64) void k_sleep(int64_t iters)
+{
+    for (int64_t i = 0; i < iters; i++) __builtin_amdgcn_s_sleep(127);
 }
 
 // div_hh against the plain division (tests: bitwise equality over all magnitudes)
@@ -3098,7 +3139,16 @@ int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, d
 int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
                 double* sink, hipStream_t st)
 {
-    if (n < 0 || (n & 1) || kind < 0 || kind > 3 || blocks <= 0) return GS_EINVAL;
+    if (kind == 5) { // k_sleep: n iterations of s_sleep(127), one wave
+        if (n < 0) return GS_EINVAL;
+        hipLaunchKernelGGL(k_sleep, dim3(1), dim3(64), 0, st, n);
+        return launch_status();
+    }
+    if (n < 0 || (n & 1) || kind < 0 || kind > 4 || blocks <= 0) return GS_EINVAL;
+    if (kind == 4) { // copy at RCCL's transport-kernel footprint (k_fatcopy)
+        hipLaunchKernelGGL(k_fatcopy, dim3(blocks), dim3(256), 0, st, out, a, n / 2);
+        return launch_status();
+    }
     using K = void (*)(double*, const double*, const double*, int64_t, double*);
     static const K tab[4][2][2] = {
         {{k_bw<0, 1, false>, k_bw<0, 1, true>}, {k_bw<0, 4, false>, k_bw<0, 4, true>}},

@@ -1,0 +1,180 @@
+"""One overlapped Z-slab pair step of config #5's per-rank slab (1024 x 1024 x 128) on one GPU, with a
+stand-in for the RCCL exchange: the boundary planes (two per side) on a high-priority stream, then a
+copy at the footprint of RCCL's gfx950 transport kernels (gs_debug_bw kind 4: 256 VGPRs, 37 KB LDS
+per workgroup; 17 MB = one neighbour's two ghost planes each way) on a second high-priority stream,
+and the interior planes 3..126 on the compute stream — unmasked, or on a stream whose CU mask leaves
+R CUs per XCD free (the driver's GS_EXCHANGE_CUS, gs_grid.cpp MaskedStream). Reports, per setting,
+the step time on the compute stream (fork to join, HIP events) and, from a kernel trace, when the
+stand-in exchange started and ended relative to the interior launch.
+    python tools/exchange_probe.py [reps]                    (step times)
+    rocprofv3 --kernel-trace -d <dir> -o run --output-format csv -- python tools/exchange_probe.py 3
+    python tools/exchange_probe.py --analyze <dir>/run_kernel_trace.csv"""
+import csv
+import ctypes as C
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NX, NY, NZ = 1024, 1024, 128
+
+
+def mask_words(cus, per_xcd):
+    """gs_grid.cpp MaskedStream::mask: bits 33x + 8r cleared (one per XCD under either bit mapping)."""
+    m = [0] * ((cus + 31) // 32)
+    for b in range(cus):
+        m[b // 32] |= 1 << (b % 32)
+    if cus == 256:
+        for r in range(min(per_xcd, 3)):
+            for x in range(8):
+                b = 33 * x + 8 * r
+                m[b // 32] &= ~(1 << (b % 32))
+    return m
+
+
+def analyze(path):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    interior, steps = None, []
+    for r in rows:
+        name, t0, t1 = r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if "k_tb2y" in name and t1 - t0 > 200000:
+            interior = (t0, t1)  # the interior launch (boundary launches: 2 planes, < 100 us)
+        elif "k_fatcopy" in name and interior:
+            i0, i1 = interior
+            steps.append(((t0 - i0) / 1e3, (t1 - i1) / 1e3, (i1 - i0) / 1e3, (t1 - t0) / 1e3))
+    print("stand-in exchange start - interior start / end - interior end / interior length / own length (us)")
+    for a in steps:
+        print("   " + "  ".join(f"{x:8.1f}" for x in a))
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    sys.path.insert(0, os.path.join(HERE, "..", "gpu-solve_amd"))
+    import torch
+    import gpusolve as gsv
+    from gpusolve.devfield import DevField
+    k = gsv.kernels()
+    hip = C.CDLL("libamdhip64.so")
+    v, o, f = DevField(NX, NY, NZ, fill=0.5), DevField(NX, NY, NZ), DevField(NX, NY, NZ, fill=1.0)
+    S = gsv.Stencil().to_abi()
+    h = 1.0 / (NY + 1)
+    least, greatest = torch.cuda.Stream.priority_range()
+    main_s = torch.cuda.Stream()
+    bnd_s, comm_s = torch.cuda.Stream(priority=greatest), torch.cuda.Stream(priority=greatest)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    streams = {0: main_s}
+    for r in ((1,) if os.environ.get("PROBE_MASK") else ()):
+        words = mask_words(cus, r)
+        raw = C.c_void_p()
+        arr = (C.c_uint32 * len(words))(*words)
+        assert hip.hipExtStreamCreateWithCUMask(C.byref(raw), len(words), arr) == 0
+        streams[r] = torch.cuda.ExternalStream(raw.value)
+    m = 2 * 2 * v.ldz  # two ghost planes each way
+    A = torch.rand(m, dtype=torch.float64, device="cuda")
+    O = torch.empty(m, dtype=torch.float64, device="cuda")
+    sink = torch.zeros(1, dtype=torch.float64, device="cuda")
+
+    def sub(z1, z2):
+        L = v.level(h)
+        L.nz = z2 - z1 + 1
+        L.z0 = z1 - 1
+        off = 8 * (z1 - 1) * v.ldz
+        return L, off
+
+    def pair(z1, z2, st):
+        L, off = sub(z1, z2)
+        assert k.gs_jacobi_sweep2(C.byref(S), C.byref(L), 0, 0.8, 1.0, v.ptr + off, o.ptr + off, f.ptr + off, None,
+                                  1, 1, st.cuda_stream) == 0
+
+    bnd2_s = torch.cuda.Stream(priority=greatest)
+
+    def step2(variant, blocks):
+        """variant: 'cur' boundary planes in sequence on one stream, interior concurrent (r02 driver);
+        'two' both boundary launches on their own streams, interior concurrent; 'first' both on their own
+        streams and the interior waits for them (the exchange and the interior become ready together);
+        'first-mask' the same with the interior on the 1-CU-per-XCD masked stream; 'delay-n' as 'first',
+        with the interior also waiting for a one-wave kernel of n x s_sleep(127) (~3.4 us each) started
+        after the boundary planes, so that the exchange kernel is dispatched onto an idle GPU first."""
+        ist = streams[1] if variant == "first-mask" else main_s
+        delay = int(variant.split("-")[1]) if variant.startswith("delay-") else 0
+        ev = torch.cuda.Event()
+        ev.record(main_s)
+        bnd_s.wait_event(ev)
+        pair(1, 2, bnd_s)
+        if variant == "cur":
+            pair(NZ - 1, NZ, bnd_s)
+        else:
+            bnd2_s.wait_event(ev)
+            pair(NZ - 1, NZ, bnd2_s)
+            bnd_s.wait_stream(bnd2_s)
+        if blocks:
+            comm_s.wait_stream(bnd_s)
+            assert k.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
+                                 comm_s.cuda_stream) == 0
+        if ist is not main_s:
+            ist.wait_event(ev)
+        if variant in ("first", "first-mask"):
+            ist.wait_stream(bnd_s)
+        if delay:  # the interior waits for the boundary planes, then a sleeping wave on its own stream
+            ist.wait_stream(bnd_s)
+            assert k.gs_debug_bw(5, 1, 1, 1, None, None, None, delay, None, ist.cuda_stream) == 0
+        pair(3, NZ - 2, ist)
+        if ist is not main_s:
+            main_s.wait_stream(ist)
+        main_s.wait_stream(comm_s if blocks else bnd_s)
+
+    res = {}
+    settings = [(v_, b, "0") for v_ in ("cur", "first", "delay-1", "delay-3", "delay-6", "delay-12")
+                for b in (0, 8, 32)]
+    if os.environ.get("PROBE_MASK"):
+        settings += [("first-mask", b, "0") for b in (0, 8, 32)]
+    for _ in range(2):
+        for v_, b, zc in settings:
+            os.environ["GS_SLAB_ZC"] = zc
+            step2(v_, b)
+    torch.cuda.synchronize()
+    for v_, b, zc in settings:
+        os.environ["GS_SLAB_ZC"] = zc
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(main_s)
+        for _ in range(reps):
+            step2(v_, b)
+        e1.record(main_s)
+        torch.cuda.synchronize()
+        res[f"{v_} interior_zc={zc} exchange={'fat x%d' % b if b else 'none'}"] = round(e0.elapsed_time(e1) / reps, 4)
+    os.environ["GS_SLAB_ZC"] = "0"
+    # interior alone: unmasked / masked; chunk lengths
+    for zc in ("32",):
+        os.environ["GS_SLAB_ZC"] = zc
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(main_s)
+        for _ in range(reps):
+            pair(3, NZ - 2, main_s)
+        e1.record(main_s)
+        torch.cuda.synchronize()
+        res[f"interior alone, zc={zc}"] = round(e0.elapsed_time(e1) / reps, 4)
+    os.environ["GS_SLAB_ZC"] = "0"
+    for r in streams:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st = streams[r]
+        st.wait_stream(main_s)
+        e0.record(st)
+        for _ in range(reps):
+            pair(3, NZ - 2, st)
+        e1.record(st)
+        torch.cuda.synchronize()
+        res[f"interior alone, mask_free_per_xcd={r}"] = round(e0.elapsed_time(e1) / reps, 4)
+    out = {"slab": [NX, NY, NZ], "cus": cus, "step_ms": res,
+           "note": "one overlapped pair step: boundary pairs (planes 1-2, 127-128, high priority) -> stand-in "
+                   "exchange (k_fatcopy, 34 MB copy at RCCL's kernel footprint) || interior pair planes 3..126"}
+    print(json.dumps(out, indent=1))
+    torch.cuda.synchronize()
+    for r in [r for r in streams if r]:
+        hip.hipStreamDestroy(C.c_void_p(streams[r].cuda_stream))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--analyze":
+        analyze(sys.argv[2])
+    else:
+        main()
