@@ -232,6 +232,37 @@ def vcycle_level0_kernels(grid, k):
     return res
 
 
+def slab_local_pair_ms(grid, rank, world, k):
+    """N > 1: the level-0 pair on this rank's slab with no exchange (gs_jacobi_sweep2 on the grid's own
+    v and f into a spare field, the slab's internal sides flagged as ghost planes), averaged over k
+    launches: set beside kernel_ms (the overlapped sweep with its RCCL exchange) it shows what the
+    exchange costs per pair on this rank."""
+    import ctypes as C
+    from gpusolve.devfield import DevField
+    kl, drv = gsv.kernels(), gsv.driver()
+    L = grid.getLevel(0).geom
+    S = grid.params.stencil.to_abi()
+    v, f = drv.gs_grid_field(grid.handle, 0, 0), drv.gs_grid_field(grid.handle, 0, 3)
+    out = DevField(L.nx, L.ny, L.nz)
+    st = grid.stream()
+    stream = torch.cuda.ExternalStream(st)
+    zlo, zhi = int(rank > 0), int(rank + 1 < world)
+
+    def run():
+        assert kl.gs_jacobi_sweep2(C.byref(S), C.byref(L), 0, 0.8, 1.0, v, out.ptr, f, None, zlo, zhi, st) == 0
+
+    for _ in range(2):
+        run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(k):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    del out
+    return e0.elapsed_time(e1) / k
+
+
 def triad_ceiling(n):
     """This GPU's achievable rate for the smoother's byte pattern (2 streamed reads + 1 streamed write,
     24 B per element) on arrays of the level's size — the best of a few grid sizes of the streaming
@@ -355,10 +386,26 @@ def main():
     # passes over the level: a fused pair reads v and f once and writes once, like a single sweep
     passes = (a.steps // 2 + a.steps % 2) if fused else a.steps
     kernel_ms = ev0.elapsed_time(ev1) / passes  # average pass duration on the solver's stream
+    own_elapsed = elapsed
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
+
+    multi = None
+    if world > 1:  # per-rank view of the timed window, and the pair's cost without its exchange
+        local = slab_local_pair_ms(grid, rank, world, max(4, passes))
+        per = torch.tensor([own_elapsed / a.steps * 1e3, kernel_ms, local], dtype=torch.float64, device="cuda")
+        allp = [torch.zeros_like(per) for _ in range(world)]
+        dist.all_gather(allp, per)
+        rows = [x.tolist() for x in allp]
+        multi = {"rank_ms_per_step": [round(r[0], 4) for r in rows],
+                 "rank_pair_ms": [round(r[1], 4) for r in rows],
+                 "rank_pair_ms_no_exchange": [round(r[2], 4) for r in rows],
+                 "exchange_ms_per_pair_max": round(max(r[1] - r[2] for r in rows), 4),
+                 "note": "rank_pair_ms: the overlapped pair (boundary planes, RCCL ghost exchange, interior) "
+                         "per launch on each rank's compute stream; _no_exchange: the same pair on the same "
+                         "slab run locally, no exchange"}
 
     single = ceiling = None
     if world == 1:
@@ -442,6 +489,7 @@ def main():
                                                  "definition; with temporal blocking (2 updates per pass) this is "
                                                  "NOT HBM traffic: the HBM-side figure is `achieved` "
                                                  "(24 B per point per launch / kernel_ms)")},
+            "multi_gpu": multi,
             "single_sweep_kernel": single,
             "measured_ceiling": ceiling,
             "vcycle": vc,

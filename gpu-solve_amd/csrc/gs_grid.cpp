@@ -230,7 +230,10 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
     check((int)hipMalloc((void**)&partials_, sizeof(double) * maxParts), "hipMalloc(partials)");
     check((int)hipMalloc((void**)&dNorm_, sizeof(double)), "hipMalloc(norm)");
     check((int)hipMalloc((void**)&dRankSums_, sizeof(double) * nranks()), "hipMalloc(rank sums)");
-    check((int)hipHostMalloc((void**)&hNorm_, sizeof(double), hipHostMallocDefault), "hipHostMalloc");
+    // the final norm goes straight from the finishing kernel to this pinned word (no D2H copy launch)
+    check((int)hipHostMalloc((void**)&hNorm_, sizeof(double), hipHostMallocMapped | hipHostMallocCoherent),
+          "hipHostMalloc");
+    check((int)hipHostGetDevicePointer((void**)&hNormDev_, hNorm_, 0), "hipHostGetDevicePointer");
     check((int)hipEventCreateWithFlags(&evA_, hipEventDisableTiming), "hipEventCreate");
     check((int)hipEventCreateWithFlags(&evB_, hipEventDisableTiming), "hipEventCreate");
     check((int)hipEventCreateWithFlags(&evC_, hipEventDisableTiming), "hipEventCreate");
@@ -291,15 +294,13 @@ double HipGridData::traceNorm()
 double HipGridData::readNorm()
 {
     if (trace) return traceNorm();
-    check((int)hipMemcpyAsync(hNorm_, dNorm_, sizeof(double), hipMemcpyDeviceToHost, stream_.s), "hipMemcpyAsync");
     sync();
-    return *hNorm_;
+    return *(volatile double*)hNorm_;
 }
 
 void HipGridData::readNormBegin()
 {
     if (trace) return;
-    check((int)hipMemcpyAsync(hNorm_, dNorm_, sizeof(double), hipMemcpyDeviceToHost, stream_.s), "hipMemcpyAsync");
     check((int)hipEventRecord(evNorm_, stream_.s), "hipEventRecord");
 }
 
@@ -309,7 +310,7 @@ double HipGridData::readNormEnd()
     // distributed: a bounded wait that also polls the communicator's error state (gs_comm.hpp)
     if (comm_ && comm_->size() > 1) comm_->syncEvent(evNorm_);
     else check((int)hipEventSynchronize(evNorm_), "hipEventSynchronize");
-    return *hNorm_;
+    return *(volatile double*)hNorm_;
 }
 
 void HipGridData::sync()
@@ -533,9 +534,9 @@ double HipSolver::finishNorm(HipGridData& grid, int64_t nparts, bool wait)
     if (grid.nranks() > 1 && grid.getLevel(0).distributed) {
         check(gs_sumsq_finish(grid.partials(), nparts, grid.dNorm(), 1, s), "gs_sumsq_finish");
         grid.comm()->allgather1(grid.dNorm(), grid.dRankSums(), s);
-        check(gs_sumsq_finish(grid.dRankSums(), grid.nranks(), grid.dNorm(), 0, s), "gs_sumsq_finish");
+        check(gs_sumsq_finish(grid.dRankSums(), grid.nranks(), grid.hNormDev(), 0, s), "gs_sumsq_finish");
     } else {
-        check(gs_sumsq_finish(grid.partials(), nparts, grid.dNorm(), 0, s), "gs_sumsq_finish");
+        check(gs_sumsq_finish(grid.partials(), nparts, grid.hNormDev(), 0, s), "gs_sumsq_finish");
     }
     if (wait) return grid.readNorm();
     grid.readNormBegin();

@@ -129,10 +129,11 @@ public:
 
     // residual-norm plumbing: per-block partials, device scalars, pinned host scalar
     double* partials() const { return partials_; }
-    double* dNorm() const { return dNorm_; }
+    double* dNorm() const { return dNorm_; }       // this rank's sum of squares (distributed norms)
+    double* hNormDev() const { return hNormDev_; } // the pinned norm word, as the finishing kernel writes it
     double* dRankSums() const { return dRankSums_; }
-    double readNorm(); // async D2H of dNorm + stream sync: the one host sync per V-cycle
-    // the same in two halves: the D2H copy + an event now, the (bounded) wait for the event later, so
+    double readNorm(); // stream sync + the pinned norm word: the one host sync per V-cycle
+    // the same in two halves: an event now, the (bounded) wait for the event later, so
     // that more work can be enqueued in between
     void readNormBegin();
     double readNormEnd();
@@ -157,6 +158,7 @@ private:
     double* dNorm_ = nullptr;
     double* dRankSums_ = nullptr;
     double* hNorm_ = nullptr;
+    double* hNormDev_ = nullptr;
     hipEvent_t evA_ = nullptr, evB_ = nullptr, evC_ = nullptr, evNorm_ = nullptr;
     std::vector<double> dryParts_;
     long traceNorms_ = 0;
