@@ -27,6 +27,7 @@ cpu_baseline: the reference's own CpuSolver::jacobi (oracle/_ref/ref_probe, comp
 """
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -394,15 +395,20 @@ def main():
 
     multi = None
     if world > 1:  # per-rank view of the timed window, and the pair's cost without its exchange
-        local = slab_local_pair_ms(grid, rank, world, max(4, passes))
+        try:
+            local = slab_local_pair_ms(grid, rank, world, max(4, passes))
+        except Exception:  # noqa: BLE001 (diagnostic only)
+            local = float("nan")
         per = torch.tensor([own_elapsed / a.steps * 1e3, kernel_ms, local], dtype=torch.float64, device="cuda")
         allp = [torch.zeros_like(per) for _ in range(world)]
         dist.all_gather(allp, per)
         rows = [x.tolist() for x in allp]
-        multi = {"rank_ms_per_step": [round(r[0], 4) for r in rows],
-                 "rank_pair_ms": [round(r[1], 4) for r in rows],
-                 "rank_pair_ms_no_exchange": [round(r[2], 4) for r in rows],
-                 "exchange_ms_per_pair_max": round(max(r[1] - r[2] for r in rows), 4),
+        fin = lambda x: round(x, 4) if math.isfinite(x) else None  # noqa: E731 (JSON has no NaN)
+        gaps = [r[1] - r[2] for r in rows if math.isfinite(r[2])]
+        multi = {"rank_ms_per_step": [fin(r[0]) for r in rows],
+                 "rank_pair_ms": [fin(r[1]) for r in rows],
+                 "rank_pair_ms_no_exchange": [fin(r[2]) for r in rows],
+                 "exchange_ms_per_pair_max": fin(max(gaps)) if gaps else None,
                  "note": "rank_pair_ms: the overlapped pair (boundary planes, RCCL ghost exchange, interior) "
                          "per launch on each rank's compute stream; _no_exchange: the same pair on the same "
                          "slab run locally, no exchange"}
@@ -423,20 +429,31 @@ def main():
 
     vc = None
     if a.vcycles > 0:
-        res = gsv.HipSolver.vcycle(grid)  # warm-up (first touch of every level)
-        barrier()
-        import ctypes as C
-        ms, last = C.c_double(), C.c_double()
-        rc = drv.gs_grid_time_vcycles(grid.handle, a.vcycles, C.byref(ms), C.byref(last))
-        if rc:
-            raise gsv.GpuSolveError(drv.gs_last_error().decode())
-        vt = torch.tensor([ms.value / a.vcycles], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(vt, op=dist.ReduceOp.MAX)
-        vc = {"ms": round(vt.item(), 3), "cycles": a.vcycles,
-              "config": f"{dims[0]}x{dims[1]}x{dims[2]} linear 2+2, norm readback included", "first_residual": res}
-        if world == 1:  # the other two level-0 passes of the V-cycle, each alone
-            vc["level0_kernels"] = vcycle_level0_kernels(grid, max(4, min(a.steps, 20)))
+        # after the headline: a failure here (e.g. the RCCL communicator timing out and aborting, which
+        # raises instead of hanging) is reported in the line rather than losing it; the ranks agree on
+        # the outcome before the cross-rank maximum
+        err = None
+        try:
+            res = gsv.HipSolver.vcycle(grid)  # warm-up (first touch of every level)
+            barrier()
+            import ctypes as C
+            ms, last = C.c_double(), C.c_double()
+            rc = drv.gs_grid_time_vcycles(grid.handle, a.vcycles, C.byref(ms), C.byref(last))
+            if rc:
+                raise gsv.GpuSolveError(drv.gs_last_error().decode())
+        except Exception as e:  # noqa: BLE001 (reported, never required)
+            err = f"{type(e).__name__}: {e}"
+        if any_rank(err is not None):
+            vc = {"error": err or "failed on another rank"}
+        else:
+            vt = torch.tensor([ms.value / a.vcycles], dtype=torch.float64, device="cuda")
+            if world > 1:
+                dist.all_reduce(vt, op=dist.ReduceOp.MAX)
+            vc = {"ms": round(vt.item(), 3), "cycles": a.vcycles,
+                  "config": f"{dims[0]}x{dims[1]}x{dims[2]} linear 2+2, norm readback included",
+                  "first_residual": res}
+            if world == 1:  # the other two level-0 passes of the V-cycle, each alone
+                vc["level0_kernels"] = vcycle_level0_kernels(grid, max(4, min(a.steps, 20)))
 
     newton = None
     if world == 1 and a.newton_iters > 0:
