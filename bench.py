@@ -330,6 +330,11 @@ def ramp_sweeps(run, ramp_ms, any_rank, chunk=40):
 
 def main():
     a = parse()
+    # stdout carries exactly the one JSON line: anything the libraries print there (RCCL writes a version
+    # banner at communicator creation) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -516,7 +521,7 @@ def main():
         }
         if pmc:
             line["roofline"]["traffic_source"] = pmc.get("source")
-        print(json.dumps(line), flush=True)
+        os.write(json_out, (json.dumps(line) + "\n").encode())
     grid.close()
     if world > 1:
         dist.destroy_process_group()

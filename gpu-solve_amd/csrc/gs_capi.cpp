@@ -426,6 +426,36 @@ void* gs_grid_create_rccl(const gs_params* p, int rank, int nranks, const unsign
     }
 }
 
+int gs_uid_publish(const char* path, const unsigned char uid[128])
+{
+    if (!path || !uid) {
+        g_err = "bad arguments";
+        return 1;
+    }
+    try {
+        gs::publishUid(path, uid);
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return 1;
+    }
+}
+
+int gs_uid_await(const char* path, double timeout_s, unsigned char uid[128])
+{
+    if (!path || !uid) {
+        g_err = "bad arguments";
+        return 1;
+    }
+    try {
+        gs::awaitUid(path, timeout_s, uid);
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return 1;
+    }
+}
+
 int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, int sweeps, int solve, double* hist,
                           int cap, int* count, double* v_host)
 {

@@ -10,6 +10,8 @@
 #include <string>
 #include <thread>
 
+#include <unistd.h>
+
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -208,6 +210,40 @@ void rcclUniqueId(void* uid)
     ncclUniqueId id;
     ncclOk(ncclGetUniqueId(&id), "ncclGetUniqueId");
     std::memcpy(uid, &id, sizeof(id));
+}
+
+void publishUid(const std::string& path, const unsigned char* uid)
+{
+    const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) throw Error("cannot write the RCCL id file " + tmp);
+    const bool ok = std::fwrite(uid, 1, 128, f) == 128;
+    if (std::fclose(f) != 0 || !ok || std::rename(tmp.c_str(), path.c_str()) != 0) {
+        std::remove(tmp.c_str());
+        throw Error("cannot publish the RCCL id file " + path);
+    }
+}
+
+void awaitUid(const std::string& path, double timeoutS, unsigned char* uid)
+{
+    const std::string err = boundedWait(
+        [&]() -> int {
+            FILE* f = std::fopen(path.c_str(), "rb");
+            if (!f) return 1;
+            const std::size_t n = std::fread(uid, 1, 128, f);
+            std::fclose(f);
+            return n == 128 ? 0 : 2;
+        },
+        [&](int) { return std::string("short RCCL id file ") + path; }, timeoutS, "waiting for rank 0's RCCL id");
+    if (!err.empty()) throw Error(err + " (" + path + ")");
+}
+
+std::string uidPath()
+{
+    const char* e = std::getenv("GS_UID_FILE");
+    if (e && *e) return e;
+    const char* port = std::getenv("MASTER_PORT");
+    return "/tmp/gpusolve-uid-" + std::to_string((long)getppid()) + "-" + (port && *port ? port : "0");
 }
 
 // ---------------------------------------------------------------------------------------------

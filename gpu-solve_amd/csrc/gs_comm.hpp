@@ -54,6 +54,15 @@ public:
 std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid);
 void rcclUniqueId(void* uid);
 
+// Sharing rank 0's 128-byte id between the processes of one node without another library (GpuSolve-hip
+// under torchrun): rank 0 writes it to `path` (a temporary file renamed into place, so a reader sees
+// all 128 bytes or nothing), the other ranks poll for it up to timeoutS (gs::Error on timeout).
+// uidPath(): $GS_UID_FILE, else /tmp/gpusolve-uid-<parent pid>-<$MASTER_PORT> — the local ranks of
+// one launcher share its pid, and no live launcher of an earlier run can have the same one.
+void publishUid(const std::string& path, const unsigned char* uid);
+void awaitUid(const std::string& path, double timeoutS, unsigned char* uid);
+std::string uidPath();
+
 // The bounded wait behind RcclComm::sync / settle (host logic, unit-tested on the CPU through
 // gs_debug_bounded_wait). poll() returns 0 done, 1 still pending, or any other value = an error whose
 // text errText(value) gives. Returns "" on completion, else the error / timeout message.

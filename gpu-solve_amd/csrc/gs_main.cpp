@@ -13,13 +13,89 @@
 // reference) are rejected like an invalid mode. With GS_METRICS=1 one more line follows the solve:
 // "[gs] mlups=... gbps=... pct_peak=... vcycle_ms=... cycles=... level_ms=..." (not matched by the
 // reference harness's regex, runExperiments.py:46).
+//
+// Multi-GPU (added): started once per GPU by a launcher that sets WORLD_SIZE / RANK / LOCAL_RANK
+// (`torchrun --nproc-per-node N --no-python GpuSolve-hip <conf>`), each process takes GPU LOCAL_RANK,
+// rank 0's RCCL id reaches the others through a file (gs_comm.hpp uidPath), and the solve runs
+// Z-slab partitioned; rank 0 prints the same stdout. GS_FORCE_RCCL=1 takes that path
+// with one rank too (tests).
+#include <cstdio>
+#include <cstdlib>
 #include <iostream>
+#include <memory>
 #include <string>
+
+#include <fcntl.h>
+#include <unistd.h>
 
 #include <hip/hip_runtime.h>
 
+#include "gs_comm.hpp"
 #include "gs_grid.hpp"
 #include "gs_params.hpp"
+
+namespace {
+int envInt(const char* name, int dflt)
+{
+    const char* e = std::getenv(name);
+    return e && *e ? std::atoi(e) : dflt;
+}
+
+// One process of a multi-GPU run: device, RCCL communicator, Z-slab grid, solve. Throws gs::Error.
+void solveDistributed(const gs::GridParams& gridParams, int rank, int world)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) throw gs::Error("no HIP device");
+    if (hipSetDevice(envInt("LOCAL_RANK", rank) % ndev) != hipSuccess) throw gs::Error("hipSetDevice failed");
+    unsigned char uid[128] = {};
+    const std::string path = gs::uidPath();
+    if (rank == 0) {
+        gs::rcclUniqueId(uid);
+        gs::publishUid(path, uid);
+    } else {
+        gs::awaitUid(path, gs::commTimeoutS("GS_COMM_INIT_TIMEOUT_S", 300.0), uid);
+    }
+    // rank 0 removes the id file when it leaves (every rank's communicator exists by then, or the run failed)
+    struct Cleanup {
+        bool on;
+        std::string p;
+        ~Cleanup()
+        {
+            if (on) std::remove(p.c_str());
+        }
+    } cleanup{rank == 0, path};
+    std::unique_ptr<gs::Comm> comm;
+    {
+        // RCCL prints a version banner to stdout at communicator creation: keep the reference's stdout
+        // contract by sending fd 1 to /dev/null for that call only
+        std::cout.flush();
+        std::fflush(stdout);
+        struct Quiet {
+            int saved = dup(1);
+            Quiet()
+            {
+                const int nul = open("/dev/null", O_WRONLY);
+                if (saved >= 0 && nul >= 0) dup2(nul, 1);
+                if (nul >= 0) close(nul);
+            }
+            ~Quiet()
+            {
+                std::fflush(stdout);
+                if (saved >= 0) {
+                    dup2(saved, 1);
+                    close(saved);
+                }
+            }
+        } quiet;
+        comm = gs::makeRcclComm(rank, world, uid);
+    }
+    gs::HipGridData grid(gridParams, comm.get());
+    grid.printProgress = rank == 0;
+    if (gridParams.mode == gs::GridParams::NEWTON) gs::NewtonSolver::solve(grid);
+    else gs::HipSolver::solve(grid);
+    if (grid.clock.on && rank == 0) std::cout << gs::metricsLine(grid) << '\n';
+}
+} // namespace
 
 int main(int argc, char* argv[])
 {
@@ -35,17 +111,35 @@ int main(int argc, char* argv[])
         std::cerr << '"' << path << "\" does not exist or is not a file\n";
         return 1;
     }
-    std::cout << "Using config file \"" << path << "\"\n";
+    const int world = envInt("WORLD_SIZE", 1), rank = envInt("RANK", 0);
+    const bool distributed = world > 1 || envInt("GS_FORCE_RCCL", 0) != 0;
+    if (rank == 0) std::cout << "Using config file \"" << path << "\"\n";
     if (st == gs::ConfigStatus::InvalidMode) {
         std::cerr << "Invalid mode\n";
         return 1;
     }
-    if (gridParams.mode == gs::GridParams::LINEAR) std::cout << "Solving linear problem\n";
-    else if (gridParams.mode == gs::GridParams::NONLINEAR) std::cout << "Solving nonlinear problem\n";
-    else std::cout << "Solving newton problem\n";
+    if (rank == 0) {
+        if (gridParams.mode == gs::GridParams::LINEAR) std::cout << "Solving linear problem\n";
+        else if (gridParams.mode == gs::GridParams::NONLINEAR) std::cout << "Solving nonlinear problem\n";
+        else std::cout << "Solving newton problem\n";
+    }
     if (st == gs::ConfigStatus::BadStencil) {
         std::cerr << "Invalid stencil offset (must be -1, 0 or 1)\n";
         return 1;
+    }
+
+    if (distributed) {
+        if (rank < 0 || rank >= world) {
+            std::cerr << "Exception: RANK " << rank << " outside WORLD_SIZE " << world << '\n';
+            return 0;
+        }
+        try {
+            solveDistributed(gridParams, rank, world);
+            if (argc > 2 && rank == 0) std::cerr << "(the solution dump is written by single-GPU runs only)\n";
+        } catch (std::exception& e) {
+            std::cerr << "Exception: " << e.what() << '\n';
+        }
+        return 0;
     }
 
     try {

@@ -133,6 +133,8 @@ DRIVER_API = {
                                 C.POINTER(i64)]),
     "gs_zslab_schedule": (C.c_int, [C.POINTER(gs_params), C.c_int, C.c_int, i64, C.c_char_p, i64, C.POINTER(i64)]),
     "gs_rccl_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
+    "gs_uid_publish": (C.c_int, [C.c_char_p, C.POINTER(C.c_ubyte)]),
+    "gs_uid_await": (C.c_int, [C.c_char_p, C.c_double, C.POINTER(C.c_ubyte)]),
     "gs_grid_create_rccl": (C.c_void_p, [C.POINTER(gs_params), C.c_int, C.c_int, C.POINTER(C.c_ubyte)]),
     "gs_zslab_loopback_run": (C.c_int, [C.POINTER(gs_params), C.c_int, i64, C.c_int, C.c_int, dptr, C.c_int,
                                         C.POINTER(C.c_int), dptr]),

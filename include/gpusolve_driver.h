@@ -100,6 +100,11 @@ int gs_rccl_unique_id(unsigned char uid[128]);
  * current HIP device). The other gs_grid_* calls then run the distributed solver; fields and
  * levels describe this rank's slab; rank 0 prints. */
 void* gs_grid_create_rccl(const gs_params* p, int rank, int nranks, const unsigned char uid[128]);
+/* The id's file hand-off of a multi-process GpuSolve-hip run (one launcher, one node): rank 0
+ * publishes (temporary file renamed into place), the others wait up to timeout_s for all 128 bytes.
+ * 0 on success, else non-zero with gs_last_error(). */
+int gs_uid_publish(const char* path, const unsigned char uid[128]);
+int gs_uid_await(const char* path, double timeout_s, unsigned char uid[128]);
 /* Single-process emulation of an nranks Z-slab run on the current device: nranks threads, each a
  * rank with its own slab and streams, device-to-device copies as the exchange. Runs `sweeps`
  * level-0 Jacobi sweeps, then (solve != 0) the solve of p. Writes rank 0's residual history and

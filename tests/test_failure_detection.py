@@ -46,3 +46,51 @@ def test_loopback_hub_abort_unwinds_every_rank(nranks, failing):
     n = d.gs_debug_loopback_abort(nranks, failing)
     assert n == nranks, "a rank thread was left parked in a barrier"
     assert d.gs_last_error().decode() == f"rank {failing} failed"
+
+
+# ---- the RCCL id's file hand-off of a multi-process GpuSolve-hip run (gs_comm.cpp publishUid / awaitUid)
+def _uid(seed):
+    return (C.c_ubyte * 128)(*[(seed * 31 + i * 7) % 256 for i in range(128)])
+
+
+def test_uid_handoff_round_trip(tmp_path):
+    d = gsv.driver()
+    path = str(tmp_path / "uid").encode()
+    sent = _uid(3)
+    assert d.gs_uid_publish(path, sent) == 0
+    got = (C.c_ubyte * 128)()
+    assert d.gs_uid_await(path, 1.0, got) == 0
+    assert bytes(got) == bytes(sent)
+    assert [p.name for p in tmp_path.iterdir()] == ["uid"]  # the temporary file was renamed into place
+
+
+def test_uid_handoff_waits_for_a_late_publisher(tmp_path):
+    import threading
+    d = gsv.driver()
+    path = str(tmp_path / "uid").encode()
+    sent = _uid(5)
+    t = threading.Timer(0.2, lambda: d.gs_uid_publish(path, sent))
+    t.start()
+    got = (C.c_ubyte * 128)()
+    t0 = time.monotonic()
+    assert d.gs_uid_await(path, 10.0, got) == 0
+    t.join()
+    assert bytes(got) == bytes(sent) and time.monotonic() - t0 >= 0.15
+
+
+def test_uid_handoff_times_out(tmp_path):
+    d = gsv.driver()
+    got = (C.c_ubyte * 128)()
+    t0 = time.monotonic()
+    assert d.gs_uid_await(str(tmp_path / "never").encode(), 0.3, got) == 1
+    msg = d.gs_last_error().decode()
+    assert "timed out after" in msg and "RCCL id" in msg
+    assert time.monotonic() - t0 < 5.0
+
+
+def test_uid_handoff_rejects_a_short_file(tmp_path):
+    (tmp_path / "uid").write_bytes(b"x" * 100)
+    d = gsv.driver()
+    got = (C.c_ubyte * 128)()
+    assert d.gs_uid_await(str(tmp_path / "uid").encode(), 1.0, got) == 1
+    assert "short RCCL id file" in d.gs_last_error().decode()

@@ -4,6 +4,7 @@ on the resulting grid, which must be bit-identical to the plain single-GPU grid.
 one GPU under RCCL, so the send/recv halo and the broadcast of replicated levels are covered by the
 loopback communicator (test_gpu_zslab.py) and the 2-rank gloo emulation (test_zslab_cpu.py)."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -65,3 +66,30 @@ def test_rccl_bad_rank_rejected():
     p = gsv.GridParams(maxiter=1, gridDim=(8, 8, 8)).to_abi()
     assert not drv.gs_grid_create_rccl(C.byref(p), 1, 1, uid)
     assert b"bad arguments" in drv.gs_last_error()
+
+
+def test_executable_rccl_path_matches_reference_stdout(tmp_path):
+    """GpuSolve-hip's multi-process path (WORLD_SIZE / RANK from a launcher, RCCL id through a file) with
+    one rank (GS_FORCE_RCCL=1): the reference's stdout line for line, as the single-GPU path, and the id
+    file removed afterwards. (Two or more ranks need as many GPUs: RCCL refuses two ranks on one.)"""
+    import re
+    import subprocess
+    from conftest import load_json
+    from test_gpu_solver import _norm_lines, params_from_case
+    exe = gsv._abi.EXECUTABLE
+    uid = tmp_path / "uid"
+    env = dict(os.environ, GS_FORCE_RCCL="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", GS_UID_FILE=str(uid))
+    cases = load_json("stdout.json")
+    for name in ("m0_n31_2+2", "m1_n15_2+2", "example_data-2nd_order"):
+        case = cases[name]
+        conf = tmp_path / f"{name}.conf"
+        conf.write_text(params_from_case(case["config"]).config_text())
+        out = subprocess.run([exe, str(conf)], capture_output=True, text=True, timeout=300, env=env)
+        assert out.returncode == 0 and "Exception" not in out.stderr, out.stderr
+        assert _norm_lines(out.stdout.splitlines()) == case["stdout"], (name, out.stdout)
+        assert not uid.exists()
+    # a rank outside the world is an error line, not a hang
+    bad = dict(env, WORLD_SIZE="2", RANK="5")
+    conf = tmp_path / "m0_n31_2+2.conf"
+    out = subprocess.run([exe, str(conf)], capture_output=True, text=True, timeout=60, env=bad)
+    assert out.returncode == 0 and re.search(r"Exception: RANK 5 outside WORLD_SIZE 2", out.stderr)
