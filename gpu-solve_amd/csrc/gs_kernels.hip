@@ -2350,6 +2350,13 @@ int slab_zc()
     return e && *e ? std::atoi(e) : 0;
 }
 
+// the same for plane ranges from a level's first plane (whole single-GPU levels of >= 2^26 points); A/B
+int whole_zc()
+{
+    const char* e = getenv("GS_PAIR_ZC");
+    return e && *e ? std::atoi(e) : 0;
+}
+
 int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
              int mode = GS_LINEAR, bool* xh = nullptr)
 {
@@ -2399,6 +2406,9 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
         if (L->z0 != 0) {
             const int sz = slab_zc();
             if (sz > 0) c = sz;
+        } else {
+            const int wz = whole_zc();
+            if (wz > 0) c = wz;
         }
     }
     c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)

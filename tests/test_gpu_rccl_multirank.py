@@ -1,0 +1,120 @@
+"""RCCL between ranks, on one GPU: 2-3 processes (one per rank, as bench.py and GpuSolve-hip run at N > 1)
+build their Z-slabs with gs_grid_create_rccl and solve; the assembled level-0 field must be bit-identical
+to the single-GPU solve and the history agree to 1e-12 (rank partials of the norm summed in rank order).
+
+RCCL refuses two ranks on one GPU of one host ("Duplicate GPU detected"); a distinct NCCL_HOSTID per
+process makes each rank its own host, so the ranks connect through RCCL's socket transport over loopback
+(NCCL_SOCKET_IFNAME=lo) instead of xGMI. The transport differs from the 8-GPU node's; everything above it
+— the non-blocking communicator's init and settle loop, the grouped ghost-plane send/recv of the
+overlapped sweeps, the in-place broadcast group that assembles replicated levels, the norm allgather —
+is the product's own code (gs_comm.cpp, gs_grid.cpp) moving real bytes between ranks."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO, rel
+
+pytestmark = pytest.mark.gpu
+
+# torch before the library, as in every GPU test module: the process then runs one HIP runtime (torch's
+# bundled libamdhip64.so.7, which the library's same-soname dependency resolves to) for its whole life
+torch = pytest.importorskip("torch")
+import gpusolve as gsv  # noqa: E402
+PROBE = os.path.join(REPO, "tests", "rccl_rank_probe.py")
+
+
+def rank_env(rank, world, extra=None):
+    env = dict(os.environ)
+    env.update({"NCCL_HOSTID": f"gs-test-rank-{rank}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1",
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0", "WORLD_SIZE": str(world), "RANK": str(rank),
+                "LOCAL_RANK": "0", "GS_COMM_INIT_TIMEOUT_S": "90", "GS_COMM_TIMEOUT_S": "60"})
+    env.update(extra or {})
+    return env
+
+
+def run_ranks(tmp_path, world, mode, dims, maxiter, extra=None):
+    uid = str(tmp_path / "uid")
+    procs = []
+    for r in range(world):
+        out = str(tmp_path / f"rank{r}.npz")
+        args = [sys.executable, PROBE, out, str(r), str(world), uid, str(mode), *map(str, dims), str(maxiter)]
+        procs.append((subprocess.Popen(args, env=rank_env(r, world, extra), stdout=subprocess.PIPE,
+                                       stderr=subprocess.PIPE, text=True), out))
+    errs = []
+    for p, _ in procs:
+        try:
+            _, err = p.communicate(timeout=150)
+        except subprocess.TimeoutExpired:
+            for q, _ in procs:
+                q.kill()
+            raise
+        if p.returncode != 0:
+            errs.append(err[-3000:])
+    assert not errs, "\n---\n".join(errs)
+    parts = [np.load(o) for _, o in procs]
+    parts.sort(key=lambda d: int(d["z0"]))
+    z = 0
+    for d in parts:  # the slabs tile the z axis in rank order
+        assert int(d["z0"]) == z, (int(d["z0"]), z)
+        z += d["v"].shape[2]
+    assert z == dims[2]
+    hists = [list(d["hist"]) for d in parts]
+    assert all(h == hists[0] for h in hists), "ranks disagree on the history"
+    return hists[0], np.concatenate([d["v"] for d in parts], axis=2)
+
+
+def single(mode, dims, maxiter):
+    p = gsv.GridParams(maxiter=maxiter, tol=0.0, gridDim=dims, mode=mode)
+    with gsv.HipGridData(p) as g:
+        h = gsv.NewtonSolver.solve(g) if mode == 2 else gsv.HipSolver.solve(g)
+        v = g.field(0, "v")[:, :, 1:-1]
+    return h, v
+
+
+@pytest.mark.parametrize("world,mode,dims,maxiter,extra", [
+    (2, 0, (32, 32, 32), 4, None),
+    (2, 1, (31, 33, 40), 4, None),
+    (2, 2, (32, 32, 32), 2, None),
+    # slabs large enough for the fused pairs, their depth-2 ghosts and the overlapped boundary planes;
+    # levels kept partitioned down to 8^3 points (GS_ZSLAB_MIN_POINTS) and the default agglomeration
+    (2, 0, (64, 256, 64), 3, {"GS_ZSLAB_MIN_POINTS": "512"}),
+    (2, 0, (64, 256, 64), 3, None),
+    (3, 0, (48, 512, 70), 3, None),
+    (3, 1, (40, 24, 50), 3, None),
+])
+def test_rccl_ranks_match_single_gpu(tmp_path, world, mode, dims, maxiter, extra):
+    h, v = run_ranks(tmp_path, world, mode, dims, maxiter, extra)
+    ref_h, ref_v = single(mode, dims, maxiter)
+    assert len(h) == len(ref_h)
+    for a, b in zip(h, ref_h):
+        assert rel(a, b) < 1e-12, (a, b)
+    np.testing.assert_array_equal(v, ref_v)
+
+
+def test_executable_two_ranks_match_reference_stdout(tmp_path):
+    """GpuSolve-hip under a launcher's WORLD_SIZE / RANK with two real ranks: rank 0 prints the
+    reference's stdout line for line (the other rank prints nothing), both exit 0."""
+    from conftest import load_json
+    from test_gpu_solver import _norm_lines, params_from_case
+    exe = gsv._abi.EXECUTABLE
+    case = load_json("stdout.json")["m0_n31_2+2"]
+    conf = tmp_path / "m0.conf"
+    conf.write_text(params_from_case(case["config"]).config_text())
+    uid = str(tmp_path / "uid")
+    procs = [subprocess.Popen([exe, str(conf)], env=rank_env(r, 2, {"GS_UID_FILE": uid}), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=150))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0 and "Exception" not in e, e[-3000:]
+    assert _norm_lines(outs[0][0].splitlines()) == case["stdout"], outs[0][0]
+    assert outs[1][0].strip() == "", outs[1][0]
