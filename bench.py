@@ -427,7 +427,9 @@ def main():
     total_lups = lups_per_rank * a.steps * world
     value = total_lups / elapsed / 1e6
     achieved = BYTES_PER_LUP * lups_per_rank / (kernel_ms * 1e-3) / 1e9
-    traffic, pmc = pmc_traffic(n)
+    # the committed PMC summary is of the N=1 grid's pair (512^3, k_tb2y); a rank's slab at N > 1 is another
+    # launch shape (config #5: 1024x1024x128, column blocks; its counters: profiles/r02h_pmc_level0.md)
+    traffic, pmc = pmc_traffic(n) if world == 1 else (None, None)
     import ctypes as C
     pair_kernel = gsv.kernels().gs_jacobi_sweep2_kernel(C.byref(grid.params.stencil.to_abi()),
                                                         C.byref(grid.getLevel(0).geom), 0).decode()

@@ -1,8 +1,7 @@
 """The RCCL communicator on ONE GPU (one rank): ncclGetUniqueId / ncclCommInitRank through the C ABI
 (gs_rccl_unique_id, gs_grid_create_rccl — the calls bench.py makes on every rank at N > 1) and a solve
-on the resulting grid, which must be bit-identical to the plain single-GPU grid. Two ranks cannot share
-one GPU under RCCL, so the send/recv halo and the broadcast of replicated levels are covered by the
-loopback communicator (test_gpu_zslab.py) and the 2-rank gloo emulation (test_zslab_cpu.py)."""
+on the resulting grid, which must be bit-identical to the plain single-GPU grid. Send/recv halos and
+the broadcast of replicated levels between real rank processes: test_gpu_rccl_multirank.py."""
 import ctypes as C
 import os
 
@@ -71,7 +70,7 @@ def test_rccl_bad_rank_rejected():
 def test_executable_rccl_path_matches_reference_stdout(tmp_path):
     """GpuSolve-hip's multi-process path (WORLD_SIZE / RANK from a launcher, RCCL id through a file) with
     one rank (GS_FORCE_RCCL=1): the reference's stdout line for line, as the single-GPU path, and the id
-    file removed afterwards. (Two or more ranks need as many GPUs: RCCL refuses two ranks on one.)"""
+    file removed afterwards (two ranks: test_gpu_rccl_multirank.py)."""
     import re
     import subprocess
     from conftest import load_json
