@@ -2399,6 +2399,14 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
             int64_t c1 = (L->nz + per - 1) / per;
             c1 += c1 & 1;
             if (c1 > c) c = c1;
+        } else if (one_round && colb && tiles > cus && L->z0 == 0) {
+            // more tiles than CUs (1024^3: 512 column-block tiles): chunks for four rounds of blocks where
+            // that lengthens them (1024^3: 512 planes, pair 4.90 vs 5.00-5.06 ms, tools/zc_sweep.sh,
+            // profiles/r02k; a 1024x1024x128 slab keeps its 128-plane chunks, 0.622 vs 0.641 ms at 64)
+            const int64_t per = std::max<int64_t>(1, 4 * cus / tiles);
+            int64_t c1 = (L->nz + per - 1) / per;
+            c1 += c1 & 1;
+            if (c1 > c) c = c1;
         }
         // plane ranges past a slab's first plane (the interior launch of an overlapped Z-slab sweep):
         // GS_SLAB_ZC-plane chunks, so that blocks retire often and the ghost exchange's kernels
