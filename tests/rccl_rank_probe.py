@@ -1,6 +1,8 @@
 """One rank of a multi-process RCCL Z-slab solve (child process of tests/test_gpu_rccl_multirank.py).
 
-    python rccl_rank_probe.py <out.npz> <rank> <world> <uid file> <mode> <nx> <ny> <nz> <maxiter>
+    python rccl_rank_probe.py <out.npz> <rank> <world> <uid file> <mode> <nx> <ny> <nz> <maxiter> [die]
+
+(`die`: the last rank leaves right after its communicator and slab exist — a peer lost mid-run.)
 
 Rank 0 creates the RCCL id and publishes it through the file (gs_uid_publish, as GpuSolve-hip's launcher
 path does), the others wait for it (gs_uid_await); every rank then builds its slab with
@@ -37,6 +39,8 @@ def main():
     g.handle = drv.gs_grid_create_rccl(C.byref(g._abi_params), rank, world, uid)
     if not g.handle:
         raise SystemExit("gs_grid_create_rccl: " + drv.gs_last_error().decode())
+    if len(sys.argv) > 10 and sys.argv[10] == "die" and rank == world - 1:
+        os._exit(3)
     try:
         hist = gsv.NewtonSolver.solve(g) if mode == 2 else gsv.HipSolver.solve(g)
         geom = g.getLevel(0).geom

@@ -35,14 +35,20 @@ def rank_env(rank, world, extra=None):
     return env
 
 
-def run_ranks(tmp_path, world, mode, dims, maxiter, extra=None):
+def start_ranks(tmp_path, world, mode, dims, maxiter, extra=None, die=False):
     uid = str(tmp_path / "uid")
     procs = []
     for r in range(world):
         out = str(tmp_path / f"rank{r}.npz")
         args = [sys.executable, PROBE, out, str(r), str(world), uid, str(mode), *map(str, dims), str(maxiter)]
+        args += ["die"] if die else []
         procs.append((subprocess.Popen(args, env=rank_env(r, world, extra), stdout=subprocess.PIPE,
                                        stderr=subprocess.PIPE, text=True), out))
+    return procs
+
+
+def run_ranks(tmp_path, world, mode, dims, maxiter, extra=None):
+    procs = start_ranks(tmp_path, world, mode, dims, maxiter, extra)
     errs = []
     for p, _ in procs:
         try:
@@ -118,3 +124,25 @@ def test_executable_two_ranks_match_reference_stdout(tmp_path):
         assert p.returncode == 0 and "Exception" not in e, e[-3000:]
     assert _norm_lines(outs[0][0].splitlines()) == case["stdout"], outs[0][0]
     assert outs[1][0].strip() == "", outs[1][0]
+
+
+def test_lost_peer_is_an_error_not_a_hang(tmp_path):
+    """Rank 1 leaves right after the communicator and its slab exist; rank 0's solve must not wait for
+    it forever: its bounded wait (GS_COMM_TIMEOUT_S) or RCCL's own error report aborts the communicator
+    and the solve fails with the RCCL message GpuSolve-hip would print after "Exception: "."""
+    import time
+    t0 = time.time()
+    procs = start_ranks(tmp_path, 2, 0, (64, 64, 64), 50, {"GS_COMM_TIMEOUT_S": "20"}, die=True)
+    res = []
+    for p, _ in procs:
+        try:
+            res.append(p.communicate(timeout=150))
+        except subprocess.TimeoutExpired:
+            for q, _ in procs:
+                q.kill()
+            raise
+    assert procs[1][0].returncode == 3
+    assert procs[0][0].returncode not in (0, None), res[0][1][-2000:]
+    err = res[0][1]
+    assert "RCCL" in err and "rank 0 of 2" in err and "aborted" in err, err[-2000:]
+    assert time.time() - t0 < 140
