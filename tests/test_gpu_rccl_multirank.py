@@ -1,4 +1,4 @@
-"""RCCL between ranks, on one GPU: 2-3 processes (one per rank, as bench.py and GpuSolve-hip run at N > 1)
+"""RCCL between ranks, on one GPU: 2-8 processes (one per rank, as bench.py and GpuSolve-hip run at N > 1)
 build their Z-slabs with gs_grid_create_rccl and solve; the assembled level-0 field must be bit-identical
 to the single-GPU solve and the history agree to 1e-12 (rank partials of the norm summed in rank order).
 
@@ -90,6 +90,9 @@ def single(mode, dims, maxiter):
     (2, 0, (64, 256, 64), 3, None),
     (3, 0, (48, 512, 70), 3, None),
     (3, 1, (40, 24, 50), 3, None),
+    # the driver's 8-GPU rank count (config #5 decomposes 1024^3 the same way: 8 slabs, default agglomeration)
+    (8, 0, (64, 96, 256), 3, None),
+    (4, 2, (32, 32, 64), 2, None),
 ])
 def test_rccl_ranks_match_single_gpu(tmp_path, world, mode, dims, maxiter, extra):
     h, v = run_ranks(tmp_path, world, mode, dims, maxiter, extra)
