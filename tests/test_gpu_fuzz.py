@@ -4,6 +4,8 @@ grid shapes from 2 to 70 points per axis (power-of-two and odd, flat and long), 
 must be bit-identical in LINEAR mode and within 1e-10 (ocml vs glibc exp) otherwise; the histories
 within 1e-12 / 1e-9. Every case exercises a different mix of fused pairs, single sweeps, zero-iterate
 sweeps, one-point small-level kernels, the coarse-cycle launch and the overlapped solve loop."""
+import os
+
 import numpy as np
 import pytest
 
@@ -18,7 +20,10 @@ from conftest import rel  # noqa: E402
 CANON = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
 
 
-def cases(n=150, seed=20261016):
+def cases(n=None, seed=None):
+    # GS_FUZZ_N / GS_FUZZ_SEED: a longer or different draw (the default run: 150 cases, the seed below)
+    n = int(os.environ.get("GS_FUZZ_N", 150)) if n is None else n
+    seed = int(os.environ.get("GS_FUZZ_SEED", 20261016)) if seed is None else seed
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
