@@ -16,6 +16,9 @@
 #ifndef GS_PRO_EXP
 #define GS_PRO_EXP 0
 #endif
+#ifndef GS_PRO_HALF
+#define GS_PRO_HALF 1 // fused prolongation: halved X-pass rows formed once per coarse row (0: per fine point)
+#endif
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -1685,6 +1688,12 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 #pragma unroll
     for (int r = 0; r < NCR; r++) crow[r] = (int64_t)min(max(cyb + r, 0), cny + 1) * cldy;
     double2 W0[NCR], W1[NCR], Wm[NCR]; // X-pass values of coarse planes K, K+1 (Wm: K-1, first step)
+    // HALF: the same rows times 0.5, the product every Y and Z pass of the reference takes of them first
+    // (0.5 * fine(y-1) + 0.5 * fine(y+1) with fine(y+-1) an X-pass value; 0.5 * fine(z) + 0.5 * fine(z+2)
+    // with fine(z), fine(z+2) X-pass values on even rows): formed once per coarse row instead of at every
+    // fine point that reads it — the same products, so the same bits
+    constexpr bool HALF = !RECOMP && GS_PRO_HALF;
+    double2 H0[HALF ? NCR : 1], H1[HALF ? NCR : 1], Hm[HALF ? NCR : 1];
     // NEWTON (RECOMP): the X-pass rows of planes K, K+1 live in LDS, slot wsl / wsl^1 — each lane
     // reads back only what it wrote, so no barrier; this keeps the variant inside 256 VGPRs
     __shared__ double2 wlds[RECOMP ? 2 : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? NCR : 1][RECOMP ? WAVE : 1];
@@ -1696,6 +1705,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         if constexpr (RECOMP) return wlds[s ^ wsl][wid_l][r][lane];
         else return s == 0 ? W0[r] : W1[r];
     };
+    auto hget = [&](int s, int r) -> double2 { return s == 2 ? Hm[HALF ? r : 0] : (s == 0 ? H0[HALF ? r : 0] : H1[HALF ? r : 0]); };
     double RA[NCR], RB[NCR], SA[NCR], SB[NCR]; // raw c (and sub) of plane K+2, in flight
     auto craw = [&](int cz) {
         // coarse planes -1 .. cnz+2 exist in the layout; only those under corrected fine planes matter
@@ -1716,6 +1726,12 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         for (int r = 0; r < NCR; r++) {
             const double a = PRO == 2 ? RA[r] - SA[r] : RA[r], b = PRO == 2 ? RB[r] - SB[r] : RB[r];
             const double2 X = make_double2(0.5 * a + 0.5 * b, b);
+            if constexpr (HALF) {
+                const double2 Hh = make_double2(0.5 * X.x, 0.5 * X.y);
+                if (s == 2) Hm[r] = Hh;
+                else if (s == 0) H0[r] = Hh;
+                else H1[r] = Hh;
+            }
             if (s == 2) Wm[r] = X;
             else if constexpr (RECOMP) wlds[s ^ wsl][wid_l][r][lane] = X;
             else if (s == 0) W0[r] = X;
@@ -1735,10 +1751,23 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             const double2 X1 = wget(s, ri + 1);
             return make_double2(0.5 * X0.x + 0.5 * X1.x, 0.5 * X0.y + 0.5 * X1.y);
         };
-        double2 e = ypass(sa);
-        if (zodd) {
-            const double2 g = ypass(sb);
-            e = make_double2(0.5 * e.x + 0.5 * g.x, 0.5 * e.y + 0.5 * g.y);
+        double2 e;
+        if constexpr (HALF) {
+            auto hsum = [](double2 p, double2 q) { return make_double2(p.x + q.x, p.y + q.y); };
+            if (!zodd) {
+                e = yodd ? hsum(hget(sa, ri), hget(sa, ri + 1)) : wget(sa, ri);
+            } else if (!yodd) {
+                e = hsum(hget(sa, ri), hget(sb, ri));
+            } else {
+                const double2 ea = hsum(hget(sa, ri), hget(sa, ri + 1)), eb = hsum(hget(sb, ri), hget(sb, ri + 1));
+                e = make_double2(0.5 * ea.x + 0.5 * eb.x, 0.5 * ea.y + 0.5 * eb.y);
+            }
+        } else {
+            e = ypass(sa);
+            if (zodd) {
+                const double2 g = ypass(sb);
+                e = make_double2(0.5 * e.x + 0.5 * g.x, 0.5 * e.y + 0.5 * g.y);
+            }
         }
         if (zin && rowc[j + 1]) {
             if (okx0) val.x = val.x + e.x;
@@ -1970,6 +1999,10 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                 } else {
 #pragma unroll
                     for (int r = 0; r < NCR; r++) W0[r] = W1[r];
+                    if constexpr (HALF) {
+#pragma unroll
+                        for (int r = 0; r < NCR; r++) H0[r] = H1[r];
+                    }
                 }
                 xpass(1);
             }

@@ -1,5 +1,6 @@
 """Timing-only: the 512^3 level-0 prolongation pair and the plain pair from the product library and
-from the GS_PRO_EXP builds (tools/pro_exp_build.sh), interleaved, HIP events on one stream.
+from the GS_PRO_EXP builds (tools/pro_exp_build.sh; exp4 = GS_PRO_HALF=0, whose output must equal the
+product's bit for bit), interleaved, HIP events on one stream.
     python tools/pro_exp.py [reps]"""
 import ctypes as C
 import json
@@ -16,7 +17,7 @@ from gpusolve.devfield import DevField  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 libs = {"prod": gsv.kernels()}
-for e in (1, 2, 3):
+for e in (1, 2, 3, 4):
     p = os.path.join(HERE, "..", "gpu-solve_amd", "build", "exp", f"libgs_exp{e}.so")
     if os.path.exists(p):
         lib = C.CDLL(p, mode=C.RTLD_LOCAL)
@@ -63,5 +64,15 @@ with gsv.HipGridData(prm) as grid:
                 ms = timed(fn)
                 out.setdefault(f"{name}_{kind}", []).append(round(ms, 4))
                 print(f"rep {r} {name:5s} {kind:4s} {ms:.4f} ms", flush=True)
+    if "exp4" in libs:  # the A/B pair of builds computes the same bits
+        res = {}
+        for name in ("prod", "exp4"):
+            assert libs[name].gs_jacobi_sweep2_prolong(C.byref(S), C.byref(L0), 0, prm.omega, prm.gamma, v, cv, None,
+                                                       C.byref(L1), o.ptr, f, None, 0, 0, st) == 0
+            torch.cuda.synchronize()
+            res[name] = o.to_xyz().copy()
+        same = res["prod"].tobytes() == res["exp4"].tobytes()
+        out["prod_vs_exp4_bit_identical"] = [same]
+        print("prod vs exp4 (GS_PRO_HALF=0) bit-identical:", same, flush=True)
     del o
 print(json.dumps({k: sorted(v)[len(v) // 2] for k, v in out.items()}))
