@@ -21,7 +21,7 @@ for e in (1, 2, 3, 4):
     p = os.path.join(HERE, "..", "gpu-solve_amd", "build", "exp", f"libgs_exp{e}.so")
     if os.path.exists(p):
         lib = C.CDLL(p, mode=C.RTLD_LOCAL)
-        for name in ("gs_jacobi_sweep2_prolong", "gs_jacobi_sweep2"):
+        for name in ("gs_jacobi_sweep2_prolong", "gs_jacobi_sweep2", "gs_residual_restrict"):
             res, args = _abi.KERNEL_API[name]
             getattr(lib, name).restype, getattr(lib, name).argtypes = res, args
         libs[f"exp{e}"] = lib
@@ -60,7 +60,10 @@ with gsv.HipGridData(prm) as grid:
             def pair():
                 assert lib.gs_jacobi_sweep2(C.byref(S), C.byref(L0), 0, prm.omega, prm.gamma, v, o.ptr, f, None,
                                             0, 0, st) == 0
-            for kind, fn in (("pro", pro), ("pair", pair)):
+            def rr():
+                assert lib.gs_residual_restrict(C.byref(S), C.byref(L0), 0, prm.gamma, v, f, None, o.ptr, None,
+                                                C.byref(L1), st) == 0
+            for kind, fn in (("pro", pro), ("pair", pair), ("rr", rr)):
                 ms = timed(fn)
                 out.setdefault(f"{name}_{kind}", []).append(round(ms, 4))
                 print(f"rep {r} {name:5s} {kind:4s} {ms:.4f} ms", flush=True)
