@@ -216,8 +216,12 @@ def vcycle_level0_kernels(grid, k):
 
     res = {}
     for name, fn, bpp in (("residual_restrict", rr, 17.0), ("prolong_pair", pro, 25.0)):
-        for _ in range(2):
+        try:
             fn()
+        except AssertionError:  # e.g. rows > 512 points: the solver prolongs unfused there
+            res[name] = {"error": "no fused kernel for this level shape"}
+            continue
+        fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(k):
