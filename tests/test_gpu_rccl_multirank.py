@@ -101,6 +101,10 @@ def single(mode, dims, maxiter):
     # the driver's 8-GPU rank count (config #5 decomposes 1024^3 the same way: 8 slabs, default agglomeration)
     (8, 0, (64, 96, 256), 3, None),
     (4, 2, (32, 32, 64), 2, None),
+    # larger slabs: two 256^3 ranks (one-round chunks on rank 0, the slab rule past it), and BASELINE
+    # config #3's grid on 8 ranks (512x512x64 slabs)
+    (2, 0, (256, 256, 512), 3, None),
+    (8, 0, (512, 512, 512), 2, None),
 ])
 def test_rccl_ranks_match_single_gpu(tmp_path, world, mode, dims, maxiter, extra):
     h, v = run_ranks(tmp_path, world, mode, dims, maxiter, extra)
