@@ -2,7 +2,8 @@
 
     python rccl_rank_probe.py <out.npz> <rank> <world> <uid file> <mode> <nx> <ny> <nz> <maxiter> [die]
 
-(`die`: the last rank leaves right after its communicator and slab exist — a peer lost mid-run.)
+(`die`: the last rank leaves right after its communicator and slab exist — a peer lost mid-run;
+`digest`: save a SHA-1 per owned z-plane of level 0's interior v instead of the planes — config #5's size.)
 
 Rank 0 creates the RCCL id and publishes it through the file (gs_uid_publish, as GpuSolve-hip's launcher
 path does), the others wait for it (gs_uid_await); every rank then builds its slab with
@@ -20,6 +21,12 @@ import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gpu-solve_amd"))
 import gpusolve as gsv  # noqa: E402
+
+
+def plane_digests(v):
+    """SHA-1 of every z-plane's interior (x, y) values of a field indexed [x][y][z]."""
+    import hashlib
+    return [hashlib.sha1(np.ascontiguousarray(v[1:-1, 1:-1, k]).tobytes()).hexdigest() for k in range(v.shape[2])]
 
 
 def main():
@@ -45,7 +52,11 @@ def main():
         hist = gsv.NewtonSolver.solve(g) if mode == 2 else gsv.HipSolver.solve(g)
         geom = g.getLevel(0).geom
         v = g.field(0, "v")[:, :, 1:geom.nz + 1]
-        np.savez(out, v=v, z0=geom.z0, hist=np.array(hist, dtype=np.float64))
+        if len(sys.argv) > 10 and sys.argv[10] == "digest":
+            np.savez(out, digests=np.array(plane_digests(v)), nz=geom.nz, z0=geom.z0,
+                     hist=np.array(hist, dtype=np.float64))
+        else:
+            np.savez(out, v=v, z0=geom.z0, hist=np.array(hist, dtype=np.float64))
     finally:
         g.close()
 

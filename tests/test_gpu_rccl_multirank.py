@@ -36,13 +36,13 @@ def rank_env(rank, world, extra=None):
     return env
 
 
-def start_ranks(tmp_path, world, mode, dims, maxiter, extra=None, die=False):
+def start_ranks(tmp_path, world, mode, dims, maxiter, extra=None, die=False, digest=False):
     uid = str(tmp_path / "uid")
     procs = []
     for r in range(world):
         out = str(tmp_path / f"rank{r}.npz")
         args = [sys.executable, PROBE, out, str(r), str(world), uid, str(mode), *map(str, dims), str(maxiter)]
-        args += ["die"] if die else []
+        args += ["die"] if die else (["digest"] if digest else [])
         procs.append((subprocess.Popen(args, env=rank_env(r, world, extra), stdout=subprocess.PIPE,
                                        stderr=subprocess.PIPE, text=True), out))
     return procs
@@ -184,3 +184,32 @@ def test_rccl_random_vs_single_gpu(tmp_path, case):
     ref_h, ref_v = single(mode, dims, maxiter)
     same_history(h, ref_h)
     np.testing.assert_array_equal(v, ref_v)
+
+
+def test_rccl_config5_eight_ranks_match_single_gpu(tmp_path):
+    """BASELINE config #5's decomposition over RCCL: 1024^3 linear 2+2 on 8 rank processes (1024x1024x128
+    slabs, column-block pairs, default agglomeration), 2 V-cycles; every owned plane of level 0 bit for bit
+    (SHA-1 per plane) against the single-GPU 1024^3 solve, histories to 1e-12."""
+    import rccl_rank_probe as probe
+    dims, world, maxiter = (1024, 1024, 1024), 8, 2
+    procs = start_ranks(tmp_path, world, 0, dims, maxiter, digest=True)
+    errs = []
+    for p, _ in procs:
+        try:
+            _, err = p.communicate(timeout=280)
+        except subprocess.TimeoutExpired:
+            for q, _ in procs:
+                q.kill()
+            raise
+        if p.returncode != 0:
+            errs.append(err[-3000:])
+    assert not errs, "\n---\n".join(errs)
+    parts = sorted((np.load(o) for _, o in procs), key=lambda d: int(d["z0"]))
+    hists = [list(d["hist"]) for d in parts]
+    assert all(np.array_equal(h, hists[0]) for h in hists)
+    ref_h, ref_v = single(0, dims, maxiter)
+    same_history(hists[0], ref_h)
+    ref = probe.plane_digests(ref_v)
+    got = [h for d in parts for h in d["digests"]]
+    assert len(got) == dims[2] and [int(d["z0"]) for d in parts] == [128 * r for r in range(world)]
+    assert got == ref
