@@ -21,6 +21,7 @@
 // with one rank too (tests).
 #include <cstdio>
 #include <cstdlib>
+#include <iomanip>
 #include <iostream>
 #include <memory>
 #include <string>
@@ -108,12 +109,12 @@ int main(int argc, char* argv[])
     // read the mode first so the "Using"/"Solving" lines come out in the reference's order
     const gs::ConfigStatus st = gs::readConfig(path, gridParams);
     if (st == gs::ConfigStatus::NotAFile) {
-        std::cerr << '"' << path << "\" does not exist or is not a file\n";
+        std::cerr << std::quoted(path) << " does not exist or is not a file\n";
         return 1;
     }
     const int world = envInt("WORLD_SIZE", 1), rank = envInt("RANK", 0);
     const bool distributed = world > 1 || envInt("GS_FORCE_RCCL", 0) != 0;
-    if (rank == 0) std::cout << "Using config file \"" << path << "\"\n";
+    if (rank == 0) std::cout << "Using config file " << std::quoted(path) << '\n';
     if (st == gs::ConfigStatus::InvalidMode) {
         std::cerr << "Invalid mode\n";
         return 1;

@@ -10,6 +10,7 @@ Outputs (all data, no reference source):
   histories.json        17-digit residual histories, keyed by case name (+ the case's config)
   large_histories.json  the BASELINE-size anchors (511^3/512^3), a few cycles each   (--large)
   stdout.json           6-digit reference stdout transcripts (timings stripped)
+  paths.json            reference stdout/stderr/exit code for quoted/escaped and missing config paths
   levels.json           level dims + h for several grid shapes
   rhs.npz               level-0 f for linear / non-linear RHS on small grids
   ops.npz               per-operator fixtures (inputs + outputs, reference layout (Px,Py,Pz))
@@ -173,6 +174,36 @@ def gen_stdout(path):
         json.dump(res, f, indent=1)
 
 
+PATH_CASES = {
+    # relative config paths (the executable runs with cwd = a scratch dir): std::filesystem::path's
+    # operator<< goes through std::quoted, so '"' and '\\' come out escaped (src/main.cpp:24,28)
+    "plain": "plain.conf",
+    "space_backslash_quote": 'my conf\\dir "x".conf',
+    "trailing_backslash": "end\\",
+    "quotes_only": '""',
+    "missing": 'no such\\"file.conf',
+    "missing_dir": "nodir/",
+}
+
+
+def gen_paths(path):
+    """Reference stdout/stderr/exit code for config paths with a space, backslash and double quote,
+    and for missing paths (round-3 verdict item 1)."""
+    res = {}
+    c = case(7, maxiter=2)
+    with tempfile.TemporaryDirectory() as td:
+        for name, rel in PATH_CASES.items():
+            if not name.startswith("missing"):
+                with open(os.path.join(td, rel), "w") as f:
+                    f.write(config_text(c))
+            p = subprocess.run([REFEXE, rel], cwd=td, capture_output=True, text=True)
+            res[name] = {"path": rel, "config": None if name.startswith("missing") else c,
+                         "stdout": [re.sub(r"Took \d+ms", "Took <T>ms", l) for l in p.stdout.splitlines()],
+                         "stderr": p.stderr.splitlines(), "returncode": p.returncode}
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
+
+
 def gen_levels(path):
     res = {}
     for dims in ((7, 7, 7), (16, 16, 16), (127, 127, 127), (128, 128, 128), (512, 512, 512), (1024, 1024, 1024),
@@ -286,6 +317,7 @@ def main():
     ap.add_argument("--only-large", action="store_true")
     ap.add_argument("--only-dumps", action="store_true")
     ap.add_argument("--config3", action="store_true", help="only the 10-cycle 511^3/512^3 anchors")
+    ap.add_argument("--only-paths", action="store_true", help="only the config-path quoting transcripts")
     ap.add_argument("--huge", action="store_true", help="only the 1023^3/1024^3 anchors (~55 GiB of host RAM)")
     a = ap.parse_args()
     if a.config3:
@@ -297,6 +329,9 @@ def main():
     for exe in (PROBE, REFEXE):
         if not os.path.exists(exe):
             sys.exit(f"{exe} missing: run `make -C oracle ref` (needs /root/reference)")
+    if a.only_paths:
+        gen_paths(os.path.join(HERE, "paths.json"))
+        return
     if a.only_dumps:
         gen_dumps(os.path.join(HERE, "dumps.json"))
         return
@@ -307,6 +342,7 @@ def main():
         gen_histories(small_cases(), os.path.join(HERE, "histories.json"))
         print("stdout ...", flush=True)
         gen_stdout(os.path.join(HERE, "stdout.json"))
+        gen_paths(os.path.join(HERE, "paths.json"))
         print("levels ...", flush=True)
         gen_levels(os.path.join(HERE, "levels.json"))
         print("rhs ...", flush=True)

@@ -107,3 +107,25 @@ def test_executable_argument_errors(tmp_path):
     r = subprocess.run([exe, str(conf)], capture_output=True, text=True)
     assert r.returncode == 1 and "Invalid mode" in r.stderr
     assert r.stdout.startswith(f'Using config file "{conf}"')
+
+
+def test_executable_config_path_quoting_without_gpu(tmp_path):
+    """src/main.cpp:24,28 stream a std::filesystem::path, i.e. through std::quoted ('"' and '\\' escaped).
+    Byte-for-byte against the reference executable's transcripts (tests/golden/paths.json) for the cases
+    that end before any device work: missing paths, and the 'Using config file' line of every other
+    path (checked here on an invalid-mode copy of the config, which exits before the solve)."""
+    from conftest import load_json
+    exe = gsv._abi.EXECUTABLE
+    for name, case in load_json("paths.json").items():
+        rel_path = case["path"]
+        if case["config"] is None:
+            r = subprocess.run([exe, rel_path], cwd=tmp_path, capture_output=True, text=True)
+            assert r.returncode == case["returncode"], name
+            assert r.stdout.splitlines() == case["stdout"], name
+            assert r.stderr.splitlines() == case["stderr"], (name, r.stderr)
+        else:
+            (tmp_path / rel_path).write_text("1\n0\n7\n7\n7\n9\n")
+            r = subprocess.run([exe, rel_path], cwd=tmp_path, capture_output=True, text=True)
+            assert r.returncode == 1 and r.stderr == "Invalid mode\n", name
+            assert r.stdout.splitlines() == case["stdout"][:1], (name, r.stdout)
+            (tmp_path / rel_path).unlink()

@@ -120,6 +120,23 @@ def test_executable_stdout_contract(tmp_path):
             assert len(pat.findall(out.stdout)) == n_iter
 
 
+def test_executable_config_path_quoting(tmp_path):
+    """GpuSolve-hip against the reference executable's own transcripts for config paths holding a space,
+    a backslash and double quotes, and for missing paths (tests/golden/paths.json): stdout, stderr and
+    exit code byte for byte (std::quoted, src/main.cpp:24,28)."""
+    from conftest import load_json
+    exe = gsv._abi.EXECUTABLE
+    for name, case in load_json("paths.json").items():
+        rel_path = case["path"]
+        if case["config"] is not None:
+            (tmp_path / rel_path).write_text(params_from_case(case["config"]).config_text())
+        r = subprocess.run([exe, rel_path], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+        assert r.returncode == case["returncode"], (name, r.stderr)
+        got = [re.sub(r"Took \d+ms", "Took <T>ms", l) for l in r.stdout.splitlines()]
+        assert got == case["stdout"], (name, r.stdout)
+        assert r.stderr.splitlines() == case["stderr"], (name, r.stderr)
+
+
 def test_example_config_verbatim():
     ex = os.path.join(REPO, "tests", "golden", "data-2nd_order.conf")
     out = subprocess.run([gsv._abi.EXECUTABLE, ex], capture_output=True, text=True, timeout=300)
