@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--vcycles", type=int, default=20, help="timed V-cycles after one warm-up cycle (0: skip)")
     ap.add_argument("--cpu-sweeps", type=int, default=6, help="cpu_baseline sample size (0: skip)")
     ap.add_argument("--cpu-vcycles", type=int, default=1, help="cpu_baseline V-cycles (0: skip)")
+    ap.add_argument("--config5", type=int, default=1,
+                    help="N=1: also time config #5's 1024^3 grid on this GPU (the strong-scaling denominator)")
     ap.add_argument("--newton-iters", type=int, default=2,
                     help="timed Newton iterations of BASELINE config #4 (512^3 Newton 2+2) at N=1 (0: skip)")
     return ap.parse_args()
@@ -319,6 +321,60 @@ def newton_timing(n, iters):
             "residuals": hist}
 
 
+CONFIG5_FILE = os.path.join(REPO, "profiles", "config5_single_gpu.json")
+
+
+def config5_single_gpu(steps, vcycles, n=1024):
+    """BASELINE config #5's grid (1024^3 linear 2+2) on this ONE GPU, after the headline and outside its
+    timed region: the same-grid denominator of the strong-scaling ratio north_star names (8 GPUs vs 1 on
+    1024^3). The level-0 smoother as the solver runs it (fused pairs, 1024-point rows: column blocks),
+    timed like the headline (untimed ramp, then `steps` sweeps bracketed by HIP events on the grid's
+    stream), and the 2+2 V-cycle wall time (norm readback included)."""
+    import ctypes as C
+    drv = gsv.driver()
+    p = gsv.GridParams(maxiter=1, tol=0.0, gridDim=(n, n, n), mode=gsv.GS_LINEAR, preSmoothing=2, postSmoothing=2)
+    with gsv.HipGridData(p) as g:
+        stream = torch.cuda.ExternalStream(g.stream())
+
+        def sweeps(k):
+            if drv.gs_grid_jacobi(g.handle, 0, k):
+                raise gsv.GpuSolveError(drv.gs_last_error().decode())
+
+        tw = time.perf_counter()
+        while (time.perf_counter() - tw) < 0.3:
+            sweeps(20)
+            g.sync()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        sweeps(steps)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        fused = drv.gs_grid_level_fused(g.handle, 0) == 1
+        passes = (steps // 2 + steps % 2) if fused else steps
+        kernel_ms = ev0.elapsed_time(ev1) / passes
+        pts = float(n) ** 3
+        kname = gsv.kernels().gs_jacobi_sweep2_kernel(C.byref(p.stencil.to_abi()), C.byref(g.getLevel(0).geom),
+                                                      0).decode()
+        out = {"grid": [n, n, n], "steps": steps, "mlups": round(pts * steps / elapsed / 1e6, 1),
+               "ms_per_step": round(elapsed / steps * 1e3, 4), "pair_kernel_ms": round(kernel_ms, 4),
+               "pair_kernel": kname.split(":")[0],
+               "pair_frac": round(BYTES_PER_LUP * pts / (kernel_ms * 1e-3) / 1e9 / PEAK_GBPS, 4)}
+        if vcycles > 0:
+            gsv.HipSolver.vcycle(g)  # warm-up
+            ms, last = C.c_double(), C.c_double()
+            if drv.gs_grid_time_vcycles(g.handle, vcycles, C.byref(ms), C.byref(last)):
+                raise gsv.GpuSolveError(drv.gs_last_error().decode())
+            out["vcycle_ms"] = round(ms.value / vcycles, 3)
+            out["vcycles"] = vcycles
+    out["note"] = ("1024^3 linear 2+2 on one GPU (BASELINE config #5's grid): the denominator of "
+                   "speedup_vs_1gpu_same_grid in the N=8 line (profiles/config5_single_gpu.json holds the "
+                   "committed copy the N=8 run divides by)")
+    return out
+
+
 def ramp_sweeps(run, ramp_ms, any_rank, chunk=40):
     """Untimed ramp: `run(chunk)` (launch + wait) until `ramp_ms` of wall time has passed on EVERY rank.
     `any_rank(flag)` is the OR of flag over all ranks, so all ranks run the same number of chunks — a
@@ -408,7 +464,12 @@ def main():
             local = slab_local_pair_ms(grid, rank, world, max(4, passes))
         except Exception:  # noqa: BLE001 (diagnostic only)
             local = float("nan")
-        per = torch.tensor([own_elapsed / a.steps * 1e3, kernel_ms, local], dtype=torch.float64, device="cuda")
+        import ctypes as C
+        hms, hcalls = C.c_double(), C.c_int64()
+        drv.gs_grid_comm_stats(grid.handle, C.byref(hms), C.byref(hcalls))
+        halo_us = hms.value / max(1, hcalls.value) * 1e3
+        per = torch.tensor([own_elapsed / a.steps * 1e3, kernel_ms, local, halo_us], dtype=torch.float64,
+                           device="cuda")
         allp = [torch.zeros_like(per) for _ in range(world)]
         dist.all_gather(allp, per)
         rows = [x.tolist() for x in allp]
@@ -418,9 +479,12 @@ def main():
                  "rank_pair_ms": [fin(r[1]) for r in rows],
                  "rank_pair_ms_no_exchange": [fin(r[2]) for r in rows],
                  "exchange_ms_per_pair_max": fin(max(gaps)) if gaps else None,
+                 "rank_halo_host_us_per_call": [fin(r[3]) for r in rows],
                  "note": "rank_pair_ms: the overlapped pair (boundary planes, RCCL ghost exchange, interior) "
                          "per launch on each rank's compute stream; _no_exchange: the same pair on the same "
-                         "slab run locally, no exchange"}
+                         "slab run locally, no exchange; rank_halo_host_us_per_call: host wall time inside one "
+                         "ghost exchange call (RCCL group issue + settle), averaged over every call so far; the "
+                         "interior launch is enqueued before it"}
 
     single = ceiling = None
     if world == 1:
@@ -469,6 +533,25 @@ def main():
     newton = None
     if world == 1 and a.newton_iters > 0:
         newton = newton_timing(n, a.newton_iters)
+
+    c5 = None
+    if world == 1 and a.config5:
+        grid.close()  # the 512^3 hierarchy is not needed any more
+        try:
+            c5 = config5_single_gpu(a.steps, 5 if a.vcycles > 0 else 0)
+        except Exception as e:  # noqa: BLE001 (reported, never required)
+            c5 = {"error": f"{type(e).__name__}: {e}"}
+    speedup = None
+    if world > 1 and tuple(dims) == (1024, 1024, 1024):
+        try:
+            with open(CONFIG5_FILE) as f:
+                ref1 = json.load(f)
+            speedup = {"value": round(value / float(ref1["mlups"]), 3), "one_gpu_mlups": ref1["mlups"],
+                       "one_gpu_source": os.path.relpath(CONFIG5_FILE, REPO) + " (" + ref1.get("source", "?") + ")",
+                       "note": "strong scaling on 1024^3: this line's MLUPS / one GPU's MLUPS on the same grid "
+                               "(bench.py N=1 config5_single_gpu)"}
+        except (OSError, ValueError, KeyError) as e:
+            speedup = {"error": str(e)}
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sweeps > 0:
@@ -522,6 +605,8 @@ def main():
             "measured_ceiling": ceiling,
             "vcycle": vc,
             "newton": newton,
+            "config5_single_gpu": c5,
+            "speedup_vs_1gpu_same_grid": speedup,
             "cpu_baseline": cpu,
             "kernel_build": gsv.build_info(),
         }

@@ -310,6 +310,15 @@ int gs_grid_sync(void* grid)
     return guarded([&] { G(grid).sync(); });
 }
 
+int gs_grid_comm_stats(void* grid, double* halo_host_ms, int64_t* halo_calls)
+{
+    return guarded([&] {
+        const auto& g = G(grid);
+        if (halo_host_ms) *halo_host_ms = g.haloHostMs;
+        if (halo_calls) *halo_calls = g.haloCalls;
+    });
+}
+
 int gs_grid_time_jacobi(void* grid, int level, int warmup, int sweeps, float* ms)
 {
     return guarded([&] {
@@ -441,6 +450,16 @@ int gs_uid_publish(const char* path, const unsigned char uid[128])
     }
 }
 
+int gs_uid_default_path(char* buf, int cap)
+{
+    const std::string p = gs::uidPath();
+    if (buf && cap > 0) {
+        std::strncpy(buf, p.c_str(), (size_t)cap - 1);
+        buf[cap - 1] = 0;
+    }
+    return (int)p.size();
+}
+
 int gs_uid_await(const char* path, double timeout_s, unsigned char uid[128])
 {
     if (!path || !uid) {
@@ -527,48 +546,18 @@ int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, in
 
 int gs_debug_bounded_wait(int scenario, int k, double timeout_s, char* msg, int cap)
 {
-    int polls = 0;
-    const std::string err = gs::boundedWait(
-        [&]() -> int {
-            polls++;
-            if (scenario == 0) return polls >= k ? 0 : 1;     // completes at poll k
-            if (scenario == 1) return polls >= k ? 2 + 3 : 1; // asynchronous error (ncclInternalError = 3)
-            return 1;                                          // never completes
-        },
-        [](int st) { return st == 5 ? std::string("internal error - please report this issue to the NCCL developers")
-                                    : std::string("error ") + std::to_string(st); },
-        timeout_s, "debug wait");
+    std::string err;
+    const int rc = gs::debugBoundedWait(scenario, k, timeout_s, &err);
     if (msg && cap > 0) {
         std::strncpy(msg, err.c_str(), (size_t)cap - 1);
         msg[cap - 1] = 0;
     }
-    return err.empty() ? 0 : 1;
+    return rc;
 }
 
 int gs_debug_loopback_abort(int nranks, int failing_rank)
 {
-    // nranks threads meet at hub barriers; failing_rank throws before its second barrier. Every
-    // thread must unwind (no hang) and the first error must be the one reported.
-    if (nranks < 1 || failing_rank < 0 || failing_rank >= nranks) return -1;
-    auto hub = gs::makeLoopbackHub(nranks);
-    std::vector<int> unwound(nranks, 0);
-    auto body = [&](int r) {
-        try {
-            gs::loopbackHubBarrier(*hub);
-            if (r == failing_rank) throw gs::Error("rank " + std::to_string(r) + " failed");
-            for (int i = 0; i < 3; i++) gs::loopbackHubBarrier(*hub);
-        } catch (const std::exception& e) {
-            unwound[r] = 1;
-            gs::abortLoopbackHub(*hub, e.what());
-        }
-    };
-    std::vector<std::thread> th;
-    for (int r = 0; r < nranks; r++) th.emplace_back(body, r);
-    for (auto& t : th) t.join();
-    g_err = gs::loopbackHubError(*hub);
-    int n = 0;
-    for (int u : unwound) n += u;
-    return n; // == nranks when every rank unwound
+    return gs::debugLoopbackAbort(nranks, failing_rank, &g_err);
 }
 
 const char* gs_last_error(void) { return g_err.c_str(); }

@@ -2,13 +2,10 @@
 #include "gs_comm.hpp"
 
 #include <chrono>
-#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <string>
-#include <thread>
 
 #include <unistd.h>
 
@@ -33,33 +30,6 @@ void ncclOk(ncclResult_t e, const char* what)
 // ---------------------------------------------------------------------------------------------
 void Comm::sync(hipStream_t s) { hipOk(hipStreamSynchronize(s), "hipStreamSynchronize"); }
 void Comm::syncEvent(hipEvent_t e) { hipOk(hipEventSynchronize(e), "hipEventSynchronize"); }
-
-double commTimeoutS(const char* env, double dflt)
-{
-    const char* e = std::getenv(env);
-    if (!e || !*e) return dflt;
-    const double v = std::strtod(e, nullptr);
-    return v > 0 ? v : dflt;
-}
-
-std::string boundedWait(const std::function<int()>& poll, const std::function<std::string(int)>& errText,
-                        double timeoutS, const char* what)
-{
-    const auto t0 = std::chrono::steady_clock::now();
-    for (long spins = 0;; spins++) {
-        const int st = poll();
-        if (st == 0) return "";
-        if (st != 1) return std::string(what) + ": " + errText(st);
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (el > timeoutS) {
-            char buf[160];
-            std::snprintf(buf, sizeof buf, ": timed out after %.1f s (a peer is dead, deadlocked or far behind)", el);
-            return std::string(what) + buf;
-        }
-        // spin briefly (a V-cycle's norm readback is ~1 ms away), then back off
-        if (spins > 2000) std::this_thread::sleep_for(std::chrono::microseconds(spins > 20000 ? 1000 : 50));
-    }
-}
 
 // RCCL over xGMI: halo planes are point-to-point send/recv with the two z-neighbours, grouped so
 // each rank's four operations progress together; the norm is an all-gather of one double. The
@@ -212,91 +182,12 @@ void rcclUniqueId(void* uid)
     std::memcpy(uid, &id, sizeof(id));
 }
 
-void publishUid(const std::string& path, const unsigned char* uid)
-{
-    const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
-    FILE* f = std::fopen(tmp.c_str(), "wb");
-    if (!f) throw Error("cannot write the RCCL id file " + tmp);
-    const bool ok = std::fwrite(uid, 1, 128, f) == 128;
-    if (std::fclose(f) != 0 || !ok || std::rename(tmp.c_str(), path.c_str()) != 0) {
-        std::remove(tmp.c_str());
-        throw Error("cannot publish the RCCL id file " + path);
-    }
-}
-
-void awaitUid(const std::string& path, double timeoutS, unsigned char* uid)
-{
-    const std::string err = boundedWait(
-        [&]() -> int {
-            FILE* f = std::fopen(path.c_str(), "rb");
-            if (!f) return 1;
-            const std::size_t n = std::fread(uid, 1, 128, f);
-            std::fclose(f);
-            return n == 128 ? 0 : 2;
-        },
-        [&](int) { return std::string("short RCCL id file ") + path; }, timeoutS, "waiting for rank 0's RCCL id");
-    if (!err.empty()) throw Error(err + " (" + path + ")");
-}
-
-std::string uidPath()
-{
-    const char* e = std::getenv("GS_UID_FILE");
-    if (e && *e) return e;
-    const char* port = std::getenv("MASTER_PORT");
-    return "/tmp/gpusolve-uid-" + std::to_string((long)getppid()) + "-" + (port && *port ? port : "0");
-}
-
 // ---------------------------------------------------------------------------------------------
 // Loopback: N ranks = N host threads on one device. A rank publishes its buffer and an event
 // recorded after the producing work; after a host barrier every rank makes its stream wait on
 // the producers' events and copies device-to-device, then records a "consumed" event that the
 // producers' streams wait on before they may overwrite the planes. Same ordering contract as RCCL
 // send/recv, so the Z-slab solver is exercised unchanged on one GPU.
-class LoopbackHub {
-public:
-    explicit LoopbackHub(int n) : n_(n), slots_(n) {}
-    struct Slot {
-        const double* p = nullptr;
-        int64_t a = 0, b = 0;
-        hipEvent_t produced = nullptr, consumed = nullptr;
-    };
-    void barrier()
-    {
-        std::unique_lock<std::mutex> lk(m_);
-        if (aborted_) throw Error("loopback exchange aborted: " + why_);
-        const int gen = gen_;
-        if (++count_ == n_) {
-            count_ = 0;
-            gen_++;
-            cv_.notify_all();
-        } else {
-            cv_.wait(lk, [&] { return gen != gen_ || aborted_; });
-            if (gen == gen_) throw Error("loopback exchange aborted: " + why_);
-        }
-    }
-    void abort(const std::string& why)
-    {
-        std::lock_guard<std::mutex> lk(m_);
-        if (!aborted_) why_ = why;
-        aborted_ = true;
-        cv_.notify_all();
-    }
-    std::string error()
-    {
-        std::lock_guard<std::mutex> lk(m_);
-        return aborted_ ? why_ : std::string();
-    }
-    int n_;
-    std::vector<Slot> slots_;
-
-private:
-    std::mutex m_;
-    std::condition_variable cv_;
-    int count_ = 0, gen_ = 0;
-    bool aborted_ = false;
-    std::string why_;
-};
-
 void abortLoopbackHub(LoopbackHub& hub, const std::string& why) { hub.abort(why); }
 std::string loopbackHubError(LoopbackHub& hub) { return hub.error(); }
 void loopbackHubBarrier(LoopbackHub& hub) { hub.barrier(); }
@@ -308,14 +199,17 @@ public:
     LoopbackComm(std::shared_ptr<LoopbackHub> hub, int rank) : h_(std::move(hub)), r_(rank)
     {
         auto& me = h_->slots_[r_];
-        hipOk(hipEventCreateWithFlags(&me.produced, hipEventDisableTiming), "hipEventCreate");
-        hipOk(hipEventCreateWithFlags(&me.consumed, hipEventDisableTiming), "hipEventCreate");
+        hipEvent_t a = nullptr, b = nullptr;
+        hipOk(hipEventCreateWithFlags(&a, hipEventDisableTiming), "hipEventCreate");
+        hipOk(hipEventCreateWithFlags(&b, hipEventDisableTiming), "hipEventCreate");
+        me.produced = a;
+        me.consumed = b;
     }
     ~LoopbackComm() override
     {
         auto& me = h_->slots_[r_];
-        if (me.produced) (void)hipEventDestroy(me.produced);
-        if (me.consumed) (void)hipEventDestroy(me.consumed);
+        if (me.produced) (void)hipEventDestroy((hipEvent_t)me.produced);
+        if (me.consumed) (void)hipEventDestroy((hipEvent_t)me.consumed);
     }
     int rank() const override { return r_; }
     int size() const override { return h_->n_; }
@@ -326,14 +220,14 @@ public:
         const size_t bytes = sizeof(double) * (size_t)(depth * ldz);
         if (r_ > 0) { // rank-1's planes nzl'-depth+1 .. nzl' -> my planes 1-depth .. 0
             auto& nb = h_->slots_[r_ - 1];
-            hipOk(hipStreamWaitEvent(s, nb.produced, 0), "hipStreamWaitEvent");
+            hipOk(hipStreamWaitEvent(s, (hipEvent_t)nb.produced, 0), "hipStreamWaitEvent");
             hipOk(hipMemcpyAsync(field + (1 - depth) * ldz, nb.p + (nb.b - depth + 1) * ldz, bytes,
                                  hipMemcpyDeviceToDevice, s),
                   "hipMemcpyAsync");
         }
         if (r_ + 1 < size()) { // rank+1's planes 1 .. depth -> my planes nzl+1 .. nzl+depth
             auto& nb = h_->slots_[r_ + 1];
-            hipOk(hipStreamWaitEvent(s, nb.produced, 0), "hipStreamWaitEvent");
+            hipOk(hipStreamWaitEvent(s, (hipEvent_t)nb.produced, 0), "hipStreamWaitEvent");
             hipOk(hipMemcpyAsync(field + (nzl + 1) * ldz, nb.p + ldz, bytes, hipMemcpyDeviceToDevice, s),
                   "hipMemcpyAsync");
         }
@@ -345,7 +239,7 @@ public:
         publish(in, 0, 0, s);
         for (int q = 0; q < size(); q++) {
             auto& nb = h_->slots_[q];
-            hipOk(hipStreamWaitEvent(s, nb.produced, 0), "hipStreamWaitEvent");
+            hipOk(hipStreamWaitEvent(s, (hipEvent_t)nb.produced, 0), "hipStreamWaitEvent");
             hipOk(hipMemcpyAsync(out + q, nb.p, sizeof(double), hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
         }
         release(s, -2, -2);
@@ -358,7 +252,7 @@ public:
         for (int q = 0; q < size(); q++) {
             if (q == r_ || hi[q] < lo[q]) continue;
             auto& nb = h_->slots_[q];
-            hipOk(hipStreamWaitEvent(s, nb.produced, 0), "hipStreamWaitEvent");
+            hipOk(hipStreamWaitEvent(s, (hipEvent_t)nb.produced, 0), "hipStreamWaitEvent");
             hipOk(hipMemcpyAsync(field + lo[q] * ldz, nb.p + lo[q] * ldz,
                                  sizeof(double) * (size_t)((hi[q] - lo[q] + 1) * ldz), hipMemcpyDeviceToDevice, s),
                   "hipMemcpyAsync");
@@ -373,19 +267,19 @@ private:
         me.p = p;
         me.a = a;
         me.b = b;
-        hipOk(hipEventRecord(me.produced, s), "hipEventRecord");
+        hipOk(hipEventRecord((hipEvent_t)me.produced, s), "hipEventRecord");
         h_->barrier();
     }
     // q1/q2: the ranks that read our buffer (-2: everyone)
     void release(hipStream_t s, int q1, int q2)
     {
         auto& me = h_->slots_[r_];
-        hipOk(hipEventRecord(me.consumed, s), "hipEventRecord");
+        hipOk(hipEventRecord((hipEvent_t)me.consumed, s), "hipEventRecord");
         h_->barrier();
         for (int q = 0; q < size(); q++) {
             if (q == r_) continue;
             if (q1 != -2 && q != q1 && q != q2) continue;
-            hipOk(hipStreamWaitEvent(s, h_->slots_[q].consumed, 0), "hipStreamWaitEvent");
+            hipOk(hipStreamWaitEvent(s, (hipEvent_t)h_->slots_[q].consumed, 0), "hipStreamWaitEvent");
         }
         h_->barrier();
     }

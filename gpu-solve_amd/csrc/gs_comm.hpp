@@ -18,6 +18,8 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "gs_hostsync.hpp"
+
 namespace gs {
 
 class Comm {
@@ -54,28 +56,14 @@ public:
 std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid);
 void rcclUniqueId(void* uid);
 
-// Sharing rank 0's 128-byte id between the processes of one node without another library (GpuSolve-hip
-// under torchrun): rank 0 writes it to `path` (a temporary file renamed into place, so a reader sees
-// all 128 bytes or nothing), the other ranks poll for it up to timeoutS (gs::Error on timeout).
-// uidPath(): $GS_UID_FILE, else /tmp/gpusolve-uid-<parent pid>-<$MASTER_PORT> — the local ranks of
-// one launcher share its pid, and no live launcher of an earlier run can have the same one.
-void publishUid(const std::string& path, const unsigned char* uid);
-void awaitUid(const std::string& path, double timeoutS, unsigned char* uid);
-std::string uidPath();
-
-// The bounded wait behind RcclComm::sync / settle (host logic, unit-tested on the CPU through
-// gs_debug_bounded_wait). poll() returns 0 done, 1 still pending, or any other value = an error whose
-// text errText(value) gives. Returns "" on completion, else the error / timeout message.
-std::string boundedWait(const std::function<int()>& poll, const std::function<std::string(int)>& errText,
-                        double timeoutS, const char* what);
-double commTimeoutS(const char* env, double dflt);
+// The rank-0 id file hand-off (publishUid / awaitUid / uidPath), the bounded wait and the loopback
+// hub live in the HIP-free gs_hostsync.hpp.
 
 // Rank `rank` of `nranks` without any transport: the communicator of HipGridData's schedule-trace
 // mode, which records exchanges instead of running them.
 std::unique_ptr<Comm> makeTraceComm(int rank, int nranks);
 
-// Loopback: nranks threads of one process on one device share a hub.
-class LoopbackHub;
+// Loopback: nranks threads of one process on one device share a hub (gs_hostsync.hpp).
 std::shared_ptr<LoopbackHub> makeLoopbackHub(int nranks);
 std::unique_ptr<Comm> makeLoopbackComm(const std::shared_ptr<LoopbackHub>& hub, int rank);
 // A rank that fails calls this: every thread parked in (or later reaching) a hub barrier throws, so

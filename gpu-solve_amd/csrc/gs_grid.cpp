@@ -324,8 +324,15 @@ void HipGridData::sync()
 void HipGridData::halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth)
 {
     if (!(L.distributed && nranks() > 1)) return;
-    if (trace) rec("halo", {{"L", (long long)levelIndex(L)}, {"depth", depth}}, fieldName(L, fld));
-    else comm_->halo(fld.data(), fld.ldz(), L.geom.nz, depth, s);
+    if (trace) {
+        rec("halo", {{"L", (long long)levelIndex(L)}, {"depth", depth}}, fieldName(L, fld));
+        return;
+    }
+    // host cost of issuing + settling the exchange (RCCL: group start/end and the async-error poll)
+    const auto t0 = std::chrono::steady_clock::now();
+    comm_->halo(fld.data(), fld.ldz(), L.geom.nz, depth, s);
+    haloHostMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    haloCalls++;
 }
 
 void HipGridData::gather(LevelData& L, DeviceField& fld)
@@ -619,9 +626,9 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
             run(1, b, bs);
             run(nz - b + 1, nz, bs);
             forkComm(grid);
+            run(b + 1, nz - b, s); // interior enqueued before the RCCL group is issued and settled
             grid.halo(L, L.vAlt, grid.commStream(), depth);
             joinComm(grid, false);
-            run(b + 1, nz - b, s);
             joinComm(grid, true);
         } else {
             run(1, nz, s);
@@ -698,9 +705,9 @@ double HipSolver::speculativeSweep(HipGridData& grid, int* sweeps, bool wait)
         run(1, b, bs);
         run(nz - b + 1, nz, bs);
         forkComm(grid);
+        run(b + 1, nz - b, s); // interior enqueued before the RCCL group is issued and settled
         grid.halo(L, L.vAlt, grid.commStream(), depth);
         joinComm(grid, false);
-        run(b + 1, nz - b, s);
         joinComm(grid, true);
     } else {
         run(1, nz, s);
@@ -743,9 +750,9 @@ void HipSolver::upLeg(HipGridData& grid, std::size_t i)
             proPlanes(grid, F, C, 1, 2, bs);
             proPlanes(grid, F, C, zt, nz, bs);
             forkComm(grid);
+            proPlanes(grid, F, C, 3, zt - 1, s); // interior first (see jacobi())
             grid.halo(F, F.vAlt, grid.commStream(), grid.vDepth(F));
             joinComm(grid, false);
-            proPlanes(grid, F, C, 3, zt - 1, s);
             joinComm(grid, true);
         } else {
             proPlanes(grid, F, C, 1, nz, s);

@@ -142,6 +142,8 @@ public:
     // ghost planes of a distributed level's field (no-op otherwise); depth 2 where possible for
     // iterate fields (the fused pair reads two ghost planes of v)
     void halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth = 1);
+    double haloHostMs = 0.0; // host wall time spent inside halo() (issue + settle), summed
+    int64_t haloCalls = 0;
     int vDepth(const LevelData& L) const { return L.minPlanes >= 2 ? 2 : 1; }
     // replicated level fed from a distributed parent: assemble every rank's owned planes
     void gather(LevelData& L, DeviceField& fld);

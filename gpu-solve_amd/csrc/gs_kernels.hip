@@ -2446,10 +2446,10 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
         // (RCCL's need a whole SIMD's registers) find a free CU soon after they are enqueued
         if (L->z0 != 0) {
             const int sz = slab_zc();
-            if (sz > 0) c = sz;
+            if (sz > 0) c = std::max(2, sz); // >= 2: the even rounding below must not reach 0
         } else {
             const int wz = whole_zc();
-            if (wz > 0) c = wz;
+            if (wz > 0) c = std::max(2, wz);
         }
     }
     c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)

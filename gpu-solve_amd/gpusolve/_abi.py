@@ -124,6 +124,7 @@ DRIVER_API = {
     "gs_grid_download": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
     "gs_grid_upload": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
     "gs_grid_sync": (C.c_int, [C.c_void_p]),
+    "gs_grid_comm_stats": (C.c_int, [C.c_void_p, dptr, C.POINTER(C.c_int64)]),
     "gs_grid_metrics": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int, dptr, C.c_int]),
     "gs_dump_write": (C.c_int, [dptr, i64, i64, i64, C.c_char_p]),
     "gs_grid_dump": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
@@ -134,6 +135,7 @@ DRIVER_API = {
     "gs_zslab_schedule": (C.c_int, [C.POINTER(gs_params), C.c_int, C.c_int, i64, C.c_char_p, i64, C.POINTER(i64)]),
     "gs_rccl_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
     "gs_uid_publish": (C.c_int, [C.c_char_p, C.POINTER(C.c_ubyte)]),
+    "gs_uid_default_path": (C.c_int, [C.c_char_p, C.c_int]),
     "gs_uid_await": (C.c_int, [C.c_char_p, C.c_double, C.POINTER(C.c_ubyte)]),
     "gs_grid_create_rccl": (C.c_void_p, [C.POINTER(gs_params), C.c_int, C.c_int, C.POINTER(C.c_ubyte)]),
     "gs_zslab_loopback_run": (C.c_int, [C.POINTER(gs_params), C.c_int, i64, C.c_int, C.c_int, dptr, C.c_int,

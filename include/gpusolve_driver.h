@@ -62,6 +62,10 @@ hipStream_t gs_grid_stream(void* grid);
 int gs_grid_download(void* grid, int level, int field, double* host);
 int gs_grid_upload(void* grid, int level, int field, const double* host);
 int gs_grid_sync(void* grid);
+/* Host cost of the ghost exchanges issued so far (Z-slab grids): total wall milliseconds spent inside
+ * the exchange calls (RCCL: group start/end and the settle poll of the non-blocking communicator) and
+ * the number of calls. Zero for single-GPU grids. */
+int gs_grid_comm_stats(void* grid, double* halo_host_ms, int64_t* halo_calls);
 /* With GS_METRICS=1 in the environment when the grid was created: the "[gs] mlups=... gbps=...
  * pct_peak=... vcycle_ms=... cycles=... level_ms=..." line GpuSolve-hip prints after its solve (over
  * the V-cycles run so far), and the device ms per level and V-cycle. Non-zero if metrics are off. */
@@ -105,6 +109,10 @@ void* gs_grid_create_rccl(const gs_params* p, int rank, int nranks, const unsign
  * 0 on success, else non-zero with gs_last_error(). */
 int gs_uid_publish(const char* path, const unsigned char uid[128]);
 int gs_uid_await(const char* path, double timeout_s, unsigned char uid[128]);
+/* The id file GpuSolve-hip uses when GS_UID_FILE is unset: /tmp/gpusolve-uid-<parent pid>-<MASTER_PORT>,
+ * plus -<TORCHELASTIC_RUN_ID>-a<TORCHELASTIC_RESTART_COUNT> under torchrun, so that each restart attempt
+ * has its own file. Writes at most cap-1 bytes + NUL; returns the full length. */
+int gs_uid_default_path(char* buf, int cap);
 /* Single-process emulation of an nranks Z-slab run on the current device: nranks threads, each a
  * rank with its own slab and streams, device-to-device copies as the exchange. Runs `sweeps`
  * level-0 Jacobi sweeps, then (solve != 0) the solve of p. Writes rank 0's residual history and

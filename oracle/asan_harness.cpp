@@ -6,17 +6,28 @@
 //   * the product's config reader (gpu-solve_amd/csrc/gs_params.cpp: valid, truncated, garbage, bad
 //     mode / stencil texts — the reference reads these fields unvalidated, src/main.cpp:32-85);
 //   * the product's Z-slab ownership plan (gpu-solve_amd/csrc/gs_plan.cpp) over many grids and rank
-//     counts, checking its invariants.
+//     counts, checking its invariants;
+//   * the exchange layer's HIP-free host logic (gpu-solve_amd/csrc/gs_hostsync.cpp): the bounded wait
+//     that settles every RCCL call (completion, error, timeout), the rank-0 id file hand-off (publish /
+//     await / a stale file of an earlier torchrun attempt), and the loopback hub's barrier/abort across
+//     rank threads.
+// Built twice: `asan` (address + undefined, everything) and `tsan` (-DGS_HOSTSYNC_ONLY, thread
+// sanitizer over the host-sync section alone: the OpenMP oracle is not TSan-instrumented).
 // Any sanitizer report aborts (-fno-sanitize-recover=all); an invariant failure exits 1.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 #include "gs_comm.hpp"
+#include "gs_hostsync.hpp"
 #include "gs_params.hpp"
 
+#ifndef GS_HOSTSYNC_ONLY
 extern "C" {
 typedef struct { double s[7]; int ox[7], oy[7], oz[7]; } gso_stencil;
 void* gso_grid_create(const gso_stencil*, const int64_t*, int, int64_t, double, double, double, int64_t, int64_t);
@@ -33,6 +44,7 @@ void gso_restrict(const double* fine, const int64_t fn[3], double* coarse, const
 void gso_interpolate(const double* coarse, const int64_t cn[3], double* e, const int64_t fn[3]);
 void gso_rhs(const int64_t n[3], double h, int mode, double gamma, double* f);
 }
+#endif
 
 namespace {
 
@@ -45,6 +57,7 @@ int failures = 0;
         }                                                                                                              \
     } while (0)
 
+#ifndef GS_HOSTSYNC_ONLY
 const gso_stencil S7{{6, -1, -1, -1, -1, -1, -1}, {0, 1, -1, 0, 0, 0, 0}, {0, 0, 0, 1, -1, 0, 0}, {0, 0, 0, 0, 0, 1, -1}};
 
 std::size_t padded(const int64_t n[3]) { return (std::size_t)((n[0] + 2) * (n[1] + 2) * (n[2] + 2)); }
@@ -138,14 +151,63 @@ void plans()
             }
 }
 
+#endif // GS_HOSTSYNC_ONLY
+
+void hostsync()
+{
+    // bounded wait: completes at poll k, an asynchronous error at poll k, a timeout
+    std::string msg;
+    CHECK(gs::debugBoundedWait(0, 5, 10.0, &msg) == 0 && msg.empty());
+    CHECK(gs::debugBoundedWait(1, 3, 10.0, &msg) == 1 && msg.find("internal error") != std::string::npos);
+    CHECK(gs::debugBoundedWait(2, 0, 0.05, &msg) == 1 && msg.find("timed out") != std::string::npos);
+    // loopback hub: every rank thread unwinds when one fails, whichever it is
+    for (int n : {1, 2, 3, 8})
+        for (int f = 0; f < n; f++) {
+            std::string first;
+            CHECK(gs::debugLoopbackAbort(n, f, &first) == n);
+            CHECK(first == "rank " + std::to_string(f) + " failed");
+        }
+    // id hand-off: publish -> await round trip; a stale file of attempt 0 is not the path of attempt 1
+    char dir[] = "/tmp/gs_hostsync_XXXXXX";
+    CHECK(mkdtemp(dir) != nullptr);
+    const std::string path = std::string(dir) + "/uid";
+    unsigned char a[128], b[128] = {};
+    for (int i = 0; i < 128; i++) a[i] = (unsigned char)(i * 7 + 1);
+    gs::publishUid(path, a);
+    gs::awaitUid(path, 5.0, b);
+    CHECK(std::memcmp(a, b, 128) == 0);
+    bool threw = false;
+    try {
+        gs::awaitUid(path + ".missing", 0.05, b);
+    } catch (const gs::Error&) {
+        threw = true;
+    }
+    CHECK(threw);
+    unsetenv("GS_UID_FILE");
+    setenv("MASTER_PORT", "29500", 1);
+    setenv("TORCHELASTIC_RUN_ID", "run/1", 1);
+    setenv("TORCHELASTIC_RESTART_COUNT", "0", 1);
+    const std::string p0 = gs::uidPath();
+    setenv("TORCHELASTIC_RESTART_COUNT", "1", 1);
+    const std::string p1 = gs::uidPath();
+    CHECK(p0 != p1 && p0.rfind('/') == 4); // one file under /tmp, the run id's '/' replaced
+    unsetenv("TORCHELASTIC_RUN_ID");
+    unsetenv("TORCHELASTIC_RESTART_COUNT");
+    std::remove(path.c_str());
+    rmdir(dir);
+}
+
 } // namespace
 
 int main()
 {
+#ifndef GS_HOSTSYNC_ONLY
     solves();
     operators();
     configs();
     plans();
+#endif
+    hostsync();
     if (failures) {
         std::fprintf(stderr, "%d check(s) failed\n", failures);
         return 1;

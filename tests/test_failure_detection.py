@@ -94,3 +94,42 @@ def test_uid_handoff_rejects_a_short_file(tmp_path):
     got = (C.c_ubyte * 128)()
     assert d.gs_uid_await(str(tmp_path / "uid").encode(), 1.0, got) == 1
     assert "short RCCL id file" in d.gs_last_error().decode()
+
+
+def test_uid_default_path_is_per_restart_attempt(monkeypatch):
+    """without GS_UID_FILE the id file was /tmp/gpusolve-uid-<ppid>-<port>, the same for every
+    torchrun --max-restarts attempt (the agent keeps its pid and port), so a file left behind by an attempt
+    whose rank 0 was killed could be read by the next attempt's ranks. The default path now carries
+    TORCHELASTIC_RUN_ID and TORCHELASTIC_RESTART_COUNT: attempt 1 never sees attempt 0's stale file."""
+    import os
+    drv = gsv.driver()
+
+    def path():
+        buf = C.create_string_buffer(512)
+        n = drv.gs_uid_default_path(buf, 512)
+        assert 0 < n < 512
+        return buf.value.decode()
+
+    monkeypatch.delenv("GS_UID_FILE", raising=False)
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", f"gs-test-{os.getpid()}")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    p0 = path()
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    p1 = path()
+    assert p0 != p1 and p0.startswith("/tmp/gpusolve-uid-")
+    stale = (C.c_ubyte * 128)(*([7] * 128))
+    fresh = (C.c_ubyte * 128)(*range(128))
+    got = (C.c_ubyte * 128)()
+    try:
+        assert drv.gs_uid_publish(p0.encode(), stale) == 0  # attempt 0's rank 0, killed before its cleanup
+        t0 = time.perf_counter()
+        assert drv.gs_uid_await(p1.encode(), 0.2, got) != 0  # attempt 1 waits for ITS rank 0
+        assert time.perf_counter() - t0 >= 0.2
+        assert drv.gs_uid_publish(p1.encode(), fresh) == 0
+        assert drv.gs_uid_await(p1.encode(), 5.0, got) == 0
+        assert bytes(got) == bytes(range(128))
+    finally:
+        for p in (p0, p1):
+            if os.path.exists(p):
+                os.unlink(p)
