@@ -212,15 +212,18 @@ def vcycle_level0_kernels(grid, k):
     def rr():
         assert kl.gs_residual_restrict(C.byref(S), C.byref(L0), 0, p.gamma, v, f, None, cf, None, C.byref(L1), st) == 0
 
+    wsn = kl.gs_jacobi_sweep2_prolong_ws_elems(C.byref(S), C.byref(L0), 0)  # rows > 512: edge-column strip
+    ws = torch.empty(max(1, wsn), dtype=torch.float64, device="cuda")
+
     def pro():
-        assert kl.gs_jacobi_sweep2_prolong(C.byref(S), C.byref(L0), 0, p.omega, p.gamma, v, cv, None, C.byref(L1),
-                                           out.ptr, f, None, 0, 0, st) == 0
+        assert kl.gs_jacobi_sweep2_prolong_ws(C.byref(S), C.byref(L0), 0, p.omega, p.gamma, v, cv, None, C.byref(L1),
+                                              out.ptr, f, None, 0, 0, ws.data_ptr(), wsn, st) == 0
 
     res = {}
     for name, fn, bpp in (("residual_restrict", rr, 17.0), ("prolong_pair", pro, 25.0)):
         try:
             fn()
-        except AssertionError:  # e.g. rows > 512 points: the solver prolongs unfused there
+        except AssertionError:
             res[name] = {"error": "no fused kernel for this level shape"}
             continue
         fn()

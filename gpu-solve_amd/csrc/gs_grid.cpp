@@ -72,6 +72,24 @@ void DeviceField::swap(DeviceField& o) noexcept
     std::swap(dry_, o.dry_);
 }
 
+DeviceBuf::~DeviceBuf()
+{
+    if (p_) (void)hipFree(p_);
+}
+
+double* DeviceBuf::get(int64_t elems)
+{
+    if (elems <= n_) return p_;
+    if (p_) check((int)hipFree(p_), "hipFree");
+    p_ = nullptr;
+    n_ = 0;
+    void* q = nullptr;
+    check((int)hipMalloc(&q, sizeof(double) * (size_t)elems), "hipMalloc(workspace)");
+    p_ = static_cast<double*>(q);
+    n_ = elems;
+    return p_;
+}
+
 StreamGuard::StreamGuard(bool create, bool high)
 {
     if (!create) return;
@@ -237,6 +255,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
     check((int)hipEventCreateWithFlags(&evA_, hipEventDisableTiming), "hipEventCreate");
     check((int)hipEventCreateWithFlags(&evB_, hipEventDisableTiming), "hipEventCreate");
     check((int)hipEventCreateWithFlags(&evC_, hipEventDisableTiming), "hipEventCreate");
+    for (auto& e : evBnd_) check((int)hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     check((int)hipEventCreateWithFlags(&evNorm_, hipEventDisableTiming), "hipEventCreate");
     // level-0 right-hand side on the device (src/cpu/CpuGridData.cpp:44-78), h = 1/(Y+1) (main.cpp:84);
     // a slab evaluates it at its global plane indices (geom.z0)
@@ -258,6 +277,8 @@ HipGridData::~HipGridData()
     if (evA_) (void)hipEventDestroy(evA_);
     if (evB_) (void)hipEventDestroy(evB_);
     if (evC_) (void)hipEventDestroy(evC_);
+    for (auto e : evBnd_)
+        if (e) (void)hipEventDestroy(e);
     if (evNorm_) (void)hipEventDestroy(evNorm_);
 }
 
@@ -428,9 +449,17 @@ void proPlanes(HipGridData& g, HipGridData::LevelData& F, HipGridData::LevelData
         g.rec("pro", {{"L", (long long)g.levelIndex(F)}, {"z1", z1}, {"z2", z2}, {"zlo", zlo}, {"zhi", zhi}});
         return;
     }
-    check(gs_jacobi_sweep2_prolong(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, F.v.data() + off, C.v.data(),
-                                   nullptr, &C.geom, F.vAlt.data() + off, F.f.data() + off,
-                                   F.newtonV ? F.newtonV.data() + off : nullptr, zlo, zhi, s),
+    // rows > 512 points (column blocks): the corrected edge columns go through a workspace, one per
+    // stream (the boundary planes' launch runs beside the interior's)
+    const int64_t wsn = gs_jacobi_sweep2_prolong_ws_elems(&g.stencilAbi, &sub, (int)g.mode);
+    // (sized for the whole level once: a plane range needs less, and no buffer is ever reallocated
+    // while a launch may still read it)
+    double* ws = wsn > 0 ? F.proWs[s == g.stream() ? 0 : 1].get(std::max(
+                                wsn, gs_jacobi_sweep2_prolong_ws_elems(&g.stencilAbi, &F.geom, (int)g.mode)))
+                         : nullptr;
+    check(gs_jacobi_sweep2_prolong_ws(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, F.v.data() + off,
+                                      C.v.data(), nullptr, &C.geom, F.vAlt.data() + off, F.f.data() + off,
+                                      F.newtonV ? F.newtonV.data() + off : nullptr, zlo, zhi, ws, wsn, s),
           "gs_jacobi_sweep2_prolong");
 }
 
@@ -602,9 +631,21 @@ static bool proWorthIt(HipGridData& grid, std::size_t l)
 
 // k sweeps (src/cpu/CpuSolver.cpp:141-180). Each reads v and writes vAlt, then the two swap. Where
 // the level allows, sweeps run in fused pairs (gs_jacobi_sweep2: one read of v and f, one write, for
-// two sweeps), an odd one as a single sweep. On a Z-slab the outermost planes (one per side for a
-// sweep, two for a pair) are computed first; their ghost exchange then runs on the comm stream while
-// the interior planes are computed on the compute stream.
+// two sweeps), an odd one as a single sweep.
+//
+// On a Z-slab the outermost planes of each step (one per side for a sweep, two for a pair) run on the
+// boundary stream, their ghost exchange follows on the comm stream, and the interior planes run on the
+// compute stream beside both. The steps of one call are pipelined so that the compute stream never waits
+// for an exchange: step k's interior reads only v's owned planes (k-1's interior, k-1's boundary
+// planes), never its ghost planes, so it needs boundary k-1 but not exchange k-1. Only the boundary
+// planes of step k wait for exchange k-1 (the ghosts they read) and for interior k-1 (whose input planes
+// they overwrite); exchange k then hides under interior k+1 instead of sitting between two interiors.
+// The last exchange is joined into the compute stream before returning. Writes never meet a read of the
+// same planes: interior k writes the buffer exchange k-2 sent from (its boundary planes only) and that
+// boundary k-1 read planes 3-4 of before it (event), boundary k writes planes exchange k-2 sent (comm is
+// in order, boundary k waits exchange k-1). The interior launch is enqueued before the exchange is issued:
+// RCCL's non-blocking group is settled on the host (gs_comm.cpp), and the GPU must not wait on that host
+// round-trip between the boundary planes and the interior.
 void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
 {
     auto& L = grid.getLevel(l);
@@ -612,6 +653,7 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
     const bool dist = L.distributed && grid.nranks() > 1;
     const int64_t nz = L.geom.nz;
     const int depth = grid.vDepth(L);
+    int step = 0; // overlapped steps issued in this call
     while (sweeps > 0) {
         const bool pair = L.fusedPairs && sweeps >= 2;
         const int64_t b = pair ? 2 : depth; // outermost planes whose ghost copies the neighbours need
@@ -622,15 +664,31 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
         if (!dist) {
             run(1, nz, s);
         } else if (grid.overlapHalo && nz >= 2 * b + 1) {
-            const hipStream_t bs = forkBoundary(grid);
+            hipStream_t bs = s;
+            if (!grid.trace) {
+                bs = grid.bndStream_.s;
+                // boundary k after interior k-1 (and everything before it on the compute stream) and after
+                // exchange k-1 (the ghost planes it reads; on the comm stream, after every earlier exchange)
+                check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
+                check((int)hipStreamWaitEvent(bs, grid.evA_, 0), "hipStreamWaitEvent");
+                if (step > 0) check((int)hipStreamWaitEvent(bs, grid.evB_, 0), "hipStreamWaitEvent");
+            }
             run(1, b, bs);
             run(nz - b + 1, nz, bs);
-            forkComm(grid);
-            run(b + 1, nz - b, s); // interior enqueued before the RCCL group is issued and settled
+            if (!grid.trace) {
+                hipEvent_t bnd = grid.evBnd_[step & 1];
+                check((int)hipEventRecord(bnd, bs), "hipEventRecord");
+                check((int)hipStreamWaitEvent(grid.commStream(), bnd, 0), "hipStreamWaitEvent");
+                // interior k reads boundary k-1's planes (boundary k's slot is recorded, k-1's still holds)
+                if (step > 0) check((int)hipStreamWaitEvent(s, grid.evBnd_[(step - 1) & 1], 0), "hipStreamWaitEvent");
+            }
+            run(b + 1, nz - b, s);
             grid.halo(L, L.vAlt, grid.commStream(), depth);
-            joinComm(grid, false);
-            joinComm(grid, true);
+            if (!grid.trace) check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+            step++;
         } else {
+            if (step > 0) joinComm(grid, true); // an earlier overlapped step's exchange
+            step = 0;
             run(1, nz, s);
             grid.halo(L, L.vAlt, s, depth);
         }
@@ -638,6 +696,11 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
         if (grid.trace) grid.rec("swap", {{"L", (long long)l}});
         L.vZero = false;
         sweeps -= pair ? 2 : 1;
+    }
+    if (step > 0) {
+        // the last exchange (and through it the last boundary planes) before anything else on the level
+        joinComm(grid, true);
+        if (!grid.trace) check((int)hipStreamWaitEvent(s, grid.evBnd_[(step - 1) & 1], 0), "hipStreamWaitEvent");
     }
 }
 

@@ -55,6 +55,21 @@ private:
     bool dry_ = false;
 };
 
+// A plain device buffer of doubles (workspaces), grown on demand.
+class DeviceBuf {
+public:
+    DeviceBuf() = default;
+    ~DeviceBuf();
+    DeviceBuf(const DeviceBuf&) = delete;
+    DeviceBuf& operator=(const DeviceBuf&) = delete;
+    double* get(int64_t elems); // at least elems doubles (reallocated when larger; contents not kept)
+    int64_t size() const { return n_; }
+
+private:
+    double* p_ = nullptr;
+    int64_t n_ = 0;
+};
+
 struct StreamGuard {
     hipStream_t s = nullptr;
     // high: the device's greatest stream priority (the exchange path: boundary planes, ghost copies)
@@ -95,6 +110,9 @@ public:
         int64_t lo = 1, hi = 0; // this rank's owned global planes (== 1..nz when not distributed)
         int64_t minPlanes = 0;  // fewest planes any rank owns on this level
         std::vector<int64_t> ranksLo, ranksHi; // every rank's owned planes (gather of replicated levels)
+        // workspaces of the fused prolongation pair on column-block rows (gs_jacobi_sweep2_prolong_ws):
+        // [0] for launches on the compute stream, [1] on the boundary stream (they run concurrently)
+        std::unique_ptr<DeviceBuf[]> proWs = std::make_unique<DeviceBuf[]>(2);
     };
 
     // comm == nullptr or comm->size() == 1: the single-GPU path. The grid does not own comm.
@@ -162,6 +180,7 @@ private:
     double* hNorm_ = nullptr;
     double* hNormDev_ = nullptr;
     hipEvent_t evA_ = nullptr, evB_ = nullptr, evC_ = nullptr, evNorm_ = nullptr;
+    hipEvent_t evBnd_[2] = {nullptr, nullptr}; // boundary planes of sweep k (k & 1) in a pipelined sequence
     std::vector<double> dryParts_;
     long traceNorms_ = 0;
     double traceNorm();

@@ -1100,6 +1100,31 @@ __global__ __launch_bounds__(256) void k_prolong_add(const double* __restrict__ 
     }
 }
 
+// The corrected iterate v + P v^2h on the four fine columns around every interior column-block
+// boundary of the prolongation pair (k_tb2y XH + PRO): columns xb-2 .. xb+1 of the boundary at xb (the
+// first column of the right block), rows 0..ny+1, local planes -1..nz+2 — what the blocks on either side
+// read of the neighbour's columns. A point gets the correction where the pair's lanes correct it (x, y
+// interior; the plane interior or a ghost plane of an internal slab side: pok) and keeps v elsewhere,
+// with the reference's X, Y, Z pass arithmetic (prolong_value), so the strip holds bit for bit what the
+// neighbour block's lanes compute in registers. Layout: es[((b * (nz + 4) + p + 1) * 4 + c) * (ny + 2) + y].
+// The coarse field is indexed from the plane under fine local plane 0 (z0 even: local parities are global).
+template <bool SUB>
+__global__ __launch_bounds__(256) void k_pro_strip(const double* __restrict__ v, const double* __restrict__ c,
+                                                   const double* __restrict__ sub, double* __restrict__ es, int nx,
+                                                   int ny, int nz, int64_t ldy, int64_t ldz, int64_t cldy,
+                                                   int64_t cldz, int bw, int zlo, int zhi)
+{
+    const int y = blockIdx.x * 256 + threadIdx.x;
+    if (y > ny + 1) return;
+    const int p = (int)blockIdx.y - 1;
+    const int b = (int)blockIdx.z >> 2, col = (int)blockIdx.z & 3;
+    const int x = 1 + (b + 1) * bw - 2 + col;
+    double val = v[x + (int64_t)y * ldy + (int64_t)p * ldz];
+    const bool pok = (p >= 1 && p <= nz) || (zlo && p <= 0) || (zhi && p > nz);
+    if (pok && y >= 1 && y <= ny && x >= 1 && x <= nx) val = val + prolong_value<SUB>(c, sub, x, y, p, cldy, cldz, 0);
+    es[(((int64_t)b * (nz + 4) + p + 1) * 4 + col) * (ny + 2) + y] = val;
+}
+
 // Unfused reference-shaped interpolate (whole padded fine array), used by parity tests.
 __global__ __launch_bounds__(256) void k_interpolate(const double* __restrict__ c, double* __restrict__ e, int fPx,
                                                      int fPy, int fPz, int64_t fldy, int64_t fldz, int64_t cldy,
@@ -1372,7 +1397,7 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
                                                       double* __restrict__ out, double* __restrict__ partials, int nx,
                                                       int ny, int nz, int64_t ldy, int64_t ldz, int ZC, int zlo,
                                                       int zhi, const double*, const double*, int, int, int, int64_t,
-                                                      int64_t)
+                                                      int64_t, const double*)
 {
     __shared__ double red[WXMAX];
     double sumsq = 0.0; // r^2 of sweep 1's residual over the block's own points (partials != NULL)
@@ -1571,10 +1596,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                                                            int nx, int ny, int nz, int64_t ldy, int64_t ldz, int ZC,
                                                            int zlo, int zhi, const double* __restrict__ pc,
                                                            const double* __restrict__ ps, int cnx, int cny, int cnz,
-                                                           int64_t cldy, int64_t cldz)
+                                                           int64_t cldy, int64_t cldz, const double* __restrict__ es)
 {
     static_assert(PRO == 0 || (SPEC && !ZV && RY % 2 == 0), "fused prolongation: per-wave code, even RY");
-    static_assert(!XH || (PRO == 0 && MODE != GS_NEWTON && RY + 2 <= WAVE), "column blocks: LINEAR / NONLINEAR pairs");
+    static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR) && MODE != GS_NEWTON && RY + 2 <= WAVE),
+                  "column blocks: LINEAR / NONLINEAR pairs, LINEAR prolongation pairs");
     constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
     constexpr int NE = NV + RY; // x-edge values per wave side: v rows 0..RY, sweep-1 rows 1..RY
     __shared__ double red[2 * WXMAX];
@@ -1630,6 +1656,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         erowc = y >= 1 && y <= ny;
     }
     auto eat = [&](const double* base, int dx, int z) { return base + (xe + dx) + eroff + (int64_t)z * ldz; };
+    // XH + PRO: the edge column's corrected iterate v + P v^2h (columns xe-1..xe+1) comes from the strip
+    // k_pro_strip wrote for this launch (layout there): [boundary][plane -1..nz+2][column xb-2..xb+1][row]
+    const double* esr = es;
+    if (XH && PRO != 0 && edg) {
+        const int hb = eL ? hx - 1 : hx; // the block boundary the edge column lies at
+        const int y = yof(min(lane, RY + 1));
+        esr = es + (int64_t)hb * (nz + 4) * 4 * (ny + 2) + (eL ? 1 : 2) * (ny + 2) + min(max(y, 0), ny + 1);
+    }
+    auto sat = [&](int dx, int z) { return esr + ((int64_t)(z + 1) * 4 + dx) * (ny + 2); };
 
     // PFD: prefetch distance in plane steps. 1: two operand slots (this step's, the next one's in
     // flight); 2: four named slots, three live (this step's and the next two in flight), the z loop
@@ -1664,9 +1699,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         HL[s] = ldv2<ZV>(at(v, -1, z));
         if constexpr (XH) {
             if (edg) {
-                EA[s] = ldv1<ZV>(eat(v, 0, zv));
-                EXm[s] = ldv1<ZV>(eat(v, -1, z));
-                EXp[s] = ldv1<ZV>(eat(v, 1, z));
+                if constexpr (PRO != 0) {
+                    EA[s] = *sat(0, zv);
+                    EXm[s] = *sat(-1, z);
+                    EXp[s] = *sat(1, z);
+                } else {
+                    EA[s] = ldv1<ZV>(eat(v, 0, zv));
+                    EXm[s] = ldv1<ZV>(eat(v, -1, z));
+                    EXp[s] = ldv1<ZV>(eat(v, 1, z));
+                }
                 EF[s] = *eat(f, 0, z);
             }
         }
@@ -1677,8 +1718,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         Vc[j] = ldv2<ZV>(at(v, j, zb - 1));
     }
     if (XH && edg) {
-        EP = ldv1<ZV>(eat(v, 0, zb - 2));
-        EC = ldv1<ZV>(eat(v, 0, zb - 1));
+        EP = PRO != 0 ? *sat(0, zb - 2) : ldv1<ZV>(eat(v, 0, zb - 2));
+        EC = PRO != 0 ? *sat(0, zb - 1) : ldv1<ZV>(eat(v, 0, zb - 1));
     }
     // ---- fused prolongation (PRO): coarse rows cyb .. cyb+NCR-1 lie under the wave's fine rows ----
     constexpr int NCR = RY / 2 + 2;
@@ -2739,7 +2780,7 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
-#define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr)
     // LINEAR zero-iterate pairs (the first sweep of a coarse level, v = 0: the lightest variant, three
     // blocks per CU) below 2^26 points: chunks fitted to whole rounds of resident blocks (256^3: 61 vs
     // 71 us; the same rule measured no better for the other pairs, worse for k_rr2 and for NEWTON's
@@ -2747,9 +2788,9 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     const bool refit = !v_in && !partials && (int64_t)L->nx * L->ny * L->nz < ((int64_t)1 << 26);
 #define GS_TBY1(M, Z, U) do { \
         if (refit && M == GS_LINEAR) refit_chunks(&k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M), false, U>, (int)(b.x * b.y * b.z), nz, 4, 64, true, 2.0, &zc, &g); \
-        hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M), false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0); } while (0)
+        hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, tby_pfd(M), false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr); } while (0)
 #define GS_TBY(M, Z) do { if (k.unit) GS_TBY1(M, Z, true); else GS_TBY1(M, Z, false); } while (0)
-#define GS_TBX1(M, Z, P, U) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0)
+#define GS_TBX1(M, Z, P, U) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr)
 #define GS_TBX(M, Z, P) do { if (k.unit) GS_TBX1(M, Z, P, true); else GS_TBX1(M, Z, P, false); } while (0)
     const bool zv = !v_in;
     if (xh) {
@@ -2785,37 +2826,65 @@ int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, i
 {
     int zc;
     dim3 g, b;
-    bool y2 = false;
-    // LINEAR only: the NEWTON variant (newtonV rows on top of the coarse planes) spills 240 B per lane
-    // (measured 3.0 ms per 512^3 launch against 1.54 ms for gs_prolong_add + the pair) and the
-    // NONLINEAR one carries restV too
-    // the fine planes' parities must be the global ones (even z0): they select each plane's combination
+    bool y2 = false, xh = false;
+    // LINEAR and NEWTON (NONLINEAR carries restV too). Rows of more than 512 points (column blocks, XH):
+    // LINEAR, with the workspace of gs_jacobi_sweep2_prolong_ws_elems (the corrected edge columns).
+    // The fine planes' parities must be the global ones (even z0): they select each plane's combination
     return !bad_level(L) && valid_stencil(S) && (mode == GS_LINEAR || mode == GS_NEWTON) && L->z0 % 2 == 0 &&
-           tb2_plan(S, L, &zc, &g, &b, &y2, mode) && y2;
+           tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh) && (y2 || (xh && mode == GS_LINEAR));
+}
+
+int64_t gs_jacobi_sweep2_prolong_ws_elems(const gs_stencil* S, const gs_level* L, int mode)
+{
+    int zc;
+    dim3 g, b;
+    bool y2 = false, xh = false;
+    if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh) || !xh)
+        return 0;
+    const int64_t bw = 2 * WAVE * TBY_WX, nb = (L->nx + bw - 1) / bw - 1; // interior block boundaries
+    return nb * (L->nz + 4) * 4 * (L->ny + 2);
 }
 
 int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
                              const double* v_in, const double* coarse_v, const double* coarse_sub, const gs_level* cl,
                              double* v_out, const double* f, const double* w, int zlo, int zhi, hipStream_t st)
 {
+    return gs_jacobi_sweep2_prolong_ws(S, L, mode, omega, gamma, v_in, coarse_v, coarse_sub, cl, v_out, f, w, zlo, zhi,
+                                       nullptr, 0, st);
+}
+
+int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                                const double* v_in, const double* coarse_v, const double* coarse_sub,
+                                const gs_level* cl, double* v_out, const double* f, const double* w, int zlo, int zhi,
+                                double* ws, int64_t ws_elems, hipStream_t st)
+{
     int zc;
     dim3 g, b;
-    bool y2 = false;
+    bool y2 = false, xh = false;
     // coarse plane of fine local plane z: (z >> 1) + czoff, z0 even (a slab, or a plane range of one)
     const int64_t czoff = cl ? L->z0 / 2 - cl->z0 : 0;
     if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || bad_level(cl) || czoff < 0 || !v_in || !coarse_v ||
         !v_out || !f || v_in == v_out || (mode == GS_NONLINEAR) != (coarse_sub != nullptr) || (mode == GS_NEWTON && !w) ||
         (L->nx + 1) / 2 > cl->nx + 1 || (L->ny + 1) / 2 > cl->ny + 1 || (L->nz + 1) / 2 + czoff > cl->nz + 1 ||
-        !tb2_plan(S, L, &zc, &g, &b, &y2, mode))
+        !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh))
         return GS_EINVAL;
+    const int64_t need = gs_jacobi_sweep2_prolong_ws_elems(S, L, mode);
+    if (need > 0 && (!ws || ws_elems < need)) return GS_EINVAL;
     // the kernel indexes the coarse field from the plane under fine local plane 0
     coarse_v += czoff * cl->ldz;
     if (coarse_sub) coarse_sub += czoff * cl->ldz;
     const Coef k = make_coef(S, L, omega, gamma);
-#define GS_TBP1(M, P, U) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, false, true, P, 1, false, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz)
-#define GS_TBP(M, P) do { if (k.unit) GS_TBP1(M, P, true); else GS_TBP1(M, P, false); } while (0)
-    if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1);
-    else GS_TBP(GS_LINEAR, 1);
+    if (xh && need > 0) {
+        const int bw = 2 * WAVE * TBY_WX, nb = (int)((L->nx + bw - 1) / bw - 1);
+        hipLaunchKernelGGL(k_pro_strip<false>, dim3((unsigned)((L->ny + 2 + 255) / 256), (unsigned)(L->nz + 4), (unsigned)(4 * nb)),
+                           dim3(256), 0, st, v_in, coarse_v, nullptr, ws, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy,
+                           L->ldz, cl->ldy, cl->ldz, bw, zlo ? 1 : 0, zhi ? 1 : 0);
+    }
+#define GS_TBP1(M, P, U, X) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, false, true, P, 1, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
+#define GS_TBP(M, P, X) do { if (k.unit) GS_TBP1(M, P, true, X); else GS_TBP1(M, P, false, X); } while (0)
+    if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1, false);
+    else if (xh) GS_TBP(GS_LINEAR, 1, true);
+    else GS_TBP(GS_LINEAR, 1, false);
 #undef GS_TBP
 #undef GS_TBP1
     return launch_status();
@@ -3140,7 +3209,7 @@ struct PairVariant {
     const char* name;
     int ry, wxmax, wy;
     void (*kern)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
-                 int64_t, int, int, int, const double*, const double*, int, int, int, int64_t, int64_t);
+                 int64_t, int, int, int, const double*, const double*, int, int, int, int64_t, int64_t, const double*);
 };
 #define GS_PV(RY, WX) {"tb2 ry" #RY " wx" #WX, RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true>}
 #define GS_PVF(RY, WX) {"tb2 ry" #RY " wx" #WX " f-cached", RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true, false>}
@@ -3183,7 +3252,7 @@ int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, d
     const Coef k = make_coef(S, L, omega, 0.0);
     hipLaunchKernelGGL(V.kern, dim3((unsigned)tiles, (unsigned)((L->nz + zc - 1) / zc)), dim3(WAVE, (unsigned)wx, V.wy), 0,
                        st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc,
-                       0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0);
+                       0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0, nullptr);
     return launch_status();
 }
 

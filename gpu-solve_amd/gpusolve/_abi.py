@@ -59,6 +59,11 @@ KERNEL_API = {
     "gs_jacobi_sweep2_prolong": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double, C.c_double,
                                            C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(gs_level), C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "gs_jacobi_sweep2_prolong_ws_elems": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int]),
+    "gs_jacobi_sweep2_prolong_ws": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double,
+                                              C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(gs_level),
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, i64,
+                                              C.c_void_p]),
     "gs_jacobi_sweep2_restrict_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level),
                                                       C.POINTER(gs_level), C.c_int]),
     "gs_jacobi_sweep2_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,

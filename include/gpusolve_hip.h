@@ -113,8 +113,8 @@ int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L, in
  * trilinear interpolation of gs_prolong_add; bit-identical to gs_prolong_add followed by
  * gs_jacobi_sweep2, with the corrected iterate never stored. Replaces CpuSolver.cpp:127-135
  * (interpolate, v += e, jacobi(post)) for the first two post-smoothing sweeps. Supported
- * (gs_jacobi_sweep2_prolong_supported != 0) for LINEAR and NEWTON levels of rows <= 512 points whose
- * z0 is even (a level, a Z-slab of one, or a plane range of either); coarse_sub must then be NULL. Fine local
+ * (gs_jacobi_sweep2_prolong_supported != 0) for LINEAR and NEWTON levels of rows <= 512 points, and
+ * LINEAR levels of longer rows (with a workspace, gs_jacobi_sweep2_prolong_ws), whose z0 is even (a level, a Z-slab of one, or a plane range of either); coarse_sub must then be NULL. Fine local
  * plane z interpolates from coarse planes (z + z0) / 2 - coarse->z0 (+1); zlo / zhi as for
  * gs_jacobi_sweep2 — the ghost planes of an internal side are corrected too, from the coarse field's
  * planes under them (coarse ghost planes -1 / nz+1 must then be current). w: the level's newtonV
@@ -124,6 +124,17 @@ int gs_jacobi_sweep2_prolong(const gs_stencil* S, const gs_level* L, int mode, d
                              const double* v_in, const double* coarse_v, const double* coarse_sub,
                              const gs_level* coarse, double* v_out, const double* f, const double* w, int zlo,
                              int zhi, hipStream_t stream);
+/* The same with a device workspace, which LINEAR levels of rows longer than 512 points (the column-block
+ * pair: BASELINE config #5's 1024-point rows) need: gs_jacobi_sweep2_prolong_ws_elems doubles (0 when
+ * none is needed; gs_jacobi_sweep2_prolong is this call with no workspace and fails with GS_EINVAL
+ * where one is needed). The launch first writes the corrected iterate of the four columns around
+ * every interior column-block boundary into it (the neighbouring blocks' edge columns), then runs the
+ * pair; concurrent launches need separate workspaces. */
+int64_t gs_jacobi_sweep2_prolong_ws_elems(const gs_stencil* S, const gs_level* L, int mode);
+int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma,
+                                const double* v_in, const double* coarse_v, const double* coarse_sub,
+                                const gs_level* coarse, double* v_out, const double* f, const double* w, int zlo,
+                                int zhi, double* ws, int64_t ws_elems, hipStream_t stream);
 /* The first pre-smoothing pair of a 2-sweep pre-smoothing, the residual of its result and the full
  * weighting in one pass: v_out = S(S(v_in)), coarse_a (and coarse_b if not NULL) = R(f - A(v_out)) on
  * the coarse interior, partials (may be NULL) = gs_jacobi_sweep2_restrict_num_partials per-block sums

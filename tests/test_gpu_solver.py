@@ -51,7 +51,9 @@ def test_all_small_histories(histories):
     print("worst relative deviation per case:", max(worst.values()))
 
 
-@pytest.mark.parametrize("dims", [(31, 31, 31), (32, 32, 32), (17, 9, 12), (64, 48, 40), (127, 127, 127)])
+@pytest.mark.parametrize("dims", [(31, 31, 31), (32, 32, 32), (17, 9, 12), (64, 48, 40), (127, 127, 127),
+                                  # rows > 512 points: column-block pairs, fused prolongation with the edge strip
+                                  (1024, 9, 8), (700, 12, 10), (1100, 10, 12)])
 def test_linear_fields_bit_identical(dims):
     p = gsv.GridParams(maxiter=4, tol=0.0, gridDim=dims, mode=0)
     with gsv.HipGridData(p) as g:

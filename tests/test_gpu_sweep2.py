@@ -196,7 +196,20 @@ def test_zero_iterate_rejected_in_fas_mode():
 
 
 PRO_SHAPES = [(1, 1, 1), (2, 5, 3), (5, 4, 33), (127, 9, 17), (128, 8, 8), (129, 13, 40), (257, 6, 10),
-              (500, 7, 9), (512, 4, 5), (64, 64, 64), (63, 31, 65), (200, 33, 70)]
+              (500, 7, 9), (512, 4, 5), (64, 64, 64), (63, 31, 65), (200, 33, 70),
+              # rows > 512 points: column blocks (BASELINE config #5's 1024-point rows), edge columns through
+              # the workspace; 513 / 1025: a last block of one column
+              (513, 5, 6), (700, 9, 11), (1024, 6, 9), (1025, 4, 7), (1100, 13, 5), (1536, 3, 4)]
+
+
+def prolong_ws(S, L, mode, v, c, sub, Lc, out, f, w, zlo, zhi):
+    """gs_jacobi_sweep2_prolong_ws with a workspace of the size the level needs (none for rows <= 512)."""
+    n = k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(S), C.byref(L), mode)
+    ws = torch.empty(max(n, 1), dtype=torch.float64, device="cuda") if n > 0 else None
+    rc = k().gs_jacobi_sweep2_prolong_ws(C.byref(S), C.byref(L), mode, 0.8, 1.0, v, c, sub, C.byref(Lc), out, f, w,
+                                         zlo, zhi, ws.data_ptr() if ws is not None else None, n, st())
+    torch.cuda.synchronize()
+    return rc
 
 
 @pytest.mark.parametrize("mode", [0, 2])
@@ -224,9 +237,11 @@ def test_prolong_fused_pair_bit_identical(shape, mode):
                             st()))
     # fused
     v2, out = DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz)
-    ok(k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v2.ptr, c.ptr, None,
-                                    C.byref(Lc), out.ptr, f.ptr, wp, 0, 0, st()))
+    ok(prolong_ws(stencil(), L, mode, v2.ptr, c.ptr, None, Lc, out.ptr, f.ptr, wp, 0, 0))
     np.testing.assert_array_equal(out.to_xyz(), out_ref.to_xyz())
+    if nx > 512:  # the call without a workspace is refused where one is needed
+        assert k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v2.ptr, c.ptr, None,
+                                            C.byref(Lc), out.ptr, f.ptr, wp, 0, 0, st()) == gsv._abi.GS_EINVAL
     np.testing.assert_array_equal(v2.to_xyz(), v0)  # the input iterate is left as it was
 
 
@@ -236,7 +251,11 @@ PRO_SPLITS = [((64, 64, 64), [(1, 2), (63, 64), (3, 62)]),
               ((63, 31, 65), [(1, 2), (63, 65), (3, 62)]),  # odd extent: three top planes
               ((200, 33, 70), [(1, 14), (15, 40), (41, 70)]),
               ((5, 4, 33), [(1, 2), (3, 30), (31, 33)]),
-              ((127, 9, 17), [(1, 1), (2, 2), (1, 2), (3, 14), (15, 17), (17, 17)])]  # (2, 2): even start, refused
+              ((127, 9, 17), [(1, 1), (2, 2), (1, 2), (3, 14), (15, 17), (17, 17)]),  # (2, 2): even start, refused
+              # column blocks: config #5's per-rank slab split (bottom pair, top planes, interior)
+              ((1024, 7, 24), [(1, 2), (23, 24), (3, 22)]),
+              ((700, 11, 19), [(1, 2), (17, 19), (3, 16)]),
+              ((1100, 5, 20), [(1, 6), (7, 12), (13, 20)])]
 
 
 @pytest.mark.parametrize("coarse_view", [False, True])
@@ -255,8 +274,7 @@ def test_prolong_fused_pair_plane_ranges(shape, ranges, coarse_view):
     v, f, c, out_ref = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
                         DevField(*cd).from_xyz(c0), DevField(nx, ny, nz))
     Lc = c.level(2 * h)
-    ok(k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, c.ptr, None, C.byref(Lc),
-                                    out_ref.ptr, f.ptr, None, 0, 0, st()))
+    ok(prolong_ws(stencil(), L, 0, v.ptr, c.ptr, None, Lc, out_ref.ptr, f.ptr, None, 0, 0))
     out = DevField(nx, ny, nz)
     for z1, z2 in ranges:
         off = 8 * (z1 - 1) * L.ldz
@@ -266,9 +284,8 @@ def test_prolong_fused_pair_plane_ranges(shape, ranges, coarse_view):
             z0c = (z1 - 1) // 2
             cptr = c.ptr + 8 * z0c * Lc.ldz
             cl = gsv._abi.gs_level(Lc.nx, Lc.ny, min((z2 - z1 + 2) // 2, cd[2] - z0c), Lc.ldy, Lc.ldz, z0c, 2 * h)
-        rc = k().gs_jacobi_sweep2_prolong(C.byref(stencil()), C.byref(sub), 0, 0.8, 1.0, v.ptr + off, cptr, None,
-                                          C.byref(cl), out.ptr + off, f.ptr + off, None, int(z1 > 1), int(z2 < nz),
-                                          st())
+        rc = prolong_ws(stencil(), sub, 0, v.ptr + off, cptr, None, cl, out.ptr + off, f.ptr + off, None,
+                        int(z1 > 1), int(z2 < nz))
         if z1 % 2 == 0:
             assert rc == gsv._abi.GS_EINVAL  # plane parities must be the global ones
         else:
@@ -285,7 +302,31 @@ def test_prolong_fused_pair_rejects():
                                       C.byref(c.level(1 / 9.0)), out.ptr, f.ptr, None, 0, 0, st())
     assert rc == gsv._abi.GS_EINVAL  # NEWTON needs newtonV
     L2 = DevField(600, 4, 4).level(0.2)
-    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 0) == 0  # rows > 512
+    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 0) == 1  # rows > 512: LINEAR
+    assert k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(stencil()), C.byref(L2), 0) == 1 * (4 + 4) * 4 * (4 + 2)
+    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 2) == 0  # NEWTON: k_tb2 rows
+    L3 = DevField(512, 4, 4).level(0.2)
+    assert k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(stencil()), C.byref(L3), 0) == 0
+
+
+def test_prolong_fused_pair_full_1024_plane_set():
+    """Config #5's row length on a full 1024 x 1024 plane set (8 planes): the column-block prolongation pair
+    against gs_prolong_add + the plain pair, bit for bit."""
+    rng = np.random.default_rng(10241)
+    shape = (1024, 1024, 8)
+    nx, ny, nz = shape
+    cd = [x // 2 for x in shape]
+    h = 1.0 / 1025
+    v0, f0, c0 = rand_full(rng, *shape), rand_full(rng, *shape, 100.0), rand_full(rng, *cd)
+    L = DevField(*shape).level(h)
+    v, f, c, out_ref = (DevField(*shape).from_xyz(v0), DevField(*shape).from_xyz(f0), DevField(*cd).from_xyz(c0),
+                        DevField(*shape))
+    Lc = c.level(2 * h)
+    ok(k().gs_prolong_add(c.ptr, None, C.byref(Lc), v.ptr, C.byref(L), st()))
+    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, out_ref.ptr, f.ptr, None, 0, 0, st()))
+    v2, out = DevField(*shape).from_xyz(v0), DevField(*shape)
+    ok(prolong_ws(stencil(), L, 0, v2.ptr, c.ptr, None, Lc, out.ptr, f.ptr, None, 0, 0))
+    np.testing.assert_array_equal(out.to_xyz(), out_ref.to_xyz())
 
 
 def test_sweep2_full_1024_plane():

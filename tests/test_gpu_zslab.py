@@ -5,6 +5,8 @@ assembled fields must be bit-identical to the single-GPU solve in every mode; th
 histories differ only by the norm's summation order (rank partials are summed in rank order)."""
 import ctypes as C
 
+import math
+
 import numpy as np
 import pytest
 
@@ -53,14 +55,18 @@ def test_sweeps_bit_identical(dims, nranks):
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("dims,nranks,min_points", [((32, 32, 32), 2, 0), ((31, 31, 63), 4, 0),
                                                     ((48, 40, 64), 3, 4096), ((64, 64, 64), 2, -1),
-                                                    ((64, 256, 64), 2, -1), ((32, 512, 64), 4, -1)])
+                                                    ((64, 256, 64), 2, -1), ((32, 512, 64), 4, -1),
+                                                    # column-block rows: the prolongation pair's edge strip on
+                                                    # the boundary and interior streams of every rank
+                                                    ((1024, 32, 64), 2, -1)])
 def test_solve_matches_single_gpu(mode, dims, nranks, min_points):
     p = gsv.GridParams(maxiter=3 if mode == 2 else 5, tol=0.0, gridDim=dims, mode=mode)
     ref_h, ref_v = single(p, 0, True)
     h, v = loopback(p, nranks, min_points, 0, True)
     assert len(h) == len(ref_h)
     for a, b in zip(h, ref_h):
-        assert rel(a, b) < 1e-12, (a, b)
+        # a diverging draw (NONLINEAR at 1024x32x64) ends in the same inf / nan on both sides
+        assert a == b or (math.isnan(a) and math.isnan(b)) or rel(a, b) < 1e-12, (a, b)
     # Newton keeps its result in newtonV; v is the last inner correction — equal in every mode
     np.testing.assert_array_equal(v[:, :, 1:-1], ref_v[:, :, 1:-1])
 

@@ -8,7 +8,9 @@ the step time on the compute stream (fork to join, HIP events) and, from a kerne
 stand-in exchange started and ended relative to the interior launch.
     python tools/exchange_probe.py [reps]                    (step times)
     rocprofv3 --kernel-trace -d <dir> -o run --output-format csv -- python tools/exchange_probe.py 3
-    python tools/exchange_probe.py --analyze <dir>/run_kernel_trace.csv"""
+    python tools/exchange_probe.py --analyze <dir>/run_kernel_trace.csv
+r03: 'pipelined xK' times K consecutive steps under the driver's pipelined schedule (HipSolver::jacobi),
+per step: exchange k overlaps interior k+1, the compute stream never waits for an exchange."""
 import csv
 import ctypes as C
 import json
@@ -123,7 +125,45 @@ def main():
             main_s.wait_stream(ist)
         main_s.wait_stream(comm_s if blocks else bnd_s)
 
+    def pipe_steps(blocks, nsteps):
+        """r03 driver (HipSolver::jacobi): a sequence of overlapped steps in which the compute stream never
+        waits for an exchange. Boundary k waits for interior k-1 and exchange k-1; the interior k waits for
+        boundary k-1 only; exchange k follows boundary k on the comm stream; the last exchange is joined."""
+        evb = [None, None]
+        ev_x = None
+        for k_ in range(nsteps):
+            ev_a = torch.cuda.Event()
+            ev_a.record(main_s)
+            bnd_s.wait_event(ev_a)
+            if ev_x is not None:
+                bnd_s.wait_event(ev_x)
+            pair(1, 2, bnd_s)
+            pair(NZ - 1, NZ, bnd_s)
+            evb[k_ & 1] = torch.cuda.Event()
+            evb[k_ & 1].record(bnd_s)
+            comm_s.wait_event(evb[k_ & 1])
+            if k_ > 0:
+                main_s.wait_event(evb[(k_ - 1) & 1])
+            pair(3, NZ - 2, main_s)
+            if blocks:
+                assert k.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
+                                     comm_s.cuda_stream) == 0
+            ev_x = torch.cuda.Event()
+            ev_x.record(comm_s)
+        main_s.wait_event(ev_x)
+        main_s.wait_event(evb[(nsteps - 1) & 1])
+
     res = {}
+    for b in (0, 8, 32):
+        for _ in range(2):
+            pipe_steps(b, reps)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(main_s)
+        pipe_steps(b, reps)
+        e1.record(main_s)
+        torch.cuda.synchronize()
+        res[f"pipelined x{reps} exchange={'fat x%d' % b if b else 'none'}"] = round(e0.elapsed_time(e1) / reps, 4)
     settings = [(v_, b, "0") for v_ in ("cur", "first", "delay-1", "delay-3", "delay-6", "delay-12")
                 for b in (0, 8, 32)]
     if os.environ.get("PROBE_MASK"):
