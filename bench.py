@@ -278,7 +278,7 @@ def triad_ceiling(n):
     24 B per element) on arrays of the level's size — the best of a few grid sizes of the streaming
     triad kernel (gs_debug_bw). Boxes differ by up to ~25%, so the kernel's fraction of it is reported
     next to the fraction of the 8 TB/s datasheet peak."""
-    kl = gsv.kernels()
+    kl = gsv.diag()  # the streaming probe lives in the diagnostics library
     A = torch.rand(n, dtype=torch.float64, device="cuda")
     B = torch.rand(n, dtype=torch.float64, device="cuda")
     O = torch.empty(n, dtype=torch.float64, device="cuda")

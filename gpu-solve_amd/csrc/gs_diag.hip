@@ -1,0 +1,538 @@
+// gs_diag.hip — libgpusolve_diag.so (include/gpusolve_diag.h): measurement and tuning code that is NOT
+// part of the product: the tuning variants of the sweep and pair kernels (tools/kbench.py), streaming
+// bandwidth probes (bench.py's measured ceiling, tools/), the exact-division check, and k_prr — the
+// pre-smoothing pair + residual + restriction in one pass, built, bit-identical and measured slower than
+// the two passes the driver runs, kept as a tested operator. Only tools/, tests/ and
+// bench.py's measured-ceiling leg load this library.
+#include "gs_device.hpp"
+#include "gpusolve_diag.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// The first pre-smoothing pair, the residual of its result and the full-weighting restriction in ONE
+// pass (k_prr, LINEAR; CpuSolver.cpp:94-99 with preSmoothing = 2: jacobi x2, compResidual, restrict).
+// Level 0 of a 2+2 V-cycle is then two passes instead of three: this kernel reads v and f once and
+// writes v'' and the coarse f (25 B per fine point instead of 24 + 17).
+// A block is the whole x-row — PRR_WX waves, ONE column per lane, so a lane's z-windows of four stages
+// fit its registers — times a tile of PRR_T = 4 output rows y0..y0+3 (y0 odd: the tile holds the
+// centres of coarse rows (y0+1)/2 and (y0+3)/2). The restriction needs r on rows y0..y0+4, r needs v''
+// on y0-1..y0+5, v'' needs sweep 1 on y0-2..y0+6 and sweep 1 needs v on y0-3..y0+7: every stage's
+// extra rows are recomputed in-lane (no y exchange). Wavefront along z, at step z: sweep 1 at plane
+// z, sweep 2 at z-1, r at z-2, and the restriction of coarse plane Z = (z-4)/2 from r at z-5..z-3
+// (one step late, so that every x-edge it reads was published before this step's one barrier).
+// x-neighbours: DPP lane shifts, the columns beyond a wave's edges (v, sweep 1, sweep 2) through LDS;
+// r goes to an LDS ring of five planes that the restriction reads directly. A block walks a chunk of
+// coarse planes Zb..Ze: fine output planes 2Zb-1..2Ze (the last chunk up to nz), with the pipeline's
+// z-halo (sweep 1 from 2Zb-3, r up to 2Ze+1) recomputed at the chunk ends. Every point uses the
+// expression of k_tb2y / k_rr2 (same order, same boundary values), so v'' and the coarse f are
+// bit-identical to gs_jacobi_sweep2 + gs_residual_restrict; the norm partials are those of r = f - A v
+// (the input), as the speculative pair's, in this kernel's block order.
+// MEASURED SLOWER than the two passes it replaces, so the driver does not use it: 1.45 vs 1.10 ms at
+// 512^3 (tools/prr_bench.py). Its traffic is 1.06 x the 25 B/point, but the in-lane recomputation
+// costs 21 stencil evaluations per 4 outputs against 15 for pair + k_rr2, and one column per lane
+// doubles the DPP shifts: PMC 1.54 x the VALU instructions of the two kernels at 254 VGPRs (no
+// prefetch room beyond one plane of v). Kept as a tested operator (tests/test_gpu_pair_restrict.py).
+constexpr int PRR_WX = 8, PRR_T = 4, PRR_RS = 5; // x-waves, output rows per block, r ring planes
+
+template <bool UN>
+__global__ __launch_bounds__(WAVE* PRR_WX) void k_prr(Coef k, const double* __restrict__ v, const double* __restrict__ f,
+                                                      double* __restrict__ out, double* __restrict__ partials,
+                                                      double* __restrict__ ca, double* __restrict__ cb, int nx, int ny,
+                                                      int nz, int64_t ldy, int64_t ldz, int cnx, int cny, int cnz,
+                                                      int64_t cldy, int64_t cldz, int ZC)
+{
+    // local rows i (global y0 + i): v -3..7, sweep 1 -2..6, sweep 2 -1..5, r 0..4
+    constexpr int NV = 11, N1 = 9, N2 = 7, NR = 5;
+    constexpr int NE = N1 + N2 + NR; // x-edge values per wave side and plane parity
+    constexpr int RW = WAVE * PRR_WX + 2; // r ring row: columns 0 .. 64 WX + 1
+    __shared__ double edge[2][PRR_WX + 2][2][NE];
+    // r of the last planes, every column of the tile's rows 0..4: slot p mod 5 (the restriction at step z
+    // reads planes z-5..z-3 while a wave one step ahead writes z-1 — five slots keep them apart)
+    __shared__ double rring[PRR_RS][NR][RW];
+    __shared__ double red[PRR_WX];
+    const int lane = threadIdx.x;
+    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int WX = blockDim.y;
+    const int tid = lane + WAVE * wx;
+    for (int i = tid; i < 2 * (PRR_WX + 2) * 2 * NE; i += WAVE * WX) (&edge[0][0][0][0])[i] = 0.0;
+    for (int i = tid; i < PRR_RS * NR * RW; i += WAVE * WX) (&rring[0][0][0])[i] = 0.0;
+    __syncthreads();
+    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+    const int y0 = 1 + (int)(tile % gridDim.x) * PRR_T;
+    const int Zb = 1 + (int)(tile / gridDim.x) * ZC, Ze = min(Zb + ZC - 1, cnz);
+    const int zb = 2 * Zb - 1, ze = Ze == cnz ? nz : 2 * Ze; // output planes of v''
+    const int rlast = 2 * Ze + 1;                            // last plane of r
+    const int s2last = max(ze, rlast + 1), s1last = s2last + 1;
+    const int x = 1 + wx * WAVE + lane;
+    const int xl = min(x, nx + 1);
+    const bool okx = x <= nx;
+    int64_t roff[NV]; // rows -3..7 at index i + 3
+    bool rowc[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        const int y = y0 - 3 + i;
+        roff[i] = (int64_t)min(max(y, 0), ny + 1) * ldy;
+        rowc[i] = y >= 1 && y <= ny;
+    }
+    auto at = [&](const double* b, int i, int p) {
+        return b + xl + roff[i + 3] + (int64_t)min(max(p, 0), nz + 1) * ldz;
+    };
+    auto pin = [&](int p) { return p >= 1 && p <= nz; };
+    auto rslot = [](int p) { return ((p % PRR_RS) + PRR_RS) % PRR_RS; };
+
+    double Vm[N1], Vc[NV], Vn[NV], VL[NV]; // v at z-1 (rows -2..6), z, z+1, z+2 in flight (rows -3..7)
+    double F0[N1], F1[N2], F2[NR];        // f at z (rows -2..6), z-1 (-1..5), z-2 (0..4)
+    double S1a[N2], S1b[N1];              // sweep 1 at z-2 (rows -1..5), z-1 (-2..6)
+    double S2a[NR], S2b[N2];              // sweep 2 at z-3 (rows 0..4), z-2 (-1..5)
+#pragma unroll
+    for (int i = 0; i < N1; i++) Vm[i] = *at(v, i - 2, zb - 3);
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        Vc[i] = *at(v, i - 3, zb - 2);
+        Vn[i] = *at(v, i - 3, zb - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < N2; i++) {
+        F1[i] = 0.0;
+        S1a[i] = 0.0;
+        S2b[i] = 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < N1; i++) S1b[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+        F2[i] = 0.0;
+        S2a[i] = 0.0;
+    }
+    double sumsq = 0.0;
+    auto lds_barrier = [] {
+        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): LDS only, the loads stay in flight
+        __builtin_amdgcn_s_barrier();
+    };
+
+    for (int z = zb - 2; z <= s1last + 1; z++) {
+        // ---- loads: v(z+2) for the next step, f(z) for this step's sweep 1 ----
+#pragma unroll
+        for (int i = 0; i < NV; i++) VL[i] = *at(v, i - 3, z + 2);
+#pragma unroll
+        for (int i = 0; i < N1; i++) F0[i] = *at(f, i - 2, z);
+        // ---- publish x-edges: v(z) rows -2..6, sweep 1 (z-1) rows -1..5, sweep 2 (z-2) rows 0..4 ----
+        const int ph = z & 1;
+        if (lane == 0 || lane == WAVE - 1) {
+            const int sd = lane == 0 ? 0 : 1;
+#pragma unroll
+            for (int i = 0; i < N1; i++) edge[ph][wx + 1][sd][i] = Vc[i + 1];
+#pragma unroll
+            for (int i = 0; i < N2; i++) edge[ph][wx + 1][sd][N1 + i] = S1b[i + 1];
+#pragma unroll
+            for (int i = 0; i < NR; i++) edge[ph][wx + 1][sd][N1 + N2 + i] = S2b[i + 1];
+        }
+        lds_barrier();
+        // the columns left of lane 0 / right of lane 63 (LDS broadcast reads, straight into the DPP's old operand)
+        auto CL = [&](int i) { return edge[ph][wx][1][i]; };
+        auto CR = [&](int i) { return edge[ph][wx + 2][0][i]; };
+
+        // ---- restriction of coarse plane Z from r at 2Z-1, 2Z, 2Z+1 (= z-5, z-4, z-3), read from the ring ----
+        if (!(z & 1) && (z - 4) / 2 >= Zb && (z - 4) / 2 <= Ze) {
+            const int Z = (z - 4) / 2;
+            const int X = x >> 1;
+            const int sl[3] = {rslot(z - 5), rslot(z - 4), rslot(z - 3)};
+            if (!(x & 1) && X <= cnx) {
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const int Y = (y0 + 1) / 2 + t, ic = 1 + 2 * t; // centre row y0 + ic = 2Y
+                    if (Y > cny) continue;
+                    double acc = 0.0;
+#pragma unroll
+                    for (int a = -1; a <= 1; a++)
+#pragma unroll
+                        for (int b = -1; b <= 1; b++)
+#pragma unroll
+                            for (int c = -1; c <= 1; c++) {
+                                const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
+                                                   ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                                acc += wgt * rring[sl[c + 1]][ic + b][x + a];
+                            }
+                    const int64_t q = X + Y * cldy + (int64_t)Z * cldz;
+                    ca[q] = acc;
+                    if (cb) cb[q] = acc;
+                }
+            }
+        }
+
+        // ---- sweep 1 at plane z, rows -2..6 ----
+        double S1n[N1];
+        if (z <= s1last) {
+            double q[N1];
+#pragma unroll
+            for (int i = 0; i < N1; i++) {
+                const double c = Vc[i + 1];
+                const double xm = lane_from_left<true>(c, CL(i)), xp = lane_from_right<true>(c, CR(i));
+                q[i] = stencil_sum<UN>(k, c, xp, xm, Vc[i + 2], Vc[i], Vn[i + 1], Vm[i]);
+            }
+            div_hh_n(k, q);
+            const bool pz = pin(z);
+            const bool own = partials && z >= zb && z <= ze && pz && okx;
+#pragma unroll
+            for (int i = 0; i < N1; i++) {
+                const double c = Vc[i + 1];
+                const double r0 = F0[i] - q[i];
+                const double n = jacobi_update<GS_LINEAR>(k, c, r0, 0.0);
+                S1n[i] = (pz && rowc[i + 1] && okx) ? n : c;
+                if (own && i >= 2 && i <= 5 && rowc[i + 1]) sumsq += r0 * r0;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < N1; i++) S1n[i] = 0.0;
+        }
+        // ---- sweep 2 at plane z-1, rows -1..5 (stored: rows 0..3 of the output planes) ----
+        double S2n[N2];
+        if (z - 1 >= zb - 1 && z - 1 <= s2last) {
+            double q[N2];
+#pragma unroll
+            for (int i = 0; i < N2; i++) {
+                const double c = S1b[i + 1];
+                const double xm = lane_from_left<true>(c, CL(N1 + i)), xp = lane_from_right<true>(c, CR(N1 + i));
+                q[i] = stencil_sum<UN>(k, c, xp, xm, S1b[i + 2], S1b[i], S1n[i + 1], S1a[i]);
+            }
+            div_hh_n(k, q);
+            const int p = z - 1;
+            const bool pz = pin(p);
+            const bool st = p >= zb && p <= ze && pz && okx;
+#pragma unroll
+            for (int i = 0; i < N2; i++) {
+                const double c = S1b[i + 1];
+                const double n = jacobi_update<GS_LINEAR>(k, c, F1[i] - q[i], 0.0);
+                S2n[i] = (pz && rowc[i + 2] && okx) ? n : c;
+                if (st && i >= 1 && i <= 4 && rowc[i + 2])
+                    __builtin_nontemporal_store(n, out + x + roff[i + 2] + (int64_t)p * ldz);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < N2; i++) S2n[i] = 0.0;
+        }
+        // ---- r = f - A v'' at plane z-2, rows 0..4 (0 outside the interior) -> the ring ----
+        if (z - 2 >= zb && z - 2 <= rlast) {
+            double q[NR];
+#pragma unroll
+            for (int i = 0; i < NR; i++) {
+                const double c = S2b[i + 1];
+                const double xm = lane_from_left<true>(c, CL(N1 + N2 + i)), xp = lane_from_right<true>(c, CR(N1 + N2 + i));
+                q[i] = stencil_sum<UN>(k, c, xp, xm, S2b[i + 2], S2b[i], S2n[i + 1], S2a[i]);
+            }
+            div_hh_n(k, q);
+            const bool pz = pin(z - 2);
+            const int sl = rslot(z - 2);
+#pragma unroll
+            for (int i = 0; i < NR; i++) rring[sl][i][x] = (pz && rowc[i + 3] && okx) ? F2[i] - q[i] : 0.0;
+        }
+        // ---- rotate ----
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            S2a[i] = S2b[i + 1];
+            F2[i] = F1[i + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < N2; i++) {
+            S2b[i] = S2n[i];
+            S1a[i] = S1b[i + 1];
+            F1[i] = F0[i + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < N1; i++) {
+            S1b[i] = S1n[i];
+            Vm[i] = Vc[i + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            Vc[i] = Vn[i];
+            Vn[i] = VL[i];
+        }
+    }
+    if (partials) {
+        sumsq = wave_sum(sumsq);
+        if (lane == 0) red[wx] = sumsq;
+        __syncthreads();
+        if (tid == 0) {
+            double t = 0.0;
+            for (int i = 0; i < WX; i++) t += red[i];
+            partials[tile] = t;
+        }
+    }
+}
+
+// ---- tuning variants of the LINEAR sweep (tools/kbench.py) -------------------------------------
+using RbKernel = void (*)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
+                          int64_t, int);
+struct Variant {
+    const char* name;
+    int ry, wy, zc;
+    bool oneD;
+    RbKernel kern;
+};
+#define GS_VX(RY, W, ZC, NT, X, NTV, TAG) \
+    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, RY, W, ZC, X, k_rb<GS_LINEAR, 0, false, RY, W, true, NT, X, NTV>}
+const Variant kVariants[] = {
+    GS_VX(2, 4, 32, true, false, false, "dpp nt (production shape)"),
+    GS_VX(2, 4, 32, false, false, false, "dpp"),
+    GS_VX(2, 4, 32, true, true, false, "dpp nt xcd"),
+    GS_VX(2, 4, 32, true, false, true, "dpp nt ntv"),
+    GS_VX(2, 4, 16, true, false, false, "dpp nt"),
+    GS_VX(2, 4, 64, true, false, false, "dpp nt"),
+    GS_VX(2, 8, 32, true, false, false, "dpp nt"),
+    GS_VX(2, 2, 32, true, false, false, "dpp nt"),
+    GS_VX(1, 8, 32, true, false, false, "dpp nt"),
+    GS_VX(4, 4, 32, true, false, false, "dpp nt"),
+    GS_VX(4, 2, 32, true, false, false, "dpp nt"),
+    GS_VX(8, 2, 32, true, false, false, "dpp nt"),
+};
+#undef GS_VX
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// Bandwidth ceilings. KIND 0 read a, 1 write out, 2 copy a->out, 3 triad out = a + 0.8 b.
+// UNROLL independent dwordx4 per thread per iteration, NT non-temporal loads/stores.
+template <int KIND, int UNROLL, bool NT>
+__global__ __launch_bounds__(256) void k_bw(double* __restrict__ out, const double* __restrict__ a,
+                                            const double* __restrict__ b, int64_t n2, double* __restrict__ sink)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    double acc = 0.0;
+    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n2; i0 += stride * UNROLL) {
+        double2 va[UNROLL], vb[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) {
+            const int64_t i = i0 + u * stride;
+            if (i < n2) {
+                if (KIND != 1) va[u] = ld2s<NT>(a + 2 * i);
+                if (KIND == 3) vb[u] = ld2s<NT>(b + 2 * i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) {
+            const int64_t i = i0 + u * stride;
+            if (i >= n2) continue;
+            if (KIND == 0) acc += va[u].x + va[u].y;
+            else if (KIND == 1) st2s<NT>(out + 2 * i, 1.0, 2.0);
+            else if (KIND == 2) st2s<NT>(out + 2 * i, va[u].x, va[u].y);
+            else st2s<NT>(out + 2 * i, va[u].x + 0.8 * vb[u].x, va[u].y + 0.8 * vb[u].y);
+        }
+    }
+    if (KIND == 0 && acc == -1.2345e300) *sink = acc; // keeps the loads alive
+}
+
+// A copy with the resource footprint of RCCL's gfx950 transport kernels (ncclDevKernel_Generic: 256
+// VGPRs, 37664 B of LDS per 256-thread workgroup): the clobber of v255 makes the allocator reserve
+// every VGPR. Stands in for the ghost exchange in tools/exchange_probe.py (when does a workgroup
+// that needs a whole SIMD's registers get a CU while the interior pair holds the GPU?).
+__global__ __launch_bounds__(256) void k_fatcopy(double* __restrict__ out, const double* __restrict__ a, int64_t n2)
+{
+    __shared__ double pad[4708];
+    asm volatile("" ::: "v255");
+    for (int i = threadIdx.x; i < 4708; i += 256) pad[i] = 0.0;
+    __syncthreads();
+    const double z = pad[(threadIdx.x * 17) % 4708];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const double2 x = ld2s<true>(a + 2 * i);
+        st2s<true>(out + 2 * i, x.x + z, x.y + z);
+    }
+}
+
+// One wave that sleeps `iters` x s_sleep(127) (~3.4 us each at 2.4 GHz) and touches no memory: a delay
+// on a stream, e.g. between the boundary planes and the interior launch of an overlapped Z-slab sweep
+// so that the exchange's kernels are dispatched first (tools/exchange_probe.py).
+__global__ __launch_bounds__(64) void k_sleep(int64_t iters)
+{
+    for (int64_t i = 0; i < iters; i++) __builtin_amdgcn_s_sleep(127);
+}
+
+// div_hh against the plain division (tests: bitwise equality over all magnitudes)
+__global__ __launch_bounds__(256) void k_div_check(const double* __restrict__ a, int64_t n, Coef k,
+                                                   double* __restrict__ fast, double* __restrict__ ref)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fast[i] = div_hh(k, a[i]);
+    ref[i] = a[i] / k.hh;
+}
+
+__global__ __launch_bounds__(256) void k_triad(double* __restrict__ out, const double* __restrict__ a,
+                                               const double* __restrict__ b, int64_t n2)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const double2 x = reinterpret_cast<const double2*>(a)[i], y = reinterpret_cast<const double2*>(b)[i];
+        reinterpret_cast<double2*>(out)[i] = make_double2(x.x + 0.8 * y.x, x.y + 0.8 * y.y);
+    }
+}
+
+} // namespace
+
+// =============================================================================================
+extern "C" {
+
+// k_prr geometry: the whole row in one block (<= 512 points), 4-row tiles, chunks of coarse planes for
+// ~512 blocks (one 8-wave block per CU, two rounds at 512^3; 4..64 coarse planes: the chunk ends
+// recompute five planes of the pipeline)
+static bool prr_plan(const gs_stencil* S, const gs_level* fl, const gs_level* cl, int mode, int* zc, dim3* g, dim3* b)
+{
+    if (!S || !valid_stencil(S) || !canonical_order(S) || mode != GS_LINEAR || bad_level(fl) || bad_level(cl) ||
+        !make_coef(S, fl, 0.0, 0.0).unit || // the unit-neighbour stencil sum (the general one spills here)
+        fl->z0 != 0 || cl->z0 != 0 || fl->nx < 1 || fl->nx > WAVE * PRR_WX || fl->ny < 1 || fl->nz < 2 ||
+        cl->nx != fl->nx / 2 || cl->ny != fl->ny / 2 || cl->nz != fl->nz / 2 || cl->nx < 1 || cl->ny < 1)
+        return false;
+    const int64_t tiles = (fl->ny + PRR_T - 1) / PRR_T;
+    int64_t c = (cl->nz * tiles + 511) / 512;
+    c = c < 4 ? 4 : (c > 64 ? 64 : c);
+    *zc = (int)c;
+    *g = dim3((unsigned)tiles, (unsigned)((cl->nz + c - 1) / c));
+    *b = dim3(WAVE, (unsigned)((fl->nx + WAVE - 1) / WAVE));
+    return true;
+}
+
+int gs_jacobi_sweep2_restrict_supported(const gs_stencil* S, const gs_level* fl, const gs_level* cl, int mode)
+{
+    int zc;
+    dim3 g, b;
+    return prr_plan(S, fl, cl, mode, &zc, &g, &b) ? 1 : 0;
+}
+
+int64_t gs_jacobi_sweep2_restrict_num_partials(const gs_stencil* S, const gs_level* fl, const gs_level* cl)
+{
+    int zc;
+    dim3 g, b;
+    return prr_plan(S, fl, cl, GS_LINEAR, &zc, &g, &b) ? (int64_t)g.x * g.y : 0;
+}
+
+int gs_jacobi_sweep2_restrict(const gs_stencil* S, const gs_level* fl, double omega, const double* v_in,
+                              double* v_out, const double* f, double* partials, double* ca, double* cb,
+                              const gs_level* cl, hipStream_t st)
+{
+    int zc;
+    dim3 g, b;
+    if (!prr_plan(S, fl, cl, GS_LINEAR, &zc, &g, &b) || !v_in || !v_out || !f || !ca || v_in == v_out)
+        return GS_EINVAL;
+    const Coef k = make_coef(S, fl, omega, 0.0);
+    hipLaunchKernelGGL((k_prr<true>), g, b, 0, st, k, v_in, f, v_out, partials, ca, cb, (int)fl->nx, (int)fl->ny,
+                       (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, zc);
+    return launch_status();
+}
+
+int gs_debug_num_variants(void) { return kNumVariants; }
+
+const char* gs_debug_variant_name(int variant)
+{
+    return (variant >= 0 && variant < kNumVariants) ? kVariants[variant].name : "";
+}
+
+int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
+                           double* v_out, const double* f, hipStream_t st)
+{
+    if (variant < 0 || variant >= kNumVariants || !S || bad_level(L) || !canonical_order(S) || !v_in || !v_out ||
+        !f || v_in == v_out)
+        return GS_EINVAL;
+    if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
+    const Variant& V = kVariants[variant];
+    const Coef k = make_coef(S, L, omega, 0.0);
+    hipLaunchKernelGGL(V.kern, rb_grid(L, V.ry, V.wy, V.zc, V.oneD), dim3(WAVE, V.wy), 0, st, k, v_in, f, nullptr,
+                       v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, V.zc);
+    return launch_status();
+}
+
+// Fused-pair shapes for tools/kbench.py --pairs (LINEAR): output rows per wave x max waves per
+// block (the launch bound, hence the VGPR budget: 4 waves -> 512, 8 waves -> 256 per lane).
+struct PairVariant {
+    const char* name;
+    int ry, wxmax, wy;
+    void (*kern)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
+                 int64_t, int, int, int, const double*, const double*, int, int, int, int64_t, int64_t, const double*);
+};
+#define GS_PV(RY, WX) {"tb2 ry" #RY " wx" #WX, RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true>}
+#define GS_PVF(RY, WX) {"tb2 ry" #RY " wx" #WX " f-cached", RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true, false>}
+#define GS_PVY(RY, NTF, SPEC, TAG) {"tb2y ry" #RY " wx4 wy2" TAG, RY, 4, 2, k_tb2y<GS_LINEAR, RY, 4, true, NTF, false, SPEC>}
+const PairVariant kPairVariants[] = {GS_PVF(2, 4),
+                                     GS_PVF(2, 8),
+                                     GS_PV(2, 4),
+                                     GS_PVY(2, false, false, " f-cached"),
+                                     GS_PVY(3, false, false, " f-cached"),
+                                     GS_PVY(2, false, true, " f-cached spec"),
+                                     GS_PVY(3, false, true, " f-cached spec"),
+                                     GS_PVY(3, true, false, " f-nt"),
+                                     {"tb2y ry2 wx4 wy2 f-cached spec pfd2", 2, 4, 2,
+                                      k_tb2y<GS_LINEAR, 2, 4, true, false, false, true, 0, 2>}};
+#undef GS_PVY
+#undef GS_PVF
+#undef GS_PV
+constexpr int kNumPairVariants = (int)(sizeof(kPairVariants) / sizeof(kPairVariants[0]));
+
+int gs_debug_num_pair_variants(void) { return kNumPairVariants; }
+const char* gs_debug_pair_variant_name(int variant)
+{
+    return (variant >= 0 && variant < kNumPairVariants) ? kPairVariants[variant].name : "";
+}
+
+int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
+                          double* v_out, const double* f, int zc, hipStream_t st)
+{
+    if (variant < 0 || variant >= kNumPairVariants || !S || bad_level(L) || !canonical_order(S) || !v_in ||
+        !v_out || !f || v_in == v_out || zc < 0)
+        return GS_EINVAL;
+    const PairVariant& V = kPairVariants[variant];
+    const int64_t wx = (L->nx + 2 * WAVE - 1) / (2 * WAVE);
+    if (L->nx < 1 || L->ny < 1 || L->nz < 1 || wx > V.wxmax) return GS_EINVAL;
+    const int64_t tiles = (L->ny + V.ry * V.wy - 1) / (V.ry * V.wy);
+    if (zc == 0) {
+        int64_t c = tiles * L->nz / 1024;
+        zc = (int)(c < 4 ? 4 : (c > 32 ? 32 : c));
+    }
+    const Coef k = make_coef(S, L, omega, 0.0);
+    hipLaunchKernelGGL(V.kern, dim3((unsigned)tiles, (unsigned)((L->nz + zc - 1) / zc)), dim3(WAVE, (unsigned)wx, V.wy), 0,
+                       st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc,
+                       0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0, nullptr);
+    return launch_status();
+}
+
+int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
+                double* sink, hipStream_t st)
+{
+    if (kind == 5) { // k_sleep: n iterations of s_sleep(127), one wave
+        if (n < 0) return GS_EINVAL;
+        hipLaunchKernelGGL(k_sleep, dim3(1), dim3(64), 0, st, n);
+        return launch_status();
+    }
+    if (n < 0 || (n & 1) || kind < 0 || kind > 4 || blocks <= 0) return GS_EINVAL;
+    if (kind == 4) { // copy at RCCL's transport-kernel footprint (k_fatcopy)
+        hipLaunchKernelGGL(k_fatcopy, dim3(blocks), dim3(256), 0, st, out, a, n / 2);
+        return launch_status();
+    }
+    using K = void (*)(double*, const double*, const double*, int64_t, double*);
+    static const K tab[4][2][2] = {
+        {{k_bw<0, 1, false>, k_bw<0, 1, true>}, {k_bw<0, 4, false>, k_bw<0, 4, true>}},
+        {{k_bw<1, 1, false>, k_bw<1, 1, true>}, {k_bw<1, 4, false>, k_bw<1, 4, true>}},
+        {{k_bw<2, 1, false>, k_bw<2, 1, true>}, {k_bw<2, 4, false>, k_bw<2, 4, true>}},
+        {{k_bw<3, 1, false>, k_bw<3, 1, true>}, {k_bw<3, 4, false>, k_bw<3, 4, true>}},
+    };
+    hipLaunchKernelGGL(tab[kind][unroll > 1][nt != 0], dim3(blocks), dim3(256), 0, st, out, a, b, n / 2, sink);
+    return launch_status();
+}
+
+int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, double* ref, hipStream_t st)
+{
+    if (!a || !fast || !ref || n < 0) return GS_EINVAL;
+    if (n == 0) return 0;
+    Coef k{};
+    k.hh = hh;
+    k.fastdiv = hh >= 0x1p-120 && hh <= 1.0;
+    hipLaunchKernelGGL(k_div_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, n, k, fast, ref);
+    return launch_status();
+}
+
+int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t n, hipStream_t st)
+{
+    if (!out || !a || !b || n < 0 || (n & 1)) return GS_EINVAL;
+    hipLaunchKernelGGL(k_triad, dim3(4096), dim3(256), 0, st, out, a, b, n / 2);
+    return launch_status();
+}
+
+} // extern "C"

@@ -164,6 +164,16 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         stencilAbi.oy[i] = stencil.getYOffset(i);
         stencilAbi.oz[i] = stencil.getZOffset(i);
     }
+    {
+        auto on = [](const char* name) { return std::getenv(name) != nullptr; };
+        sw.fusedSweeps = !on("GS_NO_FUSED_SWEEPS");
+        sw.speculation = !on("GS_NO_SPECULATION");
+        sw.fusedProlong = !on("GS_NO_FUSED_PROLONG");
+        sw.fusedRR = !on("GS_NO_FUSED_RR");
+        sw.zeroGuess = !on("GS_NO_ZERO_GUESS");
+        sw.pipeline = !on("GS_NO_PIPELINE");
+        if (const char* e = std::getenv("GS_NEWTON_PRO_POINTS")) sw.newtonProPoints = std::strtoll(e, nullptr, 10);
+    }
     std::vector<int64_t> nzs, pts;
     for (int l = 0; l < nlev; l++) {
         LevelData& L = levels_[l];
@@ -208,12 +218,11 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         L.minPlanes = nz;
         if (L.distributed)
             for (int q = 0; q < nranks(); q++) L.minPlanes = std::min(L.minPlanes, L.ranksHi[q] - L.ranksLo[q] + 1);
-        static const bool noPairs = std::getenv("GS_NO_FUSED_SWEEPS") != nullptr;
         // rank-uniform on a Z-slab level (the smoothing schedule decides the ghost exchanges): judged
         // on the thinnest slab, as the kernel's fill count grows with the plane count
         gs_level thin = L.geom;
         thin.nz = L.minPlanes;
-        L.fusedPairs = !noPairs && gs_jacobi_sweep2_supported_mode(&stencilAbi, &thin, (int)mode) == 2 &&
+        L.fusedPairs = sw.fusedSweeps && gs_jacobi_sweep2_supported_mode(&stencilAbi, &thin, (int)mode) == 2 &&
                        (!L.distributed || L.minPlanes >= 2);
     }
     // The coarse end of the V-cycle runs as one gs_coarse_cycle launch from the first level of at
@@ -524,8 +533,7 @@ void HipSolver::joinComm(HipGridData& grid, bool wait)
 
 bool HipSolver::speculationEnabled(const HipGridData& grid)
 {
-    static const bool off = std::getenv("GS_NO_SPECULATION") != nullptr;
-    return !off && grid.preSmoothing > 0 && grid.numLevels() > 1;
+    return grid.sw.speculation && grid.preSmoothing > 0 && grid.numLevels() > 1;
 }
 
 // src/cpu/CpuSolver.cpp:12-43. Every norm the loop reads (the initial one and each V-cycle's closing
@@ -623,8 +631,7 @@ static bool proSlabOk(HipGridData& grid, std::size_t l)
 static bool proWorthIt(HipGridData& grid, std::size_t l)
 {
     if (grid.mode != GridParams::NEWTON) return true;
-    const char* e = std::getenv("GS_NEWTON_PRO_POINTS"); // read per call: tests switch it
-    const int64_t minPoints = e ? std::strtoll(e, nullptr, 10) : (int64_t)1 << 26;
+    const int64_t minPoints = grid.sw.newtonProPoints;
     const auto& F = grid.getLevel(l);
     return (int64_t)F.levelDim[0] * (int64_t)F.levelDim[1] * F.minPlanes >= minPoints;
 }
@@ -796,8 +803,7 @@ void HipSolver::upLeg(HipGridData& grid, std::size_t i)
     auto& F = grid.getLevel(i - 1);
     grid.clock.mark(s, (int)(i - 1), true);
     materialize(grid, i); // only if the level had no sweep at all
-    static const bool noFusedPro = std::getenv("GS_NO_FUSED_PROLONG") != nullptr;
-    if (!noFusedPro && F.fusedPairs && grid.postSmoothing >= 2 && proWorthIt(grid, i - 1) && proSlabOk(grid, i - 1) &&
+    if (grid.sw.fusedProlong && F.fusedPairs && grid.postSmoothing >= 2 && proWorthIt(grid, i - 1) && proSlabOk(grid, i - 1) &&
         gs_jacobi_sweep2_prolong_supported(&grid.stencilAbi, &F.geom, (int)grid.mode)) {
         // the first two post-smoothing sweeps of v^h + P v^2h in one pass (the corrected
         // iterate is never stored), then the remaining ones. On a Z-slab each rank corrects its
@@ -860,10 +866,9 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
         jacobi(grid, i, pre);
         auto& L = grid.getLevel(i);
         auto& C = grid.getLevel(i + 1);
-        static const bool noFusedRR = std::getenv("GS_NO_FUSED_RR") != nullptr;
         // f^2h = R (f^h - A v^h) in one pass: the fine residual is never stored
         bool fused = false;
-        if (!noFusedRR) {
+        if (grid.sw.fusedRR) {
             materialize(grid, i);
             const double* w = L.newtonV ? L.newtonV.data() : nullptr;
             if (!(L.distributed && grid.nranks() > 1)) {
@@ -908,8 +913,7 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
         }
         if (grid.mode != GridParams::NONLINEAR) {
             // v^2h = 0 (CpuSolver.cpp:114-116): not stored; the first sweep on the level reads no v
-            static const bool noZeroGuess = std::getenv("GS_NO_ZERO_GUESS") != nullptr;
-            if (noZeroGuess) {
+            if (!grid.sw.zeroGuess) {
                 if (grid.trace) grid.rec("zero", {{"L", (long long)(i + 1)}}, "v");
                 C.v.zero(s);
             } else {
@@ -969,8 +973,7 @@ double HipSolver::vcycleSpeculative(HipGridData& grid, int* pending)
 // pending), level 0 is not part of the coarse-cycle launch, and no per-level clock is running.
 bool HipSolver::pipelinable(const HipGridData& grid, int pending)
 {
-    static const bool off = std::getenv("GS_NO_PIPELINE") != nullptr;
-    return !off && !grid.clock.on && speculationEnabled(grid) && pending > 0 &&
+    return grid.sw.pipeline && !grid.clock.on && speculationEnabled(grid) && pending > 0 &&
            (std::size_t)pending == grid.preSmoothing && std::min(grid.coarseFrom, grid.numLevels() - 1) >= 1;
 }
 

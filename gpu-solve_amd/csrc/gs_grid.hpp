@@ -136,6 +136,18 @@ public:
     int rank() const { return comm_ ? comm_->rank() : 0; }
     int nranks() const { return comm_ ? comm_->size() : 1; }
     bool overlapHalo = true; // boundary planes first, halo on the comm stream beside the interior
+    // Alternative-path switches, read from the environment once, when the grid is created (never on a
+    // launch path); the defaults are the measured choices. Tests pin every alternative bit-identical.
+    struct Switches {
+        bool fusedSweeps = true;   // GS_NO_FUSED_SWEEPS: one-sweep kernels only
+        bool speculation = true;   // GS_NO_SPECULATION: the closing norm from a residual pass
+        bool fusedProlong = true;  // GS_NO_FUSED_PROLONG: gs_prolong_add + the plain pair
+        bool fusedRR = true;       // GS_NO_FUSED_RR: residual stored, then restricted
+        bool zeroGuess = true;     // GS_NO_ZERO_GUESS: coarse v = 0 stored instead of flagged
+        bool pipeline = true;      // GS_NO_PIPELINE: no overlap of the norm wait with the next cycle
+        int64_t newtonProPoints = (int64_t)1 << 26; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
+                                                     // prolongation pair from this many points per rank
+    } sw;
     // levels coarseFrom .. numLevels()-1 run as ONE gs_coarse_cycle launch in every V-cycle
     // (numLevels(): none); set from GS_COARSE_POINTS at construction
     std::size_t coarseFrom = 0;

@@ -1,2684 +1,7 @@
-// gs_kernels.hip — CDNA4 (gfx950) HIP kernels of the GMG V-cycle + the extern "C" launchers
-// declared in include/gpusolve_hip.h.
-//
-// Numerics follow the reference CPU backend operator by operator (src/cpu/CpuSolver.cpp,
-// src/cpu/NewtonSolver.cpp, src/cpu/CpuGridData.cpp of Bricktricker/gpu-solve): every expression
-// keeps the reference's evaluation order and the library is built with -ffp-contract=off, so in
-// LINEAR mode every field is bit-identical to the CPU path; only the l2-norm summation order
-// (deterministic here: fixed per-block partials + fixed-order finish) and, in the non-linear
-// modes, ocml's exp vs glibc's exp (<= 1 ulp) differ.
-//
-// Layout: x unit-stride, z slowest (include/gpusolve_hip.h), so Z-slabs are contiguous planes and
-// a wave64 row load along x is one coalesced 1 KiB (dwordx4 per lane) access.
-// Timing-only experiment builds (tools/pro_exp_build.sh + tools/pro_exp.py; never the product): 1 = the fused prolongation
-// pair without the correction arithmetic, 2 = also without the coarse loads, 3 = LINEAR pairs at one
-// plane step of prefetch
-#ifndef GS_PRO_EXP
-#define GS_PRO_EXP 0
-#endif
-#ifndef GS_PRO_HALF
-#define GS_PRO_HALF 1 // fused prolongation: halved X-pass rows formed once per coarse row (0: per fine point)
-#endif
-#include <hip/hip_runtime.h>
-#include <math.h>
-#include <stdint.h>
-#include <stdlib.h>
-
-#include <map>
-#include <mutex>
-#include <utility>
-
-#include "gpusolve_hip.h"
-
-namespace {
-
-constexpr int WAVE = 64;
-
-// compile-time / run-time booleans for code specialised per wave (BoolC) or selected per use (RtBool)
-template <bool B>
-struct BoolC {
-    __device__ static constexpr bool get() { return B; }
-};
-struct RtBool {
-    bool b;
-    __device__ bool get() const { return b; }
-};
-
-// ---------------------------------------------------------------------------------------------
-// Stencil coefficients by value (they land in SGPRs).
-struct Coef {
-    double s[7];
-    double hh;     // h*h
-    double omega;
-    double gamma;
-    double alpha;  // h*h / s0          (CpuSolver.cpp:145)
-    double preFac; // s0 / (h*h)        (CpuSolver.cpp:144)
-    int fastdiv;   // 2^-120 <= hh <= 1: div_hh may take its 3-operation path
-    int unit;      // s[1..6] == -1 and |s[0]| >= 1: the unit-neighbour stencil sum applies (stencil_sum<true>)
-    int64_t off[7]; // generic kernel: linear element offsets of the 7 entries
-};
-
-bool canonical_order(const gs_stencil* S)
-{
-    static const int cx[7] = {0, 1, -1, 0, 0, 0, 0};
-    static const int cy[7] = {0, 0, 0, 1, -1, 0, 0};
-    static const int cz[7] = {0, 0, 0, 0, 0, 1, -1};
-    for (int i = 0; i < 7; i++)
-        if (S->ox[i] != cx[i] || S->oy[i] != cy[i] || S->oz[i] != cz[i]) return false;
-    return true;
-}
-
-bool valid_stencil(const gs_stencil* S)
-{
-    for (int i = 0; i < 7; i++)
-        if (S->ox[i] < -1 || S->ox[i] > 1 || S->oy[i] < -1 || S->oy[i] > 1 || S->oz[i] < -1 || S->oz[i] > 1)
-            return false;
-    return true;
-}
-
-Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamma)
-{
-    Coef k;
-    for (int i = 0; i < 7; i++) {
-        k.s[i] = S->s[i];
-        k.off[i] = S->ox[i] + S->oy[i] * L->ldy + S->oz[i] * L->ldz;
-    }
-    k.hh = L->h * L->h;
-    k.omega = omega;
-    k.gamma = gamma;
-    k.alpha = k.hh / S->s[0];
-    k.preFac = S->s[0] / k.hh;
-    k.fastdiv = k.hh >= 0x1p-120 && k.hh <= 1.0;
-    static const bool noUnit = getenv("GS_NO_UNIT_STENCIL") != nullptr;
-    k.unit = !noUnit && (S->s[0] >= 1.0 || S->s[0] <= -1.0);
-    for (int i = 1; i < 7; i++) k.unit = k.unit && S->s[i] == -1.0;
-    return k;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Point formulas (reference evaluation order; built with -ffp-contract=off).
-
-// s / hh, bit-identical to the compiler's IEEE division, in 3 FP64 operations instead of ~11.
-// The gfx950 division sequence is: D = div_scale(hh), y = rcp(D) refined by two Newton steps,
-// N = div_scale(s), q = N*y, r = fma(-D, q, N), q' = div_fmas(r, y, q), div_fixup(q', hh, s). When
-// neither operand is scaled (s and hh normal, s != 0, exponent(s) - exponent(hh) < 768, the quotient
-// normal and exponent(s) > 53) div_scale returns its operand, div_fmas is a plain fma and div_fixup
-// returns q' — and y depends on hh alone, so it is loop-invariant. The fast path is taken for
-// 2^-899 <= |s| < 2^601 with the host guaranteeing 2^-120 <= hh <= 1 (Coef::fastdiv); anything
-// else (zero, denormals, inf/nan, extreme magnitudes) takes the ordinary division.
-__device__ __forceinline__ double hh_recip(double hh)
-{
-    const double y0 = __builtin_amdgcn_rcp(hh);
-    const double y1 = __builtin_fma(y0, __builtin_fma(-hh, y0, 1.0), y0);
-    return __builtin_fma(y1, __builtin_fma(-hh, y1, 1.0), y1);
-}
-
-__device__ __forceinline__ double div_hh(const Coef& k, double s)
-{
-    const unsigned e = ((unsigned)__double2hiint(s) >> 20) & 0x7ffu; // biased exponent
-    if (k.fastdiv && e - 124u < 1500u) {                              // 124 <= e <= 1623
-        const double y = hh_recip(k.hh);
-        const double q = s * y;
-        const double r = __builtin_fma(-k.hh, q, s);
-        return __builtin_fma(r, y, q);
-    }
-    return s / k.hh;
-}
-
-// The same division for N values at once: the operand-range test of every value is combined first
-// and ONE branch picks the 3-operation path for all N (or the IEEE division for all N when any value
-// is outside the range), so a sweep over several rows has one exec branch instead of one per point
-// and the scheduler can interleave the rows' arithmetic.
-__device__ __forceinline__ bool div_hh_fast_ok(double s)
-{
-    const unsigned e = ((unsigned)__double2hiint(s) >> 20) & 0x7ffu;
-    return e - 124u < 1500u;
-}
-template <int N>
-__device__ __forceinline__ void div_hh_n(const Coef& k, double (&s)[N])
-{
-    bool ok = k.fastdiv;
-#pragma unroll
-    for (int i = 0; i < N; i++) ok &= div_hh_fast_ok(s[i]);
-    if (ok) {
-        const double y = hh_recip(k.hh);
-#pragma unroll
-        for (int i = 0; i < N; i++) {
-            const double q = s[i] * y;
-            const double r = __builtin_fma(-k.hh, q, s[i]);
-            s[i] = __builtin_fma(r, y, q);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < N; i++) s[i] = s[i] / k.hh;
-    }
-}
-
-// one row's two points: batched, except in NEWTON mode whose kernels run at the VGPR limit (the batch
-// keeps both sums live across the branch)
-template <int MODE>
-__device__ __forceinline__ void div_hh_row(const Coef& k, double (&q)[2])
-{
-    if (MODE == GS_NEWTON) {
-        q[0] = div_hh(k, q[0]);
-        q[1] = div_hh(k, q[1]);
-    } else {
-        div_hh_n(k, q);
-    }
-}
-
-// stencil sum in config order (before the division by h^2) — CpuSolver.cpp:56-62.
-// UN (Coef::unit: the six neighbour weights are exactly -1, |s0| >= 1 — every reference config): the
-// same value in 7 instead of 14 operations, bit for bit. s += (-1) * x is s - x exactly (the product
-// by -1 is a sign flip, and IEEE subtraction is the addition of the negation), and the first term
-// 0.0 + s0 * c equals fma(s0, c, 0.0): both round the product once and add an exact zero, and with
-// |s0| >= 1 a non-zero product never underflows to a signed zero (the one case where they differ).
-template <bool UN = false>
-__device__ __forceinline__ double stencil_sum(const Coef& k, double c, double xp, double xm, double yp, double ym,
-                                              double zp, double zm)
-{
-    if constexpr (UN) {
-        double s = __builtin_fma(k.s[0], c, 0.0);
-        s = s - xp;
-        s = s - xm;
-        s = s - yp;
-        s = s - ym;
-        s = s - zp;
-        s = s - zm;
-        return s;
-    }
-    double s = 0.0;
-    s += k.s[0] * c;
-    s += k.s[1] * xp;
-    s += k.s[2] * xm;
-    s += k.s[3] * yp;
-    s += k.s[4] * ym;
-    s += k.s[5] * zp;
-    s += k.s[6] * zm;
-    return s;
-}
-
-// the non-linear term added after the division — CpuSolver.cpp:63-76
-template <int MODE>
-__device__ __forceinline__ double op_finish(const Coef& k, double q, double c, double w)
-{
-    if (MODE == GS_NEWTON) {
-        const double ew = exp(w);
-        q += k.gamma * (1 + w) * c * ew;
-    } else if (MODE == GS_NONLINEAR) {
-        const double ev = exp(c);
-        const double nl = k.gamma * c * ev;
-        q += nl;
-    }
-    return q;
-}
-
-// stencil sum in config order, then /h^2 and the non-linear term  — CpuSolver.cpp:56-76
-template <int MODE, bool UN = false>
-__device__ __forceinline__ double op_value(const Coef& k, double c, double xp, double xm, double yp, double ym,
-                                           double zp, double zm, double w)
-{
-    double s = stencil_sum<UN>(k, c, xp, xm, yp, ym, zp, zm);
-    s = div_hh(k, s);
-    if (MODE == GS_NEWTON) {
-        const double ew = exp(w);
-        s += k.gamma * (1 + w) * c * ew;
-    } else if (MODE == GS_NONLINEAR) {
-        const double ev = exp(c);
-        const double nl = k.gamma * c * ev;
-        s += nl;
-    }
-    return s;
-}
-
-// Jacobi point update from the old value and its residual — CpuSolver.cpp:157-171
-template <int MODE>
-__device__ __forceinline__ double jacobi_update(const Coef& k, double v, double r, double w)
-{
-    if (MODE == GS_LINEAR) return v + k.omega * (k.alpha * r);
-    const double u = (MODE == GS_NONLINEAR) ? v : w;
-    const double eu = exp(u);
-    const double den = k.preFac + k.gamma * (1 + u) * eu;
-    return v + k.omega * (r / den);
-}
-
-// NEWTON's linearisation terms of a point, A = gamma (1 + w) and E = exp(w), computed ONCE per point
-// and pass and shared by the operator and the update of both sweeps of a fused pair: bit-identical to
-// op_finish / jacobi_update, whose reference expressions evaluate gamma * (1 + w) first and multiply
-// by exp(w) last (CpuSolver.cpp:63-66, :157-171).
-__device__ __forceinline__ double newton_op(double q, double c, double A, double E) { return q + A * c * E; }
-__device__ __forceinline__ double newton_update(const Coef& k, double v, double r, double A, double E)
-{
-    const double den = k.preFac + A * E;
-    return v + k.omega * (r / den);
-}
-
-__device__ __forceinline__ double wave_sum(double x)
-{
-#pragma unroll
-    for (int o = WAVE / 2; o > 0; o >>= 1) x += __shfl_down(x, o, WAVE);
-    return x;
-}
-
-// Block-wide fixed-order sum of nw <= NWAVES waves (default: all); result valid in thread 0.
-template <int NWAVES>
-__device__ __forceinline__ double block_sum(double x, double* lds, int nw = NWAVES)
-{
-    const int tid = threadIdx.x + threadIdx.y * blockDim.x;
-    x = wave_sum(x);
-    if ((tid & (WAVE - 1)) == 0) lds[tid / WAVE] = x;
-    __syncthreads();
-    double t = 0.0;
-    if (tid == 0) {
-#pragma unroll
-        for (int i = 0; i < NWAVES; i++)
-            if (i < nw) t += lds[i];
-    }
-    return t;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Stencil passes come in three kinds:
-//   KIND 0: Jacobi sweep         out = v_new (partials: sum r^2 of the input's residual, nullable)
-//   KIND 1: residual             out = r (nullable), partials = per-block sum r^2 (nullable)
-//   KIND 2: FAS coarse operator  out = A(u) (ADD=false) or out += A(u) (ADD=true)
-// ---------------------------------------------------------------------------------------------
-// Register-blocked z-march ("rb"): each lane owns 2 consecutive x-points (one dwordx4) of RY
-// consecutive y-rows, a wave owns a 128 x RY tile, W waves stack in y, the block walks ZC planes.
-//  - y-neighbours come from the lane's own registers (plus 2 halo rows per wave and plane),
-//  - x-neighbours from the adjacent lane by a DPP wave shift (wave_shr:1 / wave_shl:1); the two
-//    tile-edge values per row are wave-uniform scalar loads,
-//  - z-neighbours are the previous / next plane held in registers,
-//  - every load of plane z+1 (next-next v rows, halo rows, f, edges) is issued before plane z is
-//    computed, so a full plane of HBM traffic is in flight behind the arithmetic.
-// Loads use a clamped column min(x, nx+1); a pair load there reads one element past the padded
-// row, which the allocation recipe of gs_field_layout (+32 elements) keeps in bounds.
-template <bool DPP>
-__device__ __forceinline__ double lane_from_left(double src, double edge)
-{
-    // lane i <- src of lane i-1; lane 0 <- edge
-    if (DPP) {
-        const long long s = __double_as_longlong(src), e = __double_as_longlong(edge);
-        const int lo = __builtin_amdgcn_update_dpp((int)e, (int)s, 0x138, 0xf, 0xf, false);
-        const int hi = __builtin_amdgcn_update_dpp((int)(e >> 32), (int)(s >> 32), 0x138, 0xf, 0xf, false);
-        return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-    } else {
-        const double t = __shfl_up(src, 1, WAVE);
-        return (threadIdx.x & (WAVE - 1)) == 0 ? edge : t;
-    }
-}
-
-template <bool DPP>
-__device__ __forceinline__ double lane_from_right(double src, double edge)
-{
-    // lane i <- src of lane i+1; lane 63 <- edge
-    if (DPP) {
-        const long long s = __double_as_longlong(src), e = __double_as_longlong(edge);
-        const int lo = __builtin_amdgcn_update_dpp((int)e, (int)s, 0x130, 0xf, 0xf, false);
-        const int hi = __builtin_amdgcn_update_dpp((int)(e >> 32), (int)(s >> 32), 0x130, 0xf, 0xf, false);
-        return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-    } else {
-        const double t = __shfl_down(src, 1, WAVE);
-        return (threadIdx.x & (WAVE - 1)) == WAVE - 1 ? edge : t;
-    }
-}
-
-// a value every lane holds identically (an LDS broadcast read), moved to SGPRs
-__device__ __forceinline__ double uniform_d(double x)
-{
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-
-__device__ __forceinline__ double2 ld2(const double* __restrict__ p) { return *reinterpret_cast<const double2*>(p); }
-
-typedef double dv2 __attribute__((ext_vector_type(2)));
-// streamed-once operands (f, the output) optionally bypass the caches' retention (nt)
-template <bool NT>
-__device__ __forceinline__ double2 ld2s(const double* __restrict__ p)
-{
-    if (NT) {
-        const dv2 t = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(p));
-        return make_double2(t.x, t.y);
-    }
-    return ld2(p);
-}
-template <bool NT>
-__device__ __forceinline__ void st2s(double* __restrict__ p, double a, double b)
-{
-    if (NT) {
-        const dv2 t = {a, b};
-        __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p));
-    } else {
-        *reinterpret_cast<double2*>(p) = make_double2(a, b);
-    }
-}
-
-// Loads of the iterate; ZV: the iterate is identically zero (a coarse level's first sweep after
-// the reference's v = 0) and is not read at all. Multiplying the literal zeros keeps the arithmetic,
-// and so every bit of the result, that of loaded zeros (no fast-math folding).
-template <bool ZV, bool NT = false>
-__device__ __forceinline__ double2 ldv2(const double* __restrict__ p)
-{
-    if (ZV) return make_double2(0.0, 0.0);
-    return ld2s<NT>(p);
-}
-template <bool ZV>
-__device__ __forceinline__ double ldv1(const double* __restrict__ p)
-{
-    return ZV ? 0.0 : *p;
-}
-
-// Bijective XCD-aware tile order (cdna_hip_programming.md T1): hardware block b runs on XCD b % 8;
-// give each XCD a contiguous run of tiles so y-neighbour tiles share an L2 while they run.
-__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb)
-{
-    const int64_t q = nb / 8, r = nb % 8, x = b % 8, k = b / 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-}
-
-template <int MODE, int KIND, bool ADD, int RY, int W, bool DPP, bool NT = false, bool XCD = false, bool NTV = false,
-          bool ZV = false, bool UN = false>
-__global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict__ v, const double* __restrict__ f,
-                                                 const double* __restrict__ w, double* __restrict__ out,
-                                                 double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
-                                                 int64_t ldz, int ZC)
-{
-    __shared__ double red[W];
-    const int lane = threadIdx.x;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.y);
-    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    int64_t tile = blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z);
-    if (XCD) {
-        const int nbx = (nx + 2 * WAVE - 1) / (2 * WAVE), nby = (ny + RY * W - 1) / (RY * W);
-        tile = xcd_tile(blockIdx.x, gridDim.x);
-        bx = (int)(tile % nbx);
-        by = (int)((tile / nbx) % nby);
-        bz = (int)(tile / ((int64_t)nbx * nby));
-    }
-    const int x0 = 1 + bx * (2 * WAVE);
-    const int x = x0 + 2 * lane;
-    const int xl = min(x, nx + 1);
-    const int y0 = 1 + (by * W + wv) * RY;
-    const int zb = 1 + bz * ZC;
-    const int ze = min(zb + ZC - 1, nz);
-    const int xle = x0 - 1;
-    const int xre = min(x0 + 2 * WAVE, nx + 1);
-    const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
-    const double* fin = (KIND == 2) ? out : f;
-
-    int64_t roff[RY + 2]; // rows y0-1 .. y0+RY (clamped into the padded range)
-#pragma unroll
-    for (int r = 0; r < RY + 2; r++) roff[r] = (int64_t)min(y0 - 1 + r, ny + 1) * ldy;
-
-    // Planes z-1 (P) and z (C) of the wave's rows live in registers. Everything of plane z+1 (its
-    // halo rows, f, w, tile edges) and the v rows of plane z+2 is loaded into slot ph of a two-slot
-    // ring while plane z is computed from the other slot, and only moved out after it was consumed:
-    // a load's destination is never copied before its first use, so its wait lands one full plane
-    // of arithmetic after the issue (the loop is unrolled by two to make the slot index static).
-    double2 P[RY], C[RY], NL[2][RY], FL[2][RY], WL[2][RY], HL[2][2];
-    double EL[2][RY], ER[2][RY];
-    double sumsq = 0.0;
-    // slot s <- plane z1's halo rows, f, w, edges and plane z2's v rows (plane offsets)
-    auto load_slot = [&](const int s, const int64_t z1, const int64_t z2) {
-#pragma unroll
-        for (int r = 0; r < RY; r++) {
-            NL[s][r] = ldv2<ZV, NTV>(v + xl + roff[r + 1] + z2);
-            if (KIND != 2 || ADD) FL[s][r] = ld2s<NT>(fin + xl + roff[r + 1] + z1);
-            if (MODE == GS_NEWTON) WL[s][r] = ld2(w + xl + roff[r + 1] + z1);
-            EL[s][r] = ldv1<ZV>(v + xle + roff[r + 1] + z1);
-            ER[s][r] = ldv1<ZV>(v + xre + roff[r + 1] + z1);
-        }
-        HL[s][0] = ldv2<ZV>(v + xl + roff[0] + z1);
-        HL[s][1] = ldv2<ZV>(v + xl + roff[RY + 1] + z1);
-    };
-    if (zb <= ze) {
-        const int64_t zo = (int64_t)zb * ldz;
-#pragma unroll
-        for (int r = 0; r < RY; r++) {
-            P[r] = ldv2<ZV>(v + xl + roff[r + 1] + zo - ldz);
-            C[r] = ldv2<ZV>(v + xl + roff[r + 1] + zo);
-        }
-        load_slot(1, zo, zo + ldz);
-    }
-    // Both halves always run (an odd chunk ends with one step whose results are discarded), and
-    // the loads of every step are unconditional (plane indices clamped into the padded range), so
-    // the slots keep fixed registers around the loop.
-    for (int z0 = zb; z0 <= ze; z0 += 2) {
-#pragma unroll
-        for (int ph = 0; ph < 2; ph++) {
-            const int z = z0 + ph;
-            const bool real = z <= ze;
-            const int cs = ph ^ 1; // slot holding plane z
-            const int64_t zo = (int64_t)z * ldz;
-            load_slot(ph, (int64_t)min(z + 1, nz + 1) * ldz, (int64_t)min(z + 2, nz + 1) * ldz);
-#pragma unroll
-            for (int r = 0; r < RY; r++) {
-                const double2 c = C[r], ym = r == 0 ? HL[cs][0] : C[r - 1], yp = r == RY - 1 ? HL[cs][1] : C[r + 1];
-                const double2 zm = P[r], zp = NL[cs][r];
-                const double xm0 = lane_from_left<DPP>(c.y, EL[cs][r]);
-                const double xp1 = lane_from_right<DPP>(c.x, ER[cs][r]);
-                const double wx = (MODE == GS_NEWTON) ? WL[cs][r].x : 0.0;
-                const double wy = (MODE == GS_NEWTON) ? WL[cs][r].y : 0.0;
-                // NEWTON sweep: exp(w) once per point, shared by the operator and the update
-                constexpr bool NS = MODE == GS_NEWTON && KIND == 0;
-                const double Ax = NS ? k.gamma * (1 + wx) : 0.0, Ay = NS ? k.gamma * (1 + wy) : 0.0;
-                const double Ex = NS ? exp(wx) : 0.0, Ey = NS ? exp(wy) : 0.0;
-                const double a0 = NS ? newton_op(div_hh(k, stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x)), c.x, Ax, Ex)
-                                     : op_value<MODE, UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
-                const double a1 = NS ? newton_op(div_hh(k, stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)), c.y, Ay, Ey)
-                                     : op_value<MODE, UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wy);
-                double r0 = 0.0, r1 = 0.0; // residual of the input iterate
-                if (KIND != 2 || ADD) {
-                    r0 = FL[cs][r].x - a0;
-                    r1 = FL[cs][r].y - a1;
-                }
-                double o0, o1;
-                if (NS) {
-                    o0 = newton_update(k, c.x, r0, Ax, Ex);
-                    o1 = newton_update(k, c.y, r1, Ay, Ey);
-                } else if (KIND == 0) {
-                    o0 = jacobi_update<MODE>(k, c.x, r0, wx);
-                    o1 = jacobi_update<MODE>(k, c.y, r1, wy);
-                } else if (KIND == 1) {
-                    o0 = r0;
-                    o1 = r1;
-                } else {
-                    o0 = ADD ? FL[cs][r].x + a0 : a0;
-                    o1 = ADD ? FL[cs][r].y + a1 : a1;
-                }
-                const bool rowok = real && y0 + r <= ny;
-                if (KIND != 2 && partials) {
-                    if (rowok && okx0) sumsq += r0 * r0;
-                    if (rowok && okx1) sumsq += r1 * r1;
-                }
-                if (rowok && (KIND != 1 || out)) {
-                    double* q = out + x + roff[r + 1] + zo;
-                    if (okx1) st2s<NT>(q, o0, o1);
-                    else if (okx0) *q = o0;
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < RY; r++) {
-                P[r] = C[r];
-                C[r] = NL[cs][r];
-            }
-        }
-    }
-    if (KIND != 2 && partials) {
-        const double t = block_sum<W>(sumsq, red);
-        if (threadIdx.x == 0 && threadIdx.y == 0) partials[tile] = t;
-    }
-}
-
-dim3 rb_grid(const gs_level* L, int RY, int W, int ZC, bool oneD = false)
-{
-    const dim3 g((unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), (unsigned)((L->ny + RY * W - 1) / (RY * W)),
-                 (unsigned)((L->nz + ZC - 1) / ZC));
-    return oneD ? dim3(g.x * g.y * g.z) : g;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Generic-stencil pass (any 7 offsets in {-1,0,1}^3, any order): one point per thread.
-constexpr int GN_BX = 64, GN_BY = 4;
-
-template <int MODE, int KIND, bool ADD>
-__global__ __launch_bounds__(256) void k_generic(Coef k, const double* __restrict__ v, const double* __restrict__ f,
-                                                 const double* __restrict__ w, double* __restrict__ out,
-                                                 double* __restrict__ partials, int nx, int ny, int nz, int64_t ldy,
-                                                 int64_t ldz)
-{
-    __shared__ double red[GN_BY];
-    const int x = 1 + blockIdx.x * GN_BX + threadIdx.x;
-    const int y = 1 + blockIdx.y * GN_BY + threadIdx.y;
-    const int z = 1 + blockIdx.z;
-    double sumsq = 0.0;
-    if (x <= nx && y <= ny) {
-        const int64_t p = x + y * ldy + (int64_t)z * ldz;
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < 7; i++) s += k.s[i] * (v ? v[p + k.off[i]] : 0.0);
-        s = div_hh(k, s);
-        const double c = v ? v[p] : 0.0;
-        const double wv = (MODE == GS_NEWTON) ? w[p] : 0.0;
-        if (MODE == GS_NEWTON) {
-            const double ew = exp(wv);
-            s += k.gamma * (1 + wv) * c * ew;
-        } else if (MODE == GS_NONLINEAR) {
-            const double ev = exp(c);
-            const double nl = k.gamma * c * ev;
-            s += nl;
-        }
-        if (KIND == 0) {
-            const double r = f[p] - s;
-            sumsq = r * r;
-            out[p] = jacobi_update<MODE>(k, c, r, wv);
-        } else if (KIND == 1) {
-            const double r = f[p] - s;
-            sumsq = r * r;
-            if (out) out[p] = r;
-        } else {
-            out[p] = ADD ? out[p] + s : s;
-        }
-    }
-    if (KIND != 2 && partials) {
-        const double t = block_sum<GN_BY>(sumsq, red);
-        if (threadIdx.x == 0 && threadIdx.y == 0)
-            partials[blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z)] = t;
-    }
-}
-
-dim3 gn_grid(const gs_level* L)
-{
-    return dim3((unsigned)((L->nx + GN_BX - 1) / GN_BX), (unsigned)((L->ny + GN_BY - 1) / GN_BY), (unsigned)L->nz);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Deterministic finish of the per-block partial sums: one block, fixed strided order.
-constexpr int FIN_T = 1024;
-__global__ __launch_bounds__(FIN_T) void k_sumsq_finish(const double* __restrict__ partials, int64_t n,
-                                                        double* __restrict__ out, int accumulate)
-{
-    __shared__ double red[FIN_T / WAVE];
-    double s = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += FIN_T) s += partials[i];
-    const double t = block_sum<FIN_T / WAVE>(s, red);
-    if (threadIdx.x == 0) *out = accumulate ? t : sqrt(t);
-}
-
-// ---------------------------------------------------------------------------------------------
-// 27-point full weighting (CpuSolver.cpp:211-238): coarse interior point per thread, terms summed
-// with ii outermost, kk innermost. The weights are exact powers of two.
-// Z-slabs: coarse local plane z is global z + cz0, its centre fine plane global 2(z + cz0), local
-// 2(z + cz0) - fz0 (both z0 = 0 on an unpartitioned level).
-__global__ __launch_bounds__(256) void k_restrict(const double* __restrict__ fine, double* __restrict__ ca,
-                                                  double* __restrict__ cb, int cnx, int cny, int cnz, int64_t fldy,
-                                                  int64_t fldz, int64_t cldy, int64_t cldz, int zoff)
-{
-    const int x = 1 + blockIdx.x * 64 + threadIdx.x;
-    const int y = 1 + blockIdx.y * 4 + threadIdx.y;
-    const int z = 1 + blockIdx.z;
-    if (x > cnx || y > cny) return;
-    const double* c0 = fine + 2 * x + (int64_t)(2 * y) * fldy + (int64_t)(2 * z + zoff) * fldz;
-    double acc = 0.0;
-#pragma unroll
-    for (int a = -1; a <= 1; a++)
-#pragma unroll
-        for (int b = -1; b <= 1; b++)
-#pragma unroll
-            for (int c = -1; c <= 1; c++) {
-                const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) * ((2.0 - (b < 0 ? -b : b)) / 2.0) *
-                                   ((2.0 - (c < 0 ? -c : c)) / 2.0);
-                acc += wgt * c0[a + b * fldy + c * fldz];
-            }
-    const int64_t q = x + y * cldy + (int64_t)z * cldz;
-    ca[q] = acc;
-    if (cb) cb[q] = acc;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Residual fused into the full-weighting restriction: coarse f = R(f - A v) without writing the fine
-// residual to memory (CpuSolver.cpp:45-83 then :211-238; the reference stores r and re-reads it).
-// A block owns RR_TXC x RR_TYC coarse columns and marches a chunk of coarse planes. The fine region
-// its 27-point stencils touch is (2 RR_TXC + 1) x (2 RR_TYC + 1) points per plane; the v tile with its
-// one-point halo is staged in a 4-plane LDS ring (loaded once, coalesced along x), the residual of
-// that region in a 3-plane LDS ring. Per coarse plane Z: the two new v planes and the f values of the
-// next plane pair are loaded into registers while the current ones are computed (software pipeline),
-// r is evaluated on fine planes 2Z and 2Z+1 (2Z-1 is kept from the previous plane), then every
-// thread sums its coarse point's 27 terms in the reference's order. Fine points outside the interior
-// hold r = 0, as the reference's never-written boundary does. Each residual is the gs_residual
-// expression and each sum the gs_restrict one: bit-identical to the unfused pair.
-constexpr int RR_TXC = 64, RR_TYC = 4, RR_T = RR_TXC * RR_TYC;
-constexpr int RR_FX = 2 * RR_TXC + 1, RR_FY = 2 * RR_TYC + 1; // residual region per plane
-constexpr int RR_VX = RR_FX + 2, RR_VY = RR_FY + 2;           // v tile per plane (one-point halo)
-constexpr int RR_NR = (RR_FX * RR_FY + RR_T - 1) / RR_T;      // residual points per thread and plane
-constexpr int RR_NV = (RR_VX * RR_VY + RR_T - 1) / RR_T;      // v tile points per thread and plane
-
-struct StencilOffsets {
-    int lds[7]; // ox + oy * RR_VX (in-plane LDS offset)
-    int oz[7];
-};
-
-template <int MODE>
-__global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so, const double* __restrict__ v,
-                                                      const double* __restrict__ f, const double* __restrict__ w,
-                                                      double* __restrict__ ca, double* __restrict__ cb, int fnx,
-                                                      int fny, int fnz, int64_t fldy, int64_t fldz, int cnx, int cny,
-                                                      int cnz, int64_t cldy, int64_t cldz, int zoff, int ZC)
-{
-    // one LDS array addressed with integer offsets (pointers into it would become flat accesses):
-    // v ring slots 0..3 at s * RR_VP, residual ring slots 0..2 at 4 RR_VP + s * RR_RP
-    constexpr int RR_VP = RR_VY * RR_VX, RR_RP = RR_FY * RR_FX;
-    __shared__ double lds[4 * RR_VP + 3 * RR_RP];
-    const int tid = threadIdx.x;
-    // (an XCD-aware tile order, as k_tb2y uses, measured 3% slower here: tools/ab_session.sh)
-    const int X0 = 1 + blockIdx.x * RR_TXC, Y0 = 1 + blockIdx.y * RR_TYC;
-    const int Zb = 1 + blockIdx.z * ZC, Ze = min(Zb + ZC - 1, cnz);
-    if (Zb > Ze) return;
-    const int fx0 = 2 * X0 - 1, fy0 = 2 * Y0 - 1; // residual region origin (fine)
-
-    // this thread's v-tile points (clamped into the padded level: clamped copies are never used)
-    int64_t voff[RR_NV];
-#pragma unroll
-    for (int i = 0; i < RR_NV; i++) {
-        const int e = min(tid + i * RR_T, RR_VX * RR_VY - 1);
-        const int ly = e / RR_VX, lx = e - ly * RR_VX;
-        voff[i] = min(fx0 - 1 + lx, fnx + 1) + (int64_t)min(fy0 - 1 + ly, fny + 1) * fldy;
-    }
-    // this thread's residual points: global offset, LDS position, interior flag
-    int64_t roff[RR_NR];
-    int rpos[RR_NR];
-    bool rin[RR_NR];
-#pragma unroll
-    for (int i = 0; i < RR_NR; i++) {
-        const int e = tid + i * RR_T;
-        const int ry = min(e, RR_FX * RR_FY - 1) / RR_FX, rx = min(e, RR_FX * RR_FY - 1) - ry * RR_FX;
-        const int x = fx0 + rx, y = fy0 + ry;
-        rin[i] = e < RR_FX * RR_FY && x <= fnx && y <= fny;
-        roff[i] = min(x, fnx + 1) + (int64_t)min(y, fny + 1) * fldy;
-        rpos[i] = (ry + 1) * RR_VX + rx + 1;
-    }
-    auto zc = [&](int fz) { return (int64_t)min(max(fz, -1), fnz + 2) * fldz; };
-    auto load_v = [&](double (&dst)[RR_NV], int fz) {
-        const int64_t zo = zc(fz);
-#pragma unroll
-        for (int i = 0; i < RR_NV; i++) dst[i] = v[voff[i] + zo];
-    };
-    auto store_v = [&](const double (&src)[RR_NV], int fz) {
-        const int d = ((fz + 4) & 3) * RR_VP;
-#pragma unroll
-        for (int i = 0; i < RR_NV; i++)
-            if (tid + i * RR_T < RR_VP) lds[d + tid + i * RR_T] = src[i];
-    };
-    auto load_fw = [&](double (&F)[RR_NR], double (&W)[RR_NR], int fz) {
-        const int64_t zo = zc(fz);
-#pragma unroll
-        for (int i = 0; i < RR_NR; i++) {
-            F[i] = f[roff[i] + zo];
-            if (MODE == GS_NEWTON) W[i] = w[roff[i] + zo];
-        }
-    };
-    // r on fine plane fz from the v ring (needs planes fz-1 .. fz+1 staged)
-    auto residual_plane = [&](const double (&F)[RR_NR], const double (&W)[RR_NR], int fz) {
-        int toff[7]; // LDS offset of each stencil term relative to the point's in-plane position
-#pragma unroll
-        for (int t = 0; t < 7; t++) toff[t] = ((fz + 4 + so.oz[t]) & 3) * RR_VP + so.lds[t];
-        const int coff = ((fz + 4) & 3) * RR_VP;
-        const int dst = 4 * RR_VP + ((fz + 3) % 3) * RR_RP;
-        const bool zin = fz >= 1 && fz <= fnz;
-#pragma unroll
-        for (int i = 0; i < RR_NR; i++) {
-            if (tid + i * RR_T >= RR_FX * RR_FY) continue;
-            double r = 0.0;
-            if (zin && rin[i]) {
-                double sum = 0.0;
-#pragma unroll
-                for (int t = 0; t < 7; t++) sum += k.s[t] * lds[rpos[i] + toff[t]];
-                const double c = lds[rpos[i] + coff];
-                const double q = op_finish<MODE>(k, div_hh(k, sum), c, MODE == GS_NEWTON ? W[i] : 0.0);
-                r = F[i] - q;
-            }
-            lds[dst + tid + i * RR_T] = r;
-        }
-    };
-
-    double VA[RR_NV], VB[RR_NV], FA[RR_NR], FB[RR_NR], WA[RR_NR], WB[RR_NR];
-    // prologue: v planes P-2 .. P (P = 2 Zb + zoff) into the ring, r(P-1)
-    const int P0 = 2 * Zb + zoff;
-    load_v(VA, P0 - 2);
-    load_v(VB, P0 - 1);
-    load_fw(FA, WA, P0 - 1);
-    store_v(VA, P0 - 2);
-    store_v(VB, P0 - 1);
-    load_v(VA, P0);
-    store_v(VA, P0);
-    __syncthreads();
-    residual_plane(FA, WA, P0 - 1);
-    // staged for the first step: v(P+1), v(P+2), f(P), f(P+1)
-    load_v(VA, P0 + 1);
-    load_v(VB, P0 + 2);
-    load_fw(FA, WA, P0);
-    load_fw(FB, WB, P0 + 1);
-    __syncthreads(); // v(P+2) goes to the slot of v(P-2), which r(P-1) just read
-    const int cx = tid % RR_TXC, cy = tid / RR_TXC;
-    const int X = X0 + cx, Y = Y0 + cy;
-    for (int Z = Zb; Z <= Ze; Z++) {
-        const int P = 2 * Z + zoff;
-        store_v(VA, P + 1);
-        store_v(VB, P + 2);
-        __syncthreads();
-        double F0[RR_NR], F1[RR_NR], W0[RR_NR], W1[RR_NR];
-#pragma unroll
-        for (int i = 0; i < RR_NR; i++) {
-            F0[i] = FA[i];
-            F1[i] = FB[i];
-            W0[i] = WA[i];
-            W1[i] = WB[i];
-        }
-        if (Z < Ze) { // the next step's operands, in flight during this step's arithmetic
-            load_v(VA, P + 3);
-            load_v(VB, P + 4);
-            load_fw(FA, WA, P + 2);
-            load_fw(FB, WB, P + 3);
-        }
-        residual_plane(F0, W0, P);
-        residual_plane(F1, W1, P + 1);
-        __syncthreads();
-        if (X <= cnx && Y <= cny) {
-            double acc = 0.0;
-#pragma unroll
-            for (int a = -1; a <= 1; a++)
-#pragma unroll
-                for (int b = -1; b <= 1; b++)
-#pragma unroll
-                    for (int c = -1; c <= 1; c++) {
-                        const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) * ((2.0 - (b < 0 ? -b : b)) / 2.0) *
-                                           ((2.0 - (c < 0 ? -c : c)) / 2.0);
-                        acc += wgt * lds[4 * RR_VP + ((P + c + 3) % 3) * RR_RP + (2 * cy + 1 + b) * RR_FX + 2 * cx + 1 + a];
-                    }
-            const int64_t q = X + Y * cldy + (int64_t)Z * cldz;
-            ca[q] = acc;
-            if (cb) cb[q] = acc;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Residual + full weighting in registers ("rr2": canonical stencil order, all three modes, levels
-// or Z-slabs (zhi) of rows <= 1024 points). A block is the whole row of coarse columns of ONE
-// coarse row Y (WX waves of 64 lanes; lane = coarse column X, its fine pair x = 2X-1, 2X one dwordx4)
-// and marches a chunk of coarse planes. Per coarse plane Z it evaluates the residual on fine planes 2Z
-// and 2Z+1 (2Z-1 is kept from the previous plane) for the three fine rows 2Y-1 .. 2Y+1 the 27-point sum
-// reads (row 2Y+1 is also the next row's first: recomputed there, its loads hit L2) the way k_rb's
-// residual pass does: x-neighbours by DPP lane shifts with the wave-edge columns exchanged through LDS
-// (zero beyond the level's x-boundaries, which hold v = 0), y-neighbours from the lane's own rows plus
-// two halo rows, z-neighbours from the register window. r at the next coarse column's first fine
-// column (2X+1) is one more DPP shift (the right wave's lane 0 through LDS). The 27 terms are summed in
-// the reference's order (CpuSolver.cpp:225-231): 16 B of compulsory HBM reads per fine point (v, f)
-// plus 1 B of coarse writes, the residual never stored, and no LDS staging of the operands (the
-// LDS-tiled k_resrestrict, kept for the other cases, is latency-bound at 2 blocks per CU). PF = true
-// keeps the next coarse plane's loads in flight (two-slot ring, as in k_rb); production runs PF =
-// false: one slot loaded per step, 154 VGPRs and 3 waves per SIMD, measured faster. Blocks go in
-// XCD-aware order, y fastest, so the neighbouring rows that share 3 of a block's 5 v rows run on the
-// same XCD at the same time.
-constexpr int RR2_WXMAX = 8, RR2_NR2_LOG2_POINTS = 26;
-
-// NR: coarse rows per block (1: fine rows 2Y-1..2Y+1 computed; 2: 2Y-1..2Y+3, the shared row 2Y+1 and three
-// of the seven v rows once instead of twice)
-template <int MODE, bool PF, int NR = 1, bool UN = false, bool NTU = false> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
-__global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* __restrict__ v,
-                                                         const double* __restrict__ f, const double* __restrict__ w,
-                                                         double* __restrict__ ca,
-                                                         double* __restrict__ cb, int fnx, int fny, int fnz,
-                                                         int64_t fldy, int64_t fldz, int cnx, int cny, int cnz, int64_t cldy,
-                                                         int64_t cldz, int ZC, int zhi)
-{
-    static_assert(MODE != GS_NEWTON || !PF, "NEWTON: newtonV rows exceed the budget of the prefetch ring");
-    constexpr int RR = 2 * NR + 1; // computed fine rows; v rows 0 .. RR+1 (0 and RR+1: halo rows)
-    // wave-edge columns [parity][1 + wave][side][plane * 3 + row] of v, and r at each wave's first fine
-    // column [parity][1 + wave][plane * 3 + row]; slots 0 and WX+1 are the zero x-boundary
-    __shared__ double ve[2][RR2_WXMAX + 2][2][2 * RR];
-    __shared__ double re[2][RR2_WXMAX + 2][2 * RR];
-    const int lane = threadIdx.x;
-    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
-    const int WX = blockDim.y;
-    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 2 * 2 * RR; i += WAVE * WX) (&ve[0][0][0][0])[i] = 0.0;
-    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 2 * RR; i += WAVE * WX) (&re[0][0][0])[i] = 0.0;
-    __syncthreads();
-    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-    const int Y = 1 + NR * (int)(tile % gridDim.x);
-    const int Zb = 1 + (int)(tile / gridDim.x) * ZC, Ze = min(Zb + ZC - 1, cnz);
-    const int X = 1 + wx * WAVE + lane;
-    const int x = 2 * X - 1, xl = min(x, fnx + 1);
-    const bool okx0 = x <= fnx, okx1 = x + 1 <= fnx;
-    int64_t roff[RR + 2]; // fine rows 2Y-2 .. 2Y+2NR (computed: 1..RR)
-    bool rowc[RR + 2];
-#pragma unroll
-    for (int j = 0; j < RR + 2; j++) {
-        const int y = 2 * Y - 2 + j;
-        roff[j] = (int64_t)min(max(y, 0), fny + 1) * fldy;
-        rowc[j] = y >= 1 && y <= fny;
-    }
-    // zhi: plane fnz+1 is an internal Z-slab boundary (current ghost planes fnz+1 of v, f, w and
-    // fnz+2 of v): the residual there is real, not the zero of a level boundary
-    auto at = [&](const double* b, int j, int p) {
-        return b + xl + roff[j] + (int64_t)min(max(p, 0), fnz + 1 + zhi) * fldz;
-    };
-    // one step's operands: v planes 2Z+1 (A), 2Z+2 (B) of rows 1..3; halo rows 0 / 4 of planes 2Z (H0)
-    // and 2Z+1 (H1); f of planes 2Z (F0), 2Z+1 (F1) rows 1..3
-    double2 VA[2][RR], VB[2][RR], H0[2][2], H1[2][2], F0[2][RR], F1[2][RR], W0[2][RR], W1[2][RR];
-    auto load_slot = [&](const int s, const int Z) {
-        const int p = 2 * Z;
-#pragma unroll
-        for (int j = 0; j < RR; j++) {
-            // NTU: rows no neighbouring block reads (v: 2Y+1 .. 2Y+2NR-3, f: 2Y .. 2Y+2NR-2) bypass L2
-            // retention, leaving it to the shared halo rows
-            const bool uv = NTU && j >= 2 && j <= RR - 3, uf = NTU && j >= 1 && j <= RR - 2;
-            VA[s][j] = uv ? ld2s<true>(at(v, j + 1, p + 1)) : ld2(at(v, j + 1, p + 1));
-            VB[s][j] = uv ? ld2s<true>(at(v, j + 1, p + 2)) : ld2(at(v, j + 1, p + 2));
-            F0[s][j] = uf ? ld2s<true>(at(f, j + 1, p)) : ld2(at(f, j + 1, p));
-            F1[s][j] = uf ? ld2s<true>(at(f, j + 1, p + 1)) : ld2(at(f, j + 1, p + 1));
-            if (MODE == GS_NEWTON) {
-                W0[s][j] = uf ? ld2s<true>(at(w, j + 1, p)) : ld2(at(w, j + 1, p));
-                W1[s][j] = uf ? ld2s<true>(at(w, j + 1, p + 1)) : ld2(at(w, j + 1, p + 1));
-            }
-        }
-        H0[s][0] = ld2(at(v, 0, p));
-        H0[s][1] = ld2(at(v, RR + 1, p));
-        H1[s][0] = ld2(at(v, 0, p + 1));
-        H1[s][1] = ld2(at(v, RR + 1, p + 1));
-    };
-    // LDS-only barrier: the outstanding prefetch stays in flight across it
-    auto lds_barrier = [] {
-        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-    };
-    // the columns left of lane 0 / right of lane 63 on two planes: v(x-1) of lane 0, v(x+2) of lane 63
-    auto edges_v = [&](int par, const double2 (&P)[RR], const double2 (&Q)[RR], double (&CLp)[RR], double (&CRp)[RR],
-                       double (&CLq)[RR], double (&CRq)[RR]) {
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 0; j < RR; j++) {
-                ve[par][wx + 1][0][j] = P[j].x;
-                ve[par][wx + 1][0][RR + j] = Q[j].x;
-            }
-        }
-        if (lane == WAVE - 1) {
-#pragma unroll
-            for (int j = 0; j < RR; j++) {
-                ve[par][wx + 1][1][j] = P[j].y;
-                ve[par][wx + 1][1][RR + j] = Q[j].y;
-            }
-        }
-        lds_barrier();
-#pragma unroll
-        for (int j = 0; j < RR; j++) {
-            CLp[j] = uniform_d(ve[par][wx][1][j]);
-            CRp[j] = uniform_d(ve[par][wx + 2][0][j]);
-            CLq[j] = uniform_d(ve[par][wx][1][RR + j]);
-            CRq[j] = uniform_d(ve[par][wx + 2][0][RR + j]);
-        }
-    };
-    // r(2X+1) of every lane for two planes: the right neighbour lane's r.x (lane 63: the right wave's)
-    auto edges_r = [&](int par, const double2 (&R)[RR], const double2 (&S)[RR], double (&NQ)[RR], double (&NS)[RR]) {
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 0; j < RR; j++) {
-                re[par][wx + 1][j] = R[j].x;
-                re[par][wx + 1][RR + j] = S[j].x;
-            }
-        }
-        lds_barrier();
-#pragma unroll
-        for (int j = 0; j < RR; j++) {
-            NQ[j] = lane_from_right<true>(R[j].x, uniform_d(re[par][wx + 2][j]));
-            NS[j] = lane_from_right<true>(S[j].x, uniform_d(re[par][wx + 2][RR + j]));
-        }
-    };
-    // r = f - A v on fine plane p, rows 1..3 (k_rb KIND 1: same expression, same term order); 0 outside
-    // the interior, as the reference's never-written boundary of r
-    auto resid = [&](const double2 (&Vm)[RR], const double2 (&Vc)[RR], const double2 (&H)[2], const double2 (&Vp)[RR],
-                     const double2 (&F)[RR], const double2 (&W)[RR], const double (&CL)[RR], const double (&CR)[RR], int p,
-                     double2 (&R)[RR]) {
-        const bool pin = p >= 1 && (p <= fnz || (zhi && p == fnz + 1));
-#pragma unroll
-        for (int j = 0; j < RR; j++) {
-            const double2 c = Vc[j];
-            const double2 ym = j == 0 ? H[0] : Vc[j - 1], yp = j == RR - 1 ? H[1] : Vc[j + 1];
-            const double xm0 = lane_from_left<true>(c.y, CL[j]);
-            const double xp1 = lane_from_right<true>(c.x, CR[j]);
-            const double w0 = MODE == GS_NEWTON ? W[j].x : 0.0, w1 = MODE == GS_NEWTON ? W[j].y : 0.0;
-            const double a0 = op_value<MODE, UN>(k, c.x, c.y, xm0, yp.x, ym.x, Vp[j].x, Vm[j].x, w0);
-            const double a1 = op_value<MODE, UN>(k, c.y, xp1, c.x, yp.y, ym.y, Vp[j].y, Vm[j].y, w1);
-            const bool ok = pin && rowc[j + 1];
-            R[j] = make_double2((ok && okx0) ? F[j].x - a0 : 0.0, (ok && okx1) ? F[j].y - a1 : 0.0);
-        }
-    };
-
-    // prologue: r on fine plane 2Zb-1 (the top plane of the previous coarse plane's stencil)
-    double2 Vm[RR], V0[RR], Rm[RR];
-    double Nm[RR];
-    {
-        const int p = 2 * Zb - 1;
-        double2 Vq[RR], Hq[2], Fq[RR], Wq[RR];
-#pragma unroll
-        for (int j = 0; j < RR; j++) {
-            Vm[j] = ld2(at(v, j + 1, p - 1));
-            Vq[j] = ld2(at(v, j + 1, p));
-            V0[j] = ld2(at(v, j + 1, p + 1));
-            Fq[j] = ld2(at(f, j + 1, p));
-            Wq[j] = MODE == GS_NEWTON ? ld2(at(w, j + 1, p)) : make_double2(0.0, 0.0);
-        }
-        Hq[0] = ld2(at(v, 0, p));
-        Hq[1] = ld2(at(v, RR + 1, p));
-        double CL[RR], CR[RR], CL2[RR], CR2[RR], N2[RR];
-        edges_v(1, Vq, Vq, CL, CR, CL2, CR2);
-        resid(Vm, Vq, Hq, V0, Fq, Wq, CL, CR, p, Rm);
-        edges_r(1, Rm, Rm, Nm, N2);
-#pragma unroll
-        for (int j = 0; j < RR; j++) Vm[j] = Vq[j]; // window: Vm = v(2Zb-1), V0 = v(2Zb)
-    }
-    if (PF) load_slot(1, Zb);
-    // Both halves always run (an odd chunk ends with a step whose results are discarded), and every
-    // load is unconditional (plane indices clamped), so the slots keep fixed registers.
-    for (int z0 = Zb; z0 <= Ze; z0 += 2) {
-#pragma unroll
-        for (int ph = 0; ph < 2; ph++) {
-            const int Z = z0 + ph;
-            const int cs = PF ? ph ^ 1 : 0; // slot holding this step's operands
-            if (PF) load_slot(ph, Z + 1);
-            else load_slot(0, Z);
-            double CL0[RR], CR0[RR], CL1[RR], CR1[RR];
-            edges_v(ph, V0, VA[cs], CL0, CR0, CL1, CR1);
-            double2 R0[RR], R1[RR];
-            resid(Vm, V0, H0[cs], VA[cs], F0[cs], W0[cs], CL0, CR0, 2 * Z, R0);
-            resid(V0, VA[cs], H1[cs], VB[cs], F1[cs], W1[cs], CL1, CR1, 2 * Z + 1, R1);
-            double N0[RR], N1[RR];
-            edges_r(ph, R0, R1, N0, N1);
-#pragma unroll
-            for (int i = 0; i < NR; i++) {
-                if (Z <= Ze && X <= cnx && Y + i <= cny) {
-                    double acc = 0.0;
-#pragma unroll
-                    for (int a = -1; a <= 1; a++)
-#pragma unroll
-                        for (int b = -1; b <= 1; b++)
-#pragma unroll
-                            for (int c = -1; c <= 1; c++) {
-                                const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
-                                                   ((2.0 - (b < 0 ? -b : b)) / 2.0) *
-                                                   ((2.0 - (c < 0 ? -c : c)) / 2.0);
-                                const int j = 2 * i + b + 1;
-                                const double2 rp = c < 0 ? Rm[j] : (c == 0 ? R0[j] : R1[j]);
-                                const double rn = c < 0 ? Nm[j] : (c == 0 ? N0[j] : N1[j]);
-                                acc += wgt * (a < 0 ? rp.x : (a == 0 ? rp.y : rn));
-                            }
-                    const int64_t q = X + (Y + i) * cldy + (int64_t)Z * cldz;
-                    ca[q] = acc;
-                    if (cb) cb[q] = acc;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < RR; j++) {
-                Vm[j] = VA[cs][j];
-                V0[j] = VB[cs][j];
-                Rm[j] = R1[j];
-                Nm[j] = N1[j];
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Trilinear prolongation, closed form per fine point (the reference's inject + X, Y, Z passes,
-// CpuSolver.cpp:240-290, combined in the same X -> Y -> Z order). Fine index P-1 is never written by
-// the reference (stays 0) and coarse index Pc-1 is the zero boundary, so along each axis:
-//   i even -> c(i/2);  i odd -> 0.5*c(i/2) + 0.5*c(i/2+1).
-template <bool SUB>
-__device__ __forceinline__ double coarse_at(const double* __restrict__ c, const double* __restrict__ sub, int64_t q)
-{
-    return SUB ? c[q] - sub[q] : c[q];
-}
-
-// (x, y, gz) are fine indices, gz global along z; the coarse field's local plane 0 is global cz0.
-template <bool SUB>
-__device__ __forceinline__ double prolong_value(const double* __restrict__ c, const double* __restrict__ sub, int x,
-                                                int y, int gz, int64_t cldy, int64_t cldz, int cz0)
-{
-    const int cx = x >> 1, cy = y >> 1, cz = (gz >> 1) - cz0;
-    const bool ox = x & 1, oy = y & 1, oz = gz & 1;
-    auto X = [&](int jy, int jz) -> double {
-        const int64_t q = cx + jy * cldy + (int64_t)jz * cldz;
-        const double a = coarse_at<SUB>(c, sub, q);
-        if (!ox) return a;
-        const double b = coarse_at<SUB>(c, sub, q + 1);
-        return 0.5 * a + 0.5 * b;
-    };
-    auto Y = [&](int jz) -> double {
-        const double a = X(cy, jz);
-        if (!oy) return a;
-        const double b = X(cy + 1, jz);
-        return 0.5 * a + 0.5 * b;
-    };
-    const double a = Y(cz);
-    if (!oz) return a;
-    const double b = Y(cz + 1);
-    return 0.5 * a + 0.5 * b;
-}
-
-// Fused correction, two fine x-points per lane (x odd, x+1 even): one pair load / store of v, and
-// per coarse row the two coarse values c(x>>1), c(x>>1 + 1) that both points interpolate from.
-template <bool SUB>
-__global__ __launch_bounds__(256) void k_prolong_add(const double* __restrict__ c, const double* __restrict__ sub,
-                                                     double* __restrict__ fv, int fnx, int fny, int fnz, int64_t fldy,
-                                                     int64_t fldz, int64_t cldy, int64_t cldz, int fz0, int cz0)
-{
-    const int t = blockIdx.x * 64 + threadIdx.x;
-    const int x = 1 + 2 * t;
-    const int y = 1 + blockIdx.y * 4 + threadIdx.y;
-    const int z = 1 + blockIdx.z;
-    if (x > fnx || y > fny) return;
-    const int gz = z + fz0;
-    const int cx = x >> 1, cy = y >> 1, cz = (gz >> 1) - cz0;
-    const bool oy = y & 1, oz = gz & 1;
-    // X pass: e0 at fine x (odd: average of c(cx), c(cx+1)), e1 at x+1 (even: injection of c(cx+1))
-    auto X2 = [&](int jy, int jz, double& e0, double& e1) {
-        const int64_t q = cx + jy * cldy + (int64_t)jz * cldz;
-        const double a = coarse_at<SUB>(c, sub, q), b = coarse_at<SUB>(c, sub, q + 1);
-        e0 = 0.5 * a + 0.5 * b;
-        e1 = b;
-    };
-    // Y pass on top of X
-    auto Y2 = [&](int jz, double& e0, double& e1) {
-        double a0, a1;
-        X2(cy, jz, a0, a1);
-        if (!oy) {
-            e0 = a0;
-            e1 = a1;
-            return;
-        }
-        double b0, b1;
-        X2(cy + 1, jz, b0, b1);
-        e0 = 0.5 * a0 + 0.5 * b0;
-        e1 = 0.5 * a1 + 0.5 * b1;
-    };
-    double e0, e1;
-    Y2(cz, e0, e1);
-    if (oz) { // Z pass
-        double g0, g1;
-        Y2(cz + 1, g0, g1);
-        e0 = 0.5 * e0 + 0.5 * g0;
-        e1 = 0.5 * e1 + 0.5 * g1;
-    }
-    const int64_t p = x + y * fldy + (int64_t)z * fldz;
-    if (x + 1 <= fnx) {
-        const double2 v = ld2(fv + p);
-        st2s<true>(fv + p, v.x + e0, v.y + e1);
-    } else {
-        fv[p] = fv[p] + e0;
-    }
-}
-
-// The corrected iterate v + P v^2h on the four fine columns around every interior column-block
-// boundary of the prolongation pair (k_tb2y XH + PRO): columns xb-2 .. xb+1 of the boundary at xb (the
-// first column of the right block), rows 0..ny+1, local planes -1..nz+2 — what the blocks on either side
-// read of the neighbour's columns. A point gets the correction where the pair's lanes correct it (x, y
-// interior; the plane interior or a ghost plane of an internal slab side: pok) and keeps v elsewhere,
-// with the reference's X, Y, Z pass arithmetic (prolong_value), so the strip holds bit for bit what the
-// neighbour block's lanes compute in registers. Layout: es[((b * (nz + 4) + p + 1) * 4 + c) * (ny + 2) + y].
-// The coarse field is indexed from the plane under fine local plane 0 (z0 even: local parities are global).
-template <bool SUB>
-__global__ __launch_bounds__(256) void k_pro_strip(const double* __restrict__ v, const double* __restrict__ c,
-                                                   const double* __restrict__ sub, double* __restrict__ es, int nx,
-                                                   int ny, int nz, int64_t ldy, int64_t ldz, int64_t cldy,
-                                                   int64_t cldz, int bw, int zlo, int zhi)
-{
-    const int y = blockIdx.x * 256 + threadIdx.x;
-    if (y > ny + 1) return;
-    const int p = (int)blockIdx.y - 1;
-    const int b = (int)blockIdx.z >> 2, col = (int)blockIdx.z & 3;
-    const int x = 1 + (b + 1) * bw - 2 + col;
-    double val = v[x + (int64_t)y * ldy + (int64_t)p * ldz];
-    const bool pok = (p >= 1 && p <= nz) || (zlo && p <= 0) || (zhi && p > nz);
-    if (pok && y >= 1 && y <= ny && x >= 1 && x <= nx) val = val + prolong_value<SUB>(c, sub, x, y, p, cldy, cldz, 0);
-    es[(((int64_t)b * (nz + 4) + p + 1) * 4 + col) * (ny + 2) + y] = val;
-}
-
-// Unfused reference-shaped interpolate (whole padded fine array), used by parity tests.
-__global__ __launch_bounds__(256) void k_interpolate(const double* __restrict__ c, double* __restrict__ e, int fPx,
-                                                     int fPy, int fPz, int64_t fldy, int64_t fldz, int64_t cldy,
-                                                     int64_t cldz)
-{
-    const int x = blockIdx.x * 64 + threadIdx.x;
-    const int y = blockIdx.y * 4 + threadIdx.y;
-    const int z = blockIdx.z;
-    if (x >= fPx || y >= fPy) return;
-    const int64_t p = x + y * fldy + (int64_t)z * fldz;
-    if (x == fPx - 1 || y == fPy - 1 || z == fPz - 1) {
-        e[p] = 0.0;
-        return;
-    }
-    e[p] = prolong_value<false>(c, nullptr, x, y, z, cldy, cldz, 0);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Level-0 right-hand side, CpuGridData.cpp:7-12, 44-78 (same expression order).
-__device__ __forceinline__ double rhs_f0(double x)
-{
-    return 100 * x * (x - 1.0) * x * (x - 1.0) * x * (x - 1.0) * x * (x - 1.0);
-}
-__device__ __forceinline__ double rhs_f2(double x)
-{
-    return 100.0 * 4.0 * (x - 1.0) * (x - 1.0) * x * x * (14.0 * x * x - 14.0 * x + 3);
-}
-
-__global__ __launch_bounds__(256) void k_rhs(double* __restrict__ f, int mode, double h, double gamma, int nx, int ny,
-                                             int nz, int64_t z0, int64_t ldy, int64_t ldz)
-{
-    const int X = blockIdx.x * 64 + threadIdx.x; // padded indices
-    const int Y = blockIdx.y * 4 + threadIdx.y;
-    const int Z = blockIdx.z;
-    if (X > nx + 1 || Y > ny + 1) return;
-    const int64_t p = X + Y * ldy + (int64_t)Z * ldz;
-    const int64_t Zg = Z + z0;
-    if (mode == GS_LINEAR) {
-        if (X < 1 || X > nx || Y < 1 || Y > ny || Z < 1 || Z > nz) return;
-        const double x = (int)(X - 1) * h, y = (int)(Y - 1) * h, z = (int)(Zg - 1) * h;
-        f[p] = -(rhs_f2(x) * rhs_f0(y) * rhs_f0(z) + rhs_f0(x) * rhs_f2(y) * rhs_f0(z) +
-                 rhs_f0(x) * rhs_f0(y) * rhs_f2(z));
-    } else {
-        const double x = (int)X * h, y = (int)Y * h, z = (int)Zg * h;
-        const double ux = x - x * x, uy = y - y * y, uz = z - z * z;
-        f[p] = 2.0 * ((y - y * y) * (z - z * z) + (x - x * x) * (z - z * z) + (x - x * x) * (y - y * y)) +
-               gamma * ux * uy * uz * exp(ux * uy * uz);
-    }
-}
-
-__global__ __launch_bounds__(256) void k_axpy(double* __restrict__ y, const double* __restrict__ x, double a,
-                                              int64_t n)
-{
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (a == 1.0) y[i] = y[i] + x[i];
-        else if (a == -1.0) y[i] = y[i] - x[i];
-        else y[i] = y[i] + a * x[i];
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// The coarse end of the V-cycle in ONE launch of ONE workgroup (gs_coarse_cycle). A level of a few
-// hundred points is pure launch latency per operator on a chip it cannot fill (~4.5 us a sweep);
-// here the whole recursion of CpuSolver::vcycle below level lv[0] (CpuSolver.cpp:92-135) runs in one
-// 1024-thread workgroup whose levels stay in L2, with a workgroup barrier between operators instead
-// of a kernel boundary (the waves of a workgroup share one CU's L1, so the barrier's workgroup-scope
-// fences order every store before the next operator's loads). Each point is computed by the
-// expression of the per-operator kernel it replaces (k_generic KIND 0 / 1 / 2, k_restrict,
-// k_prolong_add), so every field is bit-identical to the per-operator launch sequence.
-constexpr int CC_T = 1024, CC_MAXLEV = 8;
-
-struct CcLevel {
-    double *v, *va, *f, *r, *rv, *w; // iterate, ping-pong partner, rhs, residual, restV (FAS), newtonV
-    int64_t ldy, ldz;
-    int nx, ny, nz, vz; // vz: the iterate is the zero iterate, not stored
-    Coef k;
-};
-struct CcPlan {
-    CcLevel L[CC_MAXLEV];
-    int n, pre, post;
-};
-
-__device__ __forceinline__ int64_t cc_at(const CcLevel& L, int x, int y, int z)
-{
-    return x + y * L.ldy + (int64_t)z * L.ldz;
-}
-
-// dst[p] (and dst2[p]) = fn(x, y, z, p) for every interior point p of a level, x fastest, strided
-// over the workgroup, B points per thread and pass: all B values are computed before any is stored,
-// so a phase reading the field it writes (prolongation, f += A u) sees only old values.
-template <int B, class F>
-__device__ __forceinline__ void cc_map_b(const CcLevel& L, double* dst, double* dst2, F& fn)
-{
-    const int n = L.nx * L.ny * L.nz;
-    for (int i0 = threadIdx.x; i0 < n; i0 += B * CC_T) {
-        double val[B];
-        int64_t q[B];
-        bool ok[B];
-#pragma unroll
-        for (int b = 0; b < B; b++) {
-            const int i = i0 + b * CC_T;
-            ok[b] = i < n;
-            const int ii = ok[b] ? i : i0; // a valid point; its value is discarded
-            const int t = ii / L.nx, z = t / L.ny;
-            const int x = 1 + ii - t * L.nx, y = 1 + t - z * L.ny;
-            q[b] = cc_at(L, x, y, 1 + z);
-            val[b] = fn(x, y, 1 + z, q[b]);
-        }
-#pragma unroll
-        for (int b = 0; b < B; b++)
-            if (ok[b]) {
-                dst[q[b]] = val[b];
-                if (dst2) dst2[q[b]] = val[b];
-            }
-    }
-}
-template <class F>
-__device__ __forceinline__ void cc_map(const CcLevel& L, double* dst, double* dst2, F&& fn)
-{
-    cc_map_b<1>(L, dst, dst2, fn); // 2 points per pass measured no faster (the levels it runs are tiny)
-}
-
-// A(u) at p in config order (k_generic): the stencil sum, / h^2, the non-linear term; c = u(p),
-// wv = w(p) (NEWTON). uz: u is the zero iterate (literal zeros, as k_generic's v == NULL).
-template <int MODE>
-__device__ __forceinline__ double cc_op(const Coef& k, const double* __restrict__ u, bool uz,
-                                        const double* __restrict__ w, int64_t p, double& c, double& wv)
-{
-    double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < 7; i++) s += k.s[i] * (uz ? 0.0 : u[p + k.off[i]]);
-    s = div_hh(k, s);
-    c = uz ? 0.0 : u[p];
-    wv = (MODE == GS_NEWTON) ? w[p] : 0.0;
-    if (MODE == GS_NEWTON) {
-        const double ew = exp(wv);
-        s += k.gamma * (1 + wv) * c * ew;
-    } else if (MODE == GS_NONLINEAR) {
-        const double ev = exp(c);
-        const double nl = k.gamma * c * ev;
-        s += nl;
-    }
-    return s;
-}
-
-template <int MODE>
-__global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
-{
-    unsigned alt = 0, zero = 0; // per level bit: the iterate is in va / is the unstored zero
-    for (int l = 0; l < P.n; l++)
-        if (P.L[l].vz) zero |= 1u << l;
-    auto cur = [&](int l) { return ((alt >> l) & 1) ? P.L[l].va : P.L[l].v; };
-    // v = 0 made real (HipSolver::materialize)
-    auto materialize = [&](int l) {
-        if (!((zero >> l) & 1)) return;
-        const CcLevel& L = P.L[l];
-        double* v = cur(l);
-        cc_map(L, v, nullptr, [&](int, int, int, int64_t) { return 0.0; });
-        __syncthreads();
-        zero &= ~(1u << l);
-    };
-    // `sweeps` Jacobi sweeps, residual and update fused (k_generic KIND 0), ping-pong v <-> va
-    auto smooth = [&](int l, int sweeps) {
-        const CcLevel& L = P.L[l];
-        if (sweeps == 0) materialize(l);
-        for (int s = 0; s < sweeps; s++) {
-            const bool uz = (zero >> l) & 1;
-            const double* in = cur(l);
-            double* out = ((alt >> l) & 1) ? L.v : L.va;
-            cc_map(L, out, nullptr, [&](int, int, int, int64_t p) {
-                double c, wv;
-                const double a = cc_op<MODE>(L.k, in, uz, L.w, p, c, wv);
-                const double r = L.f[p] - a;
-                return jacobi_update<MODE>(L.k, c, r, wv);
-            });
-            __syncthreads();
-            alt ^= 1u << l;
-            zero &= ~(1u << l);
-        }
-    };
-    // coarse interior of C <- 27-point full weighting of the fine field src of F (k_restrict)
-    auto restrict_to = [&](const double* __restrict__ src, const CcLevel& F, double* ca, double* cb,
-                           const CcLevel& C) {
-        cc_map(C, ca, cb, [&](int x, int y, int z, int64_t) {
-            const double* c0 = src + 2 * x + (int64_t)(2 * y) * F.ldy + (int64_t)(2 * z) * F.ldz;
-            double acc = 0.0;
-#pragma unroll
-            for (int a = -1; a <= 1; a++)
-#pragma unroll
-                for (int b = -1; b <= 1; b++)
-#pragma unroll
-                    for (int c = -1; c <= 1; c++) {
-                        const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
-                                           ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
-                        acc += wgt * c0[a + b * F.ldy + c * F.ldz];
-                    }
-            return acc;
-        });
-    };
-
-    // ---- down: pre-smoothing, f^2h = R(f - A v) [FAS: restV = v^2h = R v, f^2h += A(restV)] ----
-    for (int l = 0; l + 1 < P.n; l++) {
-        const CcLevel &F = P.L[l], &C = P.L[l + 1];
-        smooth(l, P.pre);
-        const double* u = cur(l);
-        cc_map(F, F.r, nullptr, [&](int, int, int, int64_t p) { // residual (k_generic KIND 1)
-            double c, wv;
-            const double a = cc_op<MODE>(F.k, u, false, F.w, p, c, wv);
-            return F.f[p] - a;
-        });
-        __syncthreads();
-        restrict_to(F.r, F, C.f, nullptr, C);
-        if (MODE == GS_NONLINEAR) restrict_to(u, F, C.rv, cur(l + 1), C);
-        __syncthreads();
-        if (MODE == GS_NONLINEAR) { // f += A(restV)  (k_generic KIND 2, ADD)
-            cc_map(C, C.f, nullptr, [&](int, int, int, int64_t p) {
-                double c, wv;
-                const double a = cc_op<GS_NONLINEAR>(C.k, C.rv, false, nullptr, p, c, wv);
-                return C.f[p] + a;
-            });
-            __syncthreads();
-        }
-    }
-    // ---- the coarsest level: pre + post sweeps (CpuSolver.cpp:117) ----
-    smooth(P.n - 1, P.pre + P.post);
-    // ---- up: v^h += P(v^2h [- restV^2h]) (k_prolong_add), post-smoothing ----
-    for (int l = P.n - 1; l > 0; l--) {
-        const CcLevel &C = P.L[l], &F = P.L[l - 1];
-        materialize(l);
-        const double* cv = cur(l);
-        double* fv = cur(l - 1);
-        cc_map(F, fv, nullptr, [&](int x, int y, int z, int64_t p) {
-            const double e = MODE == GS_NONLINEAR ? prolong_value<true>(cv, C.rv, x, y, z, C.ldy, C.ldz, 0)
-                                                  : prolong_value<false>(cv, nullptr, x, y, z, C.ldy, C.ldz, 0);
-            return fv[p] + e;
-        });
-        __syncthreads();
-        smooth(l - 1, P.post);
-    }
-}
-
-int launch_status()
-{
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : (int)e;
-}
-
-bool bad_level(const gs_level* L)
-{
-    return !L || L->nx < 0 || L->ny < 0 || L->nz < 0 || L->ldy < L->nx + 2 || L->ldz < L->ldy * (L->ny + 2) ||
-           L->nx > INT32_MAX / 2 || L->ny > INT32_MAX / 2 || L->nz > INT32_MAX / 2;
-}
-
-// Dispatch a stencil pass over (mode, kind) to the fast or the generic kernel.
-// ---------------------------------------------------------------------------------------------
-// Two fused Jacobi sweeps (temporal blocking): out = S(S(v)) reading v and f once and writing once
-// (24 B per two lattice updates instead of 48). Wavefront along z: at step z the block computes
-// sweep 1 at plane z — rows y0-1..y0+RY, i.e. one recomputed halo row per side — and sweep 2 at
-// plane z-1 for rows y0..y0+RY-1. A block spans the whole x-row: WX waves of 128 columns whose
-// outside columns (of v, and of the sweep-1 values) come from the neighbour waves through LDS, so
-// nothing is recomputed along x. Where a sweep-1 point is a level boundary (x or y index 0 / n+1,
-// z index 0 / nz+1 unless zlo / zhi says that side is an internal Z-slab boundary whose two ghost
-// planes are current) its value is the boundary value itself, exactly as a stored sweep would leave
-// it. Per point the arithmetic is the single sweep's, so the result is bit-identical to two
-// gs_jacobi_sweep calls.
-template <int MODE, int RY, int WXMAX, bool NT, bool NTF = NT, bool ZV = false>
-__global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __restrict__ v,
-                                                      const double* __restrict__ f, const double* __restrict__ w,
-                                                      double* __restrict__ out, double* __restrict__ partials, int nx,
-                                                      int ny, int nz, int64_t ldy, int64_t ldz, int ZC, int zlo,
-                                                      int zhi, const double*, const double*, int, int, int, int64_t,
-                                                      int64_t, const double*)
-{
-    __shared__ double red[WXMAX];
-    double sumsq = 0.0; // r^2 of sweep 1's residual over the block's own points (partials != NULL)
-    constexpr int NV = RY + 2;  // sweep-1 rows (j = 1..RY+2 <-> y0-1..y0+RY)
-    constexpr int NE = NV + RY; // LDS edge values per wave side: v rows + sweep-1 rows
-    // edge[parity][1 + wave][side][value]; slots 0 and WX+1 are virtual waves holding the x-boundary
-    // columns, which this kernel takes to be zero (the reference's homogeneous Dirichlet boundary:
-    // v's boundary cells are never written)
-    __shared__ double edge[2][WXMAX + 2][2][NE];
-    const int lane = threadIdx.x;
-    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
-    const int WX = blockDim.y;
-    for (int i = threadIdx.x + threadIdx.y * WAVE; i < 2 * (WXMAX + 2) * 2 * NE; i += WAVE * WX)
-        (&edge[0][0][0][0])[i] = 0.0;
-    __syncthreads();
-    const int x0 = 1 + wx * (2 * WAVE);
-    const int x = x0 + 2 * lane;
-    const int xl = min(x, nx + 1);
-    const bool bx0 = x > nx, bx1 = x + 1 > nx;            // boundary / beyond columns
-    const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
-    // XCD-aware order (cdna_hip_programming.md T1): hardware block b runs on XCD b % 8, so logical
-    // tiles are dealt out in contiguous runs per XCD, y-tile fastest: the blocks an XCD runs at one
-    // time are y-neighbours marching the same planes, and the halo rows one of them re-reads were
-    // just fetched into that XCD's L2 by its neighbour.
-    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-    const int y0 = 1 + (int)(tile % gridDim.x) * RY;
-    const int zb = 1 + (int)(tile / gridDim.x) * ZC;
-    const int ze = min(zb + ZC - 1, nz);
-
-    int64_t roff[RY + 4]; // rows y0-2 .. y0+RY+1
-    bool rowc[RY + 4];    // row is a computable interior row
-#pragma unroll
-    for (int j = 0; j < RY + 4; j++) {
-        const int y = y0 - 2 + j;
-        roff[j] = (int64_t)min(max(y, 0), ny + 1) * ldy;
-        rowc[j] = y >= 1 && y <= ny;
-    }
-    auto planeok = [&](int z) { return (z >= 1 && z <= nz) || (z == 0 && zlo) || (z == nz + 1 && zhi); };
-    auto at = [&](const double* base, int j, int z) { return base + xl + roff[j] + (int64_t)z * ldz; };
-
-    // Register window (rows j = 1..NV of the v planes; rows 0 and RY+3 only as halo pairs): Vp, Vc =
-    // v at planes z-1, z; V1p, V1c = sweep-1 values at planes z-2, z-1; Fprev, Wprev = f, w at z-1.
-    // What step z loads (v rows of plane z+2, f / w rows and the halo rows of plane z+1) goes into
-    // slot ph of a two-slot ring and is consumed from there one step later before being moved on,
-    // so every wait lands a full step of arithmetic after its load (loop unrolled by two).
-    double2 Vp[NV], Vc[NV], VL[2][NV], FL[2][NV], WL[2][NV], HL[2][2];
-    double2 V1p[RY], V1c[NV], Fprev[RY], Wprev[RY];
-#pragma unroll
-    for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
-#pragma unroll
-    for (int j = 0; j < RY; j++) V1p[j] = make_double2(0.0, 0.0);
-    // slot s <- plane z's f, w, halo rows and plane zv's v rows
-    auto load_slot = [&](const int s, const int z, const int zv) {
-#pragma unroll
-        for (int j = 1; j <= NV; j++) {
-            VL[s][j - 1] = ldv2<ZV>(at(v, j, zv));
-            FL[s][j - 1] = ld2s<NTF>(at(f, j, z));
-            if (MODE == GS_NEWTON) WL[s][j - 1] = ld2(at(w, j, z));
-        }
-        HL[s][0] = ldv2<ZV>(at(v, 0, z));
-        HL[s][1] = ldv2<ZV>(at(v, RY + 3, z));
-    };
-#pragma unroll
-    for (int j = 1; j <= NV; j++) {
-        Vp[j - 1] = ldv2<ZV>(at(v, j, zb - 2));
-        Vc[j - 1] = ldv2<ZV>(at(v, j, zb - 1));
-    }
-    load_slot(1, zb - 1, zb);
-    // Both halves always run (an odd step count ends with one step whose results are discarded) and
-    // every load is unconditional (plane indices clamped into the padded range), so the slots keep
-    // fixed registers around the loop.
-    for (int z0 = zb - 1; z0 <= ze + 1; z0 += 2) {
-#pragma unroll
-        for (int ph = 0; ph < 2; ph++) {
-            const int z = z0 + ph;
-            const int cs = ph ^ 1; // slot holding plane z (and v of plane z+1)
-            load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
-            // ---- exchange the columns just outside each wave: v(z) rows 1..NV, sweep-1(z-1) rows 2..RY+1 ----
-            if (lane == 0) {
-#pragma unroll
-                for (int j = 1; j <= NV; j++) edge[ph][wx + 1][0][j - 1] = Vc[j - 1].x;
-#pragma unroll
-                for (int j = 2; j <= RY + 1; j++) edge[ph][wx + 1][0][NV + j - 2] = V1c[j - 1].x;
-            }
-            if (lane == WAVE - 1) {
-#pragma unroll
-                for (int j = 1; j <= NV; j++) edge[ph][wx + 1][1][j - 1] = Vc[j - 1].y;
-#pragma unroll
-                for (int j = 2; j <= RY + 1; j++) edge[ph][wx + 1][1][NV + j - 2] = V1c[j - 1].y;
-            }
-            // LDS-only barrier: the outstanding prefetch must stay in flight across it
-            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
-            __builtin_amdgcn_s_barrier();
-            double CL[NE], CR[NE];
-#pragma unroll
-            for (int i = 0; i < NE; i++) {
-                CL[i] = edge[ph][wx][1][i];     // wave wx-1 (slot 0: the zero x = 0 boundary)
-                CR[i] = edge[ph][wx + 2][0][i]; // wave wx+1 (slot WX+1: the zero x = nx+1 boundary)
-            }
-
-            // ---- sweep 1 at plane z ----
-            double2 V1n[NV];
-            const bool pz = planeok(z);
-#pragma unroll
-            for (int j = 1; j <= NV; j++) {
-                const double2 c = Vc[j - 1], zm = Vp[j - 1], zp = VL[cs][j - 1];
-                const double2 ym = j == 1 ? HL[cs][0] : Vc[j - 2], yp = j == NV ? HL[cs][1] : Vc[j];
-                const double xm0 = lane_from_left<true>(c.y, CL[j - 1]);
-                const double xp1 = lane_from_right<true>(c.x, CR[j - 1]);
-                const double wx0 = (MODE == GS_NEWTON) ? WL[cs][j - 1].x : 0.0;
-                const double wx1 = (MODE == GS_NEWTON) ? WL[cs][j - 1].y : 0.0;
-                const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
-                const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
-                const double r0 = FL[cs][j - 1].x - a0, r1 = FL[cs][j - 1].y - a1;
-                const double n0 = jacobi_update<MODE>(k, c.x, r0, wx0);
-                const double n1 = jacobi_update<MODE>(k, c.y, r1, wx1);
-                if (partials && j >= 2 && j <= RY + 1 && z >= zb && z <= ze && rowc[j]) {
-                    if (okx0) sumsq += r0 * r0;
-                    if (okx1) sumsq += r1 * r1;
-                }
-                const bool keep = !pz || !rowc[j];
-                V1n[j - 1] = make_double2((keep || bx0) ? c.x : n0, (keep || bx1) ? c.y : n1);
-            }
-            // ---- sweep 2 at plane z-1 ----
-            if (z - 1 >= zb && z - 1 <= ze) {
-                const int64_t zo = (int64_t)(z - 1) * ldz;
-#pragma unroll
-                for (int j = 2; j <= RY + 1; j++) {
-                    const double2 c = V1c[j - 1], ym = V1c[j - 2], yp = V1c[j], zm = V1p[j - 2], zp = V1n[j - 1];
-                    const double xm0 = lane_from_left<true>(c.y, CL[NV + j - 2]);
-                    const double xp1 = lane_from_right<true>(c.x, CR[NV + j - 2]);
-                    const double wx0 = (MODE == GS_NEWTON) ? Wprev[j - 2].x : 0.0;
-                    const double wx1 = (MODE == GS_NEWTON) ? Wprev[j - 2].y : 0.0;
-                    const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
-                    const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
-                    const double o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 2].x - a0, wx0);
-                    const double o1 = jacobi_update<MODE>(k, c.y, Fprev[j - 2].y - a1, wx1);
-                    if (y0 - 2 + j <= ny) {
-                        double* q = out + x + roff[j] + zo;
-                        if (okx1) st2s<NT>(q, o0, o1);
-                        else if (okx0) *q = o0;
-                    }
-                }
-            }
-            // ---- rotate (only registers whose loads were consumed above) ----
-#pragma unroll
-            for (int j = 0; j < RY; j++) {
-                V1p[j] = V1c[j + 1];
-                Fprev[j] = FL[cs][j + 1];
-                if (MODE == GS_NEWTON) Wprev[j] = WL[cs][j + 1];
-            }
-#pragma unroll
-            for (int j = 0; j < NV; j++) {
-                V1c[j] = V1n[j];
-                Vp[j] = Vc[j];
-                Vc[j] = VL[cs][j];
-            }
-        }
-    }
-    if (partials) {
-        const double t = block_sum<WXMAX>(sumsq, red, WX);
-        if (threadIdx.x == 0 && threadIdx.y == 0) partials[tile] = t;
-    }
-}
-
-// The fused pair with two wave-rows per block ("tb2y"): the block is WX waves along x (the whole row)
-// times 2 waves along y; the y-wave 0 owns output rows y0..y0+RY-1, the y-wave 1 rows
-// y0+RY..y0+2RY-1. Between the two, the rows they need of each other (v of plane z and sweep-1 of
-// plane z-1 at the shared edge) pass through LDS instead of being re-read and recomputed, so a block
-// of 2RY output rows recomputes only ONE sweep-1 halo row per side and reads v rows y0-2..y0+2RY+1,
-// f rows y0-1..y0+2RY: v 1 + 4/(2RY), f 1 + 2/(2RY) times the compulsory bytes before any L2 reuse
-// (k_tb2 at RY rows per wave: 1 + 4/RY and 1 + 2/RY).
-// Both y-waves run the same code on a local row index j = -1..RY+1: wave 0 maps j to y0-1+j, wave 1
-// to the mirror image y0+2RY-j, so for both j = 0 is the recomputed halo row, j = 1..RY the own rows,
-// j = RY the row published to the other wave, j = RY+1 the row received from it and j = -1 the one
-// halo row of v loaded from memory. On wave 1 local j+1 is global y-1: the two y-neighbours are
-// swapped back before the stencil sum, which keeps the reference's term order.
-// PRO = 1 / 2: the input iterate is v + P(c) / v + P(c - sub) — the prolongation and correction of
-// the V-cycle's up-leg (CpuSolver.cpp:121-132, gs_prolong_add) fused into the first post-smoothing
-// pair, so the corrected iterate is never stored. The correction is added to every v value when it
-// is consumed (the loads stay in flight as before): X-pass values of the two coarse planes under the
-// current fine planes live in registers (W0, W1) and the next coarse plane is prefetched one step
-// ahead; the z-chunk is even, so every fine plane's parity, hence its Y/Z combination, is static.
-//
-// XH (rows of more than 2 * WAVE * WX points): the row is split into column blocks of 2 * WAVE * WX
-// points, one per block. The column just outside a block edge that is interior belongs to the
-// neighbouring block; the edge wave computes what its LDS slot would hold there itself: v of plane z at
-// that column (loads) and sweep 1 of plane z-1 at that column, evaluated lane-parallel one local row per
-// lane (lane j <-> local row j, y-neighbours by lane shifts, x-neighbours loaded) with the same point
-// expression, so every output is bit-identical to two gs_jacobi_sweep calls.
-template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0,
-          int PFD = 1, bool XH = false, bool UN = false>
-__global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* __restrict__ v,
-                                                           const double* __restrict__ f, const double* __restrict__ w,
-                                                           double* __restrict__ out, double* __restrict__ partials,
-                                                           int nx, int ny, int nz, int64_t ldy, int64_t ldz, int ZC,
-                                                           int zlo, int zhi, const double* __restrict__ pc,
-                                                           const double* __restrict__ ps, int cnx, int cny, int cnz,
-                                                           int64_t cldy, int64_t cldz, const double* __restrict__ es)
-{
-    static_assert(PRO == 0 || (SPEC && !ZV && RY % 2 == 0), "fused prolongation: per-wave code, even RY");
-    static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR) && MODE != GS_NEWTON && RY + 2 <= WAVE),
-                  "column blocks: LINEAR / NONLINEAR pairs, LINEAR prolongation pairs");
-    constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
-    constexpr int NE = NV + RY; // x-edge values per wave side: v rows 0..RY, sweep-1 rows 1..RY
-    __shared__ double red[2 * WXMAX];
-    // x-edges: [parity][y-wave][1 + x-wave][side][value]; x-wave slots 0 and WX+1 are the zero
-    // x-boundary columns (the reference's homogeneous Dirichlet boundary)
-    __shared__ double edge[2][2][WXMAX + 2][2][NE];
-    // y-edge rows: [parity][y-wave][x-wave][v | sweep-1][lane]
-    __shared__ double2 yrow[2][2][WXMAX][2][WAVE];
-    const int lane = threadIdx.x;
-    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
-    const int wy = __builtin_amdgcn_readfirstlane(threadIdx.z);
-    const int WX = blockDim.y;
-    const int tid = threadIdx.x + WAVE * (threadIdx.y + WX * threadIdx.z);
-    for (int i = tid; i < 2 * 2 * (WXMAX + 2) * 2 * NE; i += WAVE * WX * 2) (&edge[0][0][0][0][0])[i] = 0.0;
-    __syncthreads();
-    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-    // XH: column blocks fastest (the two edges a pair of neighbours share are read on one XCD)
-    const int BW = 2 * WAVE * WX; // columns per block
-    const int nh = XH ? (nx + BW - 1) / BW : 1;
-    const int hx = XH ? (int)((tile % gridDim.x) % nh) : 0;
-    const int xb = 1 + hx * BW;
-    const int x0 = xb + wx * (2 * WAVE);
-    const int x = x0 + 2 * lane;
-    const int xl = min(x, nx + 1);
-    const bool bx0 = x > nx, bx1 = x + 1 > nx;
-    const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
-    const int y0 = 1 + (int)((tile % gridDim.x) / nh) * (2 * RY);
-    const int zb = 1 + (int)(tile / gridDim.x) * ZC;
-    const int ze = min(zb + ZC - 1, nz);
-    const bool mir = wy != 0;
-    auto yof = [&](int j) { return mir ? y0 + 2 * RY - j : y0 - 1 + j; };
-
-    int64_t roff[RY + 2]; // local rows j = -1..RY at index j+1
-    bool rowc[RY + 2];
-#pragma unroll
-    for (int j = -1; j <= RY; j++) {
-        const int y = yof(j);
-        roff[j + 1] = (int64_t)min(max(y, 0), ny + 1) * ldy;
-        rowc[j + 1] = y >= 1 && y <= ny;
-    }
-    auto planeok = [&](int z) { return (z >= 1 && z <= nz) || (z == 0 && zlo) || (z == nz + 1 && zhi); };
-    auto at = [&](const double* base, int j, int z) { return base + xl + roff[j + 1] + (int64_t)z * ldz; };
-    // XH edge column xe (wave 0: left of the block, wave WX-1: right of it) when it is interior
-    const bool eL = XH && wx == 0 && hx > 0;
-    const bool eR = XH && wx == WX - 1 && xb + BW <= nx;
-    const bool edg = eL || eR; // wave-uniform
-    const int xe = eL ? xb - 1 : xb + BW;
-    int64_t eroff = 0; // lane j <-> local row j = 0..RY+1
-    bool erowc = false;
-    if (XH) {
-        const int y = yof(min(lane, RY + 1));
-        eroff = (int64_t)min(max(y, 0), ny + 1) * ldy;
-        erowc = y >= 1 && y <= ny;
-    }
-    auto eat = [&](const double* base, int dx, int z) { return base + (xe + dx) + eroff + (int64_t)z * ldz; };
-    // XH + PRO: the edge column's corrected iterate v + P v^2h (columns xe-1..xe+1) comes from the strip
-    // k_pro_strip wrote for this launch (layout there): [boundary][plane -1..nz+2][column xb-2..xb+1][row]
-    const double* esr = es;
-    if (XH && PRO != 0 && edg) {
-        const int hb = eL ? hx - 1 : hx; // the block boundary the edge column lies at
-        const int y = yof(min(lane, RY + 1));
-        esr = es + (int64_t)hb * (nz + 4) * 4 * (ny + 2) + (eL ? 1 : 2) * (ny + 2) + min(max(y, 0), ny + 1);
-    }
-    auto sat = [&](int dx, int z) { return esr + ((int64_t)(z + 1) * 4 + dx) * (ny + 2); };
-
-    // PFD: prefetch distance in plane steps. 1: two operand slots (this step's, the next one's in
-    // flight); 2: four named slots, three live (this step's and the next two in flight), the z loop
-    // unrolled by 4 so every slot index is static
-    static_assert(PFD == 1 || PFD == 2, "prefetch distance 1 or 2");
-    constexpr int NS = PFD == 2 ? 4 : 2, UNR = PFD == 2 ? 4 : 2;
-    double2 Vp[NV], Vc[NV], VL[NS][NV], FL[NS][NV], WL[NS][NV], HL[NS];
-    double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
-    // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes A from the
-    // newtonV rows at z-1 and reads E = exp(w) from LDS (same expressions, same values)
-    constexpr bool RECOMP = MODE == GS_NEWTON && PRO != 0;
-    // (Wprev, Fprev: sweep 2's newtonV / f rows at z-1, in LDS like the coarse rows below)
-    __shared__ double2 wprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
-    __shared__ double2 fprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
-    // exp(w) of sweep 1's own rows, by plane parity: sweep 2 reads the previous plane's (each lane its own
-    // values, no barrier) instead of evaluating exp a second time (+32 KB: 148 KB, one block per CU as before)
-    __shared__ double2 eprev_l[RECOMP ? 2 : 1][RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
-#pragma unroll
-    for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
-#pragma unroll
-    for (int j = 0; j < RY; j++) V1p[j] = make_double2(0.0, 0.0);
-    // XH edge column: v at plane z+1 (EA), its x-neighbours (EXm, EXp) and f at plane z, per slot;
-    // EP / EC: v at planes z-1 / z; ES1c: sweep 1 at plane z-1
-    double EA[XH ? NS : 1], EXm[XH ? NS : 1], EXp[XH ? NS : 1], EF[XH ? NS : 1], EP = 0.0, EC = 0.0, ES1c = 0.0;
-    auto load_slot = [&](const int s, const int z, const int zv) {
-#pragma unroll
-        for (int j = 0; j < NV; j++) {
-            VL[s][j] = ldv2<ZV>(at(v, j, zv));
-            FL[s][j] = ld2s<NTF>(at(f, j, z));
-            if (MODE == GS_NEWTON) WL[s][j] = ld2(at(w, j, z));
-        }
-        HL[s] = ldv2<ZV>(at(v, -1, z));
-        if constexpr (XH) {
-            if (edg) {
-                if constexpr (PRO != 0) {
-                    EA[s] = *sat(0, zv);
-                    EXm[s] = *sat(-1, z);
-                    EXp[s] = *sat(1, z);
-                } else {
-                    EA[s] = ldv1<ZV>(eat(v, 0, zv));
-                    EXm[s] = ldv1<ZV>(eat(v, -1, z));
-                    EXp[s] = ldv1<ZV>(eat(v, 1, z));
-                }
-                EF[s] = *eat(f, 0, z);
-            }
-        }
-    };
-#pragma unroll
-    for (int j = 0; j < NV; j++) {
-        Vp[j] = ldv2<ZV>(at(v, j, zb - 2));
-        Vc[j] = ldv2<ZV>(at(v, j, zb - 1));
-    }
-    if (XH && edg) {
-        EP = PRO != 0 ? *sat(0, zb - 2) : ldv1<ZV>(eat(v, 0, zb - 2));
-        EC = PRO != 0 ? *sat(0, zb - 1) : ldv1<ZV>(eat(v, 0, zb - 1));
-    }
-    // ---- fused prolongation (PRO): coarse rows cyb .. cyb+NCR-1 lie under the wave's fine rows ----
-    constexpr int NCR = RY / 2 + 2;
-    const int cxl = min(x >> 1, max(cnx, 0)); // the lane's coarse column (fine pair x odd, x+1 even)
-    const int cyb = mir ? ((y0 - 1) >> 1) + RY / 2 : ((y0 - 1) >> 1) - 1;
-    int64_t crow[NCR];
-#pragma unroll
-    for (int r = 0; r < NCR; r++) crow[r] = (int64_t)min(max(cyb + r, 0), cny + 1) * cldy;
-    double2 W0[NCR], W1[NCR], Wm[NCR]; // X-pass values of coarse planes K, K+1 (Wm: K-1, first step)
-    // HALF: the same rows times 0.5, the product every Y and Z pass of the reference takes of them first
-    // (0.5 * fine(y-1) + 0.5 * fine(y+1) with fine(y+-1) an X-pass value; 0.5 * fine(z) + 0.5 * fine(z+2)
-    // with fine(z), fine(z+2) X-pass values on even rows): formed once per coarse row instead of at every
-    // fine point that reads it — the same products, so the same bits
-    constexpr bool HALF = !RECOMP && GS_PRO_HALF;
-    double2 H0[HALF ? NCR : 1], H1[HALF ? NCR : 1], Hm[HALF ? NCR : 1];
-    // NEWTON (RECOMP): the X-pass rows of planes K, K+1 live in LDS, slot wsl / wsl^1 — each lane
-    // reads back only what it wrote, so no barrier; this keeps the variant inside 256 VGPRs
-    __shared__ double2 wlds[RECOMP ? 2 : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? NCR : 1][RECOMP ? WAVE : 1];
-    int wsl = 0;
-    const int wid_l = RECOMP ? wx + WX * wy : 0;
-    // coarse X-pass row r of plane slot s (0: K, 1: K+1, 2: K-1 on the first step)
-    auto wget = [&](int s, int r) -> double2 {
-        if (s == 2) return Wm[r];
-        if constexpr (RECOMP) return wlds[s ^ wsl][wid_l][r][lane];
-        else return s == 0 ? W0[r] : W1[r];
-    };
-    auto hget = [&](int s, int r) -> double2 { return s == 2 ? Hm[HALF ? r : 0] : (s == 0 ? H0[HALF ? r : 0] : H1[HALF ? r : 0]); };
-    double RA[NCR], RB[NCR], SA[NCR], SB[NCR]; // raw c (and sub) of plane K+2, in flight
-    auto craw = [&](int cz) {
-        // coarse planes -1 .. cnz+2 exist in the layout; only those under corrected fine planes matter
-        const int64_t zo = (int64_t)min(max(cz, -1), cnz + 2) * cldz + cxl;
-#pragma unroll
-        for (int r = 0; r < NCR; r++) {
-            RA[r] = pc[zo + crow[r]];
-            RB[r] = pc[zo + crow[r] + 1];
-            if (PRO == 2) {
-                SA[r] = ps[zo + crow[r]];
-                SB[r] = ps[zo + crow[r] + 1];
-            }
-        }
-    };
-    // X pass of gs_prolong_add: e(x odd) = 0.5 a + 0.5 b, e(x+1 even) = b, a / b = c(cx) / c(cx+1)
-    auto xpass = [&](int s) {
-#pragma unroll
-        for (int r = 0; r < NCR; r++) {
-            const double a = PRO == 2 ? RA[r] - SA[r] : RA[r], b = PRO == 2 ? RB[r] - SB[r] : RB[r];
-            const double2 X = make_double2(0.5 * a + 0.5 * b, b);
-            if constexpr (HALF) {
-                const double2 Hh = make_double2(0.5 * X.x, 0.5 * X.y);
-                if (s == 2) Hm[r] = Hh;
-                else if (s == 0) H0[r] = Hh;
-                else H1[r] = Hh;
-            }
-            if (s == 2) Wm[r] = X;
-            else if constexpr (RECOMP) wlds[s ^ wsl][wid_l][r][lane] = X;
-            else if (s == 0) W0[r] = X;
-            else W1[r] = X;
-        }
-    };
-    // the correction of local row j on a plane whose coarse neighbours are Wa (and Wb when the fine
-    // plane is odd), Y pass then Z pass; added where the fine point is interior
-    auto correct = [&](double2& val, int j, bool zodd, bool zin, int sa, int sb, auto mirc) {
-        constexpr bool M = decltype(mirc)::get();
-        const int u = M ? 2 * RY + 1 - j : j + 2; // fine row = 2 (coarse base) + u
-        const int ri = M ? (u >> 1) - RY / 2 : (u >> 1);
-        const bool yodd = u & 1;
-        auto ypass = [&](int s) {
-            const double2 X0 = wget(s, ri);
-            if (!yodd) return X0;
-            const double2 X1 = wget(s, ri + 1);
-            return make_double2(0.5 * X0.x + 0.5 * X1.x, 0.5 * X0.y + 0.5 * X1.y);
-        };
-        double2 e;
-        if constexpr (HALF) {
-            auto hsum = [](double2 p, double2 q) { return make_double2(p.x + q.x, p.y + q.y); };
-            if (!zodd) {
-                e = yodd ? hsum(hget(sa, ri), hget(sa, ri + 1)) : wget(sa, ri);
-            } else if (!yodd) {
-                e = hsum(hget(sa, ri), hget(sb, ri));
-            } else {
-                const double2 ea = hsum(hget(sa, ri), hget(sa, ri + 1)), eb = hsum(hget(sb, ri), hget(sb, ri + 1));
-                e = make_double2(0.5 * ea.x + 0.5 * eb.x, 0.5 * ea.y + 0.5 * eb.y);
-            }
-        } else {
-            e = ypass(sa);
-            if (zodd) {
-                const double2 g = ypass(sb);
-                e = make_double2(0.5 * e.x + 0.5 * g.x, 0.5 * e.y + 0.5 * g.y);
-            }
-        }
-        if (zin && rowc[j + 1]) {
-            if (okx0) val.x = val.x + e.x;
-            if (okx1) val.y = val.y + e.y;
-        }
-    };
-    // a fine plane gets the correction when it is interior or a ghost plane of an internal slab side
-    auto pok = [&](int p) { return (p >= 1 && p <= nz) || (zlo && p <= 0) || (zhi && p > nz); };
-    if (PRO) {
-        const int m0 = (zb - 1) >> 1; // zb is odd: planes zb-2 = 2 m0 - 1, zb - 1 = 2 m0
-        craw(m0 - 1);
-        xpass(2);
-        craw(m0);
-        xpass(0);
-        craw(m0 + 1);
-        xpass(1);
-        auto pro_init = [&](auto mirc) {
-#pragma unroll
-            for (int j = 0; j < NV; j++) {
-                correct(Vp[j], j, true, pok(zb - 2), 2, 0, mirc);
-                correct(Vc[j], j, false, pok(zb - 1), 0, 0, mirc);
-            }
-        };
-        if (mir) pro_init(BoolC<true>{});
-        else pro_init(BoolC<false>{});
-    }
-    if (PFD == 1) {
-        load_slot(1, zb - 1, zb);
-    } else {
-        load_slot(0, zb - 1, zb);
-        load_slot(1, zb, zb + 1);
-    }
-    double sumsq = 0.0;
-    for (int z0 = zb - 1; z0 <= ze + 1; z0 += UNR) {
-#pragma unroll
-        for (int ph4 = 0; ph4 < UNR; ph4++) {
-            // the last two steps of a 4-step round are skipped past the chunk (uniform branch)
-            if (UNR == 4 && ph4 == 2 && z0 + 2 > ze + 1) break;
-            const int ph = ph4 & 1; // plane parity (z0 is even): LDS double buffers, PRO combinations
-            const int z = z0 + ph4;
-            const int cs = PFD == 1 ? ph ^ 1 : ph4; // slot holding this step's operands
-            if (PFD == 1) load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
-            else load_slot((ph4 + 2) & 3, min(z + 2, nz + 1), min(z + 3, nz + 2));
-            if (PRO && GS_PRO_EXP < 2 && ph == 0) craw((z >> 1) + 2); // consumed at the end of the next step
-            // ---- publish: x-edge columns (v(z) rows 0..RY, sweep-1(z-1) rows 1..RY) and the y-edge row
-            if (lane == 0) {
-#pragma unroll
-                for (int j = 0; j < NV; j++) edge[ph][wy][wx + 1][0][j] = Vc[j].x;
-#pragma unroll
-                for (int j = 1; j <= RY; j++) edge[ph][wy][wx + 1][0][NV + j - 1] = V1c[j].x;
-            }
-            if (lane == WAVE - 1) {
-#pragma unroll
-                for (int j = 0; j < NV; j++) edge[ph][wy][wx + 1][1][j] = Vc[j].y;
-#pragma unroll
-                for (int j = 1; j <= RY; j++) edge[ph][wy][wx + 1][1][NV + j - 1] = V1c[j].y;
-            }
-            yrow[ph][wy][wx][0][lane] = Vc[RY];
-            yrow[ph][wy][wx][1][lane] = V1c[RY];
-            // LDS-only barrier: the outstanding prefetch stays in flight across it
-            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
-            __builtin_amdgcn_s_barrier();
-            double CL[NE], CR[NE];
-#pragma unroll
-            for (int i = 0; i < NE; i++) { // wave-uniform: kept in SGPRs
-                CL[i] = uniform_d(edge[ph][wy][wx][1][i]);
-                CR[i] = uniform_d(edge[ph][wy][wx + 2][0][i]);
-            }
-            const double2 vY = yrow[ph][wy ^ 1][wx][0][lane]; // v(z) at local row RY+1
-            const double2 sY = yrow[ph][wy ^ 1][wx][1][lane]; // sweep-1(z-1) at local row RY+1
-            if constexpr (XH) {
-                // the edge column beyond an interior block edge: v(z) rows 0..RY, sweep-1(z-1) rows 1..RY
-                if (edg) {
-#pragma unroll
-                    for (int i = 0; i < NE; i++) {
-                        const double e = i < NV ? EC : ES1c;
-                        const int ln = i < NV ? i : i - NV + 1;
-                        const long long b = __double_as_longlong(e);
-                        const int lo = __builtin_amdgcn_readlane((int)b, ln), hi = __builtin_amdgcn_readlane((int)(b >> 32), ln);
-                        const double u = __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
-                        if (eL) CL[i] = u;
-                        else CR[i] = u;
-                    }
-                }
-            }
-
-            // ---- the two sweeps; wave 1 (mirrored rows) runs its own copy of the code, so the swap of
-            // its y-neighbours costs no selects ----
-            double2 V1n[NV];
-            double2 Acur[RY], Ecur[RY]; // NEWTON terms of sweep 1's own rows (-> Aprev / Eprev)
-            const bool pz = planeok(z);
-            double ES1n = 0.0;
-            auto sweeps = [&](auto mirc) {
-                const bool M = mirc.get();
-                if constexpr (XH) {
-                    // sweep 1 at plane z on the edge column, local row = lane (rows 1..RY are used)
-                    if (edg) {
-                        const double c = EC;
-                        const double lm = lane_from_left<true>(EC, 0.0), lp = lane_from_right<true>(EC, 0.0);
-                        const double ym = M ? lp : lm, yp = M ? lm : lp;
-                        const double a = op_value<MODE, UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP, 0.0);
-                        const double nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
-                        ES1n = (!pz || !erowc) ? c : nv;
-                    }
-                }
-                if constexpr (PRO != 0 && GS_PRO_EXP == 0) {
-                    // the corrected iterate: plane z+1 (VL) and the halo row at plane z (HL); with z0
-                    // even, ph 0 has z even (z+1 odd: coarse K, K+1) and ph 1 has z odd
-#pragma unroll
-                    for (int j = 0; j < NV; j++)
-                        correct(VL[cs][j], j, ph == 0, pok(z + 1), ph == 0 ? 0 : 1, 1, mirc);
-                    correct(HL[cs], -1, ph == 1, pok(z), 0, 1, mirc);
-                }
-                // sweep 1 at plane z, local rows 0..RY
-#pragma unroll
-                for (int j = 0; j < NV; j++) {
-                    const double2 c = Vc[j], zm = Vp[j], zp = VL[cs][j];
-                    const double2 lm = j == 0 ? HL[cs] : Vc[j - 1], lp = j == RY ? vY : Vc[j + 1];
-                    const double2 ym = M ? lp : lm, yp = M ? lm : lp;
-                    const double xm0 = lane_from_left<true>(c.y, CL[j]);
-                    const double xp1 = lane_from_right<true>(c.x, CR[j]);
-                    double q[2] = {stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
-                                   stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
-                    div_hh_row<MODE>(k, q);
-                    double a0, a1, n0, n1;
-                    if constexpr (MODE == GS_NEWTON) {
-                        const double2 wv = WL[cs][j];
-                        const double2 A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
-                        const double2 E = make_double2(exp(wv.x), exp(wv.y));
-                        if (!RECOMP && j >= 1) {
-                            Acur[j - 1] = A;
-                            Ecur[j - 1] = E;
-                        }
-                        if (RECOMP && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
-                        a0 = newton_op(q[0], c.x, A.x, E.x);
-                        a1 = newton_op(q[1], c.y, A.y, E.y);
-                        n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
-                        n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
-                    } else {
-                        a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
-                        a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
-                        n0 = jacobi_update<MODE>(k, c.x, FL[cs][j].x - a0, 0.0);
-                        n1 = jacobi_update<MODE>(k, c.y, FL[cs][j].y - a1, 0.0);
-                    }
-                    const double r0 = FL[cs][j].x - a0, r1 = FL[cs][j].y - a1;
-                    if (partials && j >= 1 && z >= zb && z <= ze && rowc[j + 1]) {
-                        if (okx0) sumsq += r0 * r0;
-                        if (okx1) sumsq += r1 * r1;
-                    }
-                    const bool keep = !pz || !rowc[j + 1];
-                    V1n[j] = make_double2((keep || bx0) ? c.x : n0, (keep || bx1) ? c.y : n1);
-                }
-                // sweep 2 at plane z-1, own rows 1..RY
-                if (z - 1 >= zb && z - 1 <= ze) {
-                    const int64_t zo = (int64_t)(z - 1) * ldz;
-#pragma unroll
-                    for (int j = 1; j <= RY; j++) {
-                        const double2 c = V1c[j], zm = V1p[j - 1], zp = V1n[j];
-                        const double2 lm = V1c[j - 1], lp = j == RY ? sY : V1c[j + 1];
-                        const double2 ym = M ? lp : lm, yp = M ? lm : lp;
-                        const double xm0 = lane_from_left<true>(c.y, CL[NV + j - 1]);
-                        const double xp1 = lane_from_right<true>(c.x, CR[NV + j - 1]);
-                        double q[2] = {stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
-                                       stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
-                        div_hh_row<MODE>(k, q);
-                        double o0, o1;
-                        if constexpr (MODE == GS_NEWTON) {
-                            double2 A, E;
-                            if constexpr (RECOMP) {
-                                const double2 wv = wprev_l[j - 1][wx + WX * wy][lane];
-                                A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
-                                E = eprev_l[ph ^ 1][j - 1][wx + WX * wy][lane];
-                            } else {
-                                A = Aprev[j - 1];
-                                E = Eprev[j - 1];
-                            }
-                            const double a0 = newton_op(q[0], c.x, A.x, E.x);
-                            const double a1 = newton_op(q[1], c.y, A.y, E.y);
-                            const double2 fp = RECOMP ? fprev_l[j - 1][wx + WX * wy][lane] : Fprev[j - 1];
-                            o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
-                            o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
-                        } else {
-                            const double a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
-                            const double a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
-                            o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 1].x - a0, 0.0);
-                            o1 = jacobi_update<MODE>(k, c.y, Fprev[j - 1].y - a1, 0.0);
-                        }
-                        if (yof(j) <= ny) {
-                            double* qo = out + x + roff[j + 1] + zo;
-                            if (okx1) st2s<NT>(qo, o0, o1);
-                            else if (okx0) *qo = o0;
-                        }
-                    }
-                }
-            };
-            if constexpr (!SPEC) {
-                sweeps(RtBool{mir});
-            } else {
-                if (mir) sweeps(BoolC<true>{});
-                else sweeps(BoolC<false>{});
-            }
-            // ---- rotate ----
-#pragma unroll
-            for (int j = 1; j <= RY; j++) {
-                V1p[j - 1] = V1c[j];
-                if (!RECOMP) Fprev[j - 1] = FL[cs][j];
-                if constexpr (RECOMP) {
-                    wprev_l[j - 1][wx + WX * wy][lane] = WL[cs][j];
-                    fprev_l[j - 1][wx + WX * wy][lane] = FL[cs][j];
-                } else if (MODE == GS_NEWTON) {
-                    Aprev[j - 1] = Acur[j - 1];
-                    Eprev[j - 1] = Ecur[j - 1];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < NV; j++) {
-                V1c[j] = V1n[j];
-                Vp[j] = Vc[j];
-                Vc[j] = VL[cs][j];
-            }
-            if constexpr (XH) {
-                EP = EC;
-                EC = EA[cs];
-                ES1c = ES1n;
-            }
-            if (PRO && GS_PRO_EXP < 2 && ph == 1) { // next step: coarse planes K+1, K+2
-                if constexpr (RECOMP) {
-                    wsl ^= 1;
-                } else {
-#pragma unroll
-                    for (int r = 0; r < NCR; r++) W0[r] = W1[r];
-                    if constexpr (HALF) {
-#pragma unroll
-                        for (int r = 0; r < NCR; r++) H0[r] = H1[r];
-                    }
-                }
-                xpass(1);
-            }
-        }
-    }
-    if (partials) {
-        // fixed-order block sum: waves in (x, y) order
-        sumsq = wave_sum(sumsq);
-        const int wid = wx + WX * wy;
-        if (lane == 0) red[wid] = sumsq;
-        __syncthreads();
-        if (tid == 0) {
-            double t = 0.0;
-            for (int i = 0; i < 2 * WX; i++) t += red[i];
-            partials[tile] = t;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// The first pre-smoothing pair, the residual of its result and the full-weighting restriction in ONE
-// pass (k_prr, LINEAR; CpuSolver.cpp:94-99 with preSmoothing = 2: jacobi x2, compResidual, restrict).
-// Level 0 of a 2+2 V-cycle is then two passes instead of three: this kernel reads v and f once and
-// writes v'' and the coarse f (25 B per fine point instead of 24 + 17).
-// A block is the whole x-row — PRR_WX waves, ONE column per lane, so a lane's z-windows of four stages
-// fit its registers — times a tile of PRR_T = 4 output rows y0..y0+3 (y0 odd: the tile holds the
-// centres of coarse rows (y0+1)/2 and (y0+3)/2). The restriction needs r on rows y0..y0+4, r needs v''
-// on y0-1..y0+5, v'' needs sweep 1 on y0-2..y0+6 and sweep 1 needs v on y0-3..y0+7: every stage's
-// extra rows are recomputed in-lane (no y exchange). Wavefront along z, at step z: sweep 1 at plane
-// z, sweep 2 at z-1, r at z-2, and the restriction of coarse plane Z = (z-4)/2 from r at z-5..z-3
-// (one step late, so that every x-edge it reads was published before this step's one barrier).
-// x-neighbours: DPP lane shifts, the columns beyond a wave's edges (v, sweep 1, sweep 2) through LDS;
-// r goes to an LDS ring of five planes that the restriction reads directly. A block walks a chunk of
-// coarse planes Zb..Ze: fine output planes 2Zb-1..2Ze (the last chunk up to nz), with the pipeline's
-// z-halo (sweep 1 from 2Zb-3, r up to 2Ze+1) recomputed at the chunk ends. Every point uses the
-// expression of k_tb2y / k_rr2 (same order, same boundary values), so v'' and the coarse f are
-// bit-identical to gs_jacobi_sweep2 + gs_residual_restrict; the norm partials are those of r = f - A v
-// (the input), as the speculative pair's, in this kernel's block order.
-// MEASURED SLOWER than the two passes it replaces, so the driver does not use it: 1.45 vs 1.10 ms at
-// 512^3 (tools/prr_bench.py). Its traffic is 1.06 x the 25 B/point, but the in-lane recomputation
-// costs 21 stencil evaluations per 4 outputs against 15 for pair + k_rr2, and one column per lane
-// doubles the DPP shifts: PMC 1.54 x the VALU instructions of the two kernels at 254 VGPRs (no
-// prefetch room beyond one plane of v). Kept as a tested operator (tests/test_gpu_pair_restrict.py).
-constexpr int PRR_WX = 8, PRR_T = 4, PRR_RS = 5; // x-waves, output rows per block, r ring planes
-
-template <bool UN>
-__global__ __launch_bounds__(WAVE* PRR_WX) void k_prr(Coef k, const double* __restrict__ v, const double* __restrict__ f,
-                                                      double* __restrict__ out, double* __restrict__ partials,
-                                                      double* __restrict__ ca, double* __restrict__ cb, int nx, int ny,
-                                                      int nz, int64_t ldy, int64_t ldz, int cnx, int cny, int cnz,
-                                                      int64_t cldy, int64_t cldz, int ZC)
-{
-    // local rows i (global y0 + i): v -3..7, sweep 1 -2..6, sweep 2 -1..5, r 0..4
-    constexpr int NV = 11, N1 = 9, N2 = 7, NR = 5;
-    constexpr int NE = N1 + N2 + NR; // x-edge values per wave side and plane parity
-    constexpr int RW = WAVE * PRR_WX + 2; // r ring row: columns 0 .. 64 WX + 1
-    __shared__ double edge[2][PRR_WX + 2][2][NE];
-    // r of the last planes, every column of the tile's rows 0..4: slot p mod 5 (the restriction at step z
-    // reads planes z-5..z-3 while a wave one step ahead writes z-1 — five slots keep them apart)
-    __shared__ double rring[PRR_RS][NR][RW];
-    __shared__ double red[PRR_WX];
-    const int lane = threadIdx.x;
-    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
-    const int WX = blockDim.y;
-    const int tid = lane + WAVE * wx;
-    for (int i = tid; i < 2 * (PRR_WX + 2) * 2 * NE; i += WAVE * WX) (&edge[0][0][0][0])[i] = 0.0;
-    for (int i = tid; i < PRR_RS * NR * RW; i += WAVE * WX) (&rring[0][0][0])[i] = 0.0;
-    __syncthreads();
-    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-    const int y0 = 1 + (int)(tile % gridDim.x) * PRR_T;
-    const int Zb = 1 + (int)(tile / gridDim.x) * ZC, Ze = min(Zb + ZC - 1, cnz);
-    const int zb = 2 * Zb - 1, ze = Ze == cnz ? nz : 2 * Ze; // output planes of v''
-    const int rlast = 2 * Ze + 1;                            // last plane of r
-    const int s2last = max(ze, rlast + 1), s1last = s2last + 1;
-    const int x = 1 + wx * WAVE + lane;
-    const int xl = min(x, nx + 1);
-    const bool okx = x <= nx;
-    int64_t roff[NV]; // rows -3..7 at index i + 3
-    bool rowc[NV];
-#pragma unroll
-    for (int i = 0; i < NV; i++) {
-        const int y = y0 - 3 + i;
-        roff[i] = (int64_t)min(max(y, 0), ny + 1) * ldy;
-        rowc[i] = y >= 1 && y <= ny;
-    }
-    auto at = [&](const double* b, int i, int p) {
-        return b + xl + roff[i + 3] + (int64_t)min(max(p, 0), nz + 1) * ldz;
-    };
-    auto pin = [&](int p) { return p >= 1 && p <= nz; };
-    auto rslot = [](int p) { return ((p % PRR_RS) + PRR_RS) % PRR_RS; };
-
-    double Vm[N1], Vc[NV], Vn[NV], VL[NV]; // v at z-1 (rows -2..6), z, z+1, z+2 in flight (rows -3..7)
-    double F0[N1], F1[N2], F2[NR];        // f at z (rows -2..6), z-1 (-1..5), z-2 (0..4)
-    double S1a[N2], S1b[N1];              // sweep 1 at z-2 (rows -1..5), z-1 (-2..6)
-    double S2a[NR], S2b[N2];              // sweep 2 at z-3 (rows 0..4), z-2 (-1..5)
-#pragma unroll
-    for (int i = 0; i < N1; i++) Vm[i] = *at(v, i - 2, zb - 3);
-#pragma unroll
-    for (int i = 0; i < NV; i++) {
-        Vc[i] = *at(v, i - 3, zb - 2);
-        Vn[i] = *at(v, i - 3, zb - 1);
-    }
-#pragma unroll
-    for (int i = 0; i < N2; i++) {
-        F1[i] = 0.0;
-        S1a[i] = 0.0;
-        S2b[i] = 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < N1; i++) S1b[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < NR; i++) {
-        F2[i] = 0.0;
-        S2a[i] = 0.0;
-    }
-    double sumsq = 0.0;
-    auto lds_barrier = [] {
-        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): LDS only, the loads stay in flight
-        __builtin_amdgcn_s_barrier();
-    };
-
-    for (int z = zb - 2; z <= s1last + 1; z++) {
-        // ---- loads: v(z+2) for the next step, f(z) for this step's sweep 1 ----
-#pragma unroll
-        for (int i = 0; i < NV; i++) VL[i] = *at(v, i - 3, z + 2);
-#pragma unroll
-        for (int i = 0; i < N1; i++) F0[i] = *at(f, i - 2, z);
-        // ---- publish x-edges: v(z) rows -2..6, sweep 1 (z-1) rows -1..5, sweep 2 (z-2) rows 0..4 ----
-        const int ph = z & 1;
-        if (lane == 0 || lane == WAVE - 1) {
-            const int sd = lane == 0 ? 0 : 1;
-#pragma unroll
-            for (int i = 0; i < N1; i++) edge[ph][wx + 1][sd][i] = Vc[i + 1];
-#pragma unroll
-            for (int i = 0; i < N2; i++) edge[ph][wx + 1][sd][N1 + i] = S1b[i + 1];
-#pragma unroll
-            for (int i = 0; i < NR; i++) edge[ph][wx + 1][sd][N1 + N2 + i] = S2b[i + 1];
-        }
-        lds_barrier();
-        // the columns left of lane 0 / right of lane 63 (LDS broadcast reads, straight into the DPP's old operand)
-        auto CL = [&](int i) { return edge[ph][wx][1][i]; };
-        auto CR = [&](int i) { return edge[ph][wx + 2][0][i]; };
-
-        // ---- restriction of coarse plane Z from r at 2Z-1, 2Z, 2Z+1 (= z-5, z-4, z-3), read from the ring ----
-        if (!(z & 1) && (z - 4) / 2 >= Zb && (z - 4) / 2 <= Ze) {
-            const int Z = (z - 4) / 2;
-            const int X = x >> 1;
-            const int sl[3] = {rslot(z - 5), rslot(z - 4), rslot(z - 3)};
-            if (!(x & 1) && X <= cnx) {
-#pragma unroll
-                for (int t = 0; t < 2; t++) {
-                    const int Y = (y0 + 1) / 2 + t, ic = 1 + 2 * t; // centre row y0 + ic = 2Y
-                    if (Y > cny) continue;
-                    double acc = 0.0;
-#pragma unroll
-                    for (int a = -1; a <= 1; a++)
-#pragma unroll
-                        for (int b = -1; b <= 1; b++)
-#pragma unroll
-                            for (int c = -1; c <= 1; c++) {
-                                const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
-                                                   ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
-                                acc += wgt * rring[sl[c + 1]][ic + b][x + a];
-                            }
-                    const int64_t q = X + Y * cldy + (int64_t)Z * cldz;
-                    ca[q] = acc;
-                    if (cb) cb[q] = acc;
-                }
-            }
-        }
-
-        // ---- sweep 1 at plane z, rows -2..6 ----
-        double S1n[N1];
-        if (z <= s1last) {
-            double q[N1];
-#pragma unroll
-            for (int i = 0; i < N1; i++) {
-                const double c = Vc[i + 1];
-                const double xm = lane_from_left<true>(c, CL(i)), xp = lane_from_right<true>(c, CR(i));
-                q[i] = stencil_sum<UN>(k, c, xp, xm, Vc[i + 2], Vc[i], Vn[i + 1], Vm[i]);
-            }
-            div_hh_n(k, q);
-            const bool pz = pin(z);
-            const bool own = partials && z >= zb && z <= ze && pz && okx;
-#pragma unroll
-            for (int i = 0; i < N1; i++) {
-                const double c = Vc[i + 1];
-                const double r0 = F0[i] - q[i];
-                const double n = jacobi_update<GS_LINEAR>(k, c, r0, 0.0);
-                S1n[i] = (pz && rowc[i + 1] && okx) ? n : c;
-                if (own && i >= 2 && i <= 5 && rowc[i + 1]) sumsq += r0 * r0;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < N1; i++) S1n[i] = 0.0;
-        }
-        // ---- sweep 2 at plane z-1, rows -1..5 (stored: rows 0..3 of the output planes) ----
-        double S2n[N2];
-        if (z - 1 >= zb - 1 && z - 1 <= s2last) {
-            double q[N2];
-#pragma unroll
-            for (int i = 0; i < N2; i++) {
-                const double c = S1b[i + 1];
-                const double xm = lane_from_left<true>(c, CL(N1 + i)), xp = lane_from_right<true>(c, CR(N1 + i));
-                q[i] = stencil_sum<UN>(k, c, xp, xm, S1b[i + 2], S1b[i], S1n[i + 1], S1a[i]);
-            }
-            div_hh_n(k, q);
-            const int p = z - 1;
-            const bool pz = pin(p);
-            const bool st = p >= zb && p <= ze && pz && okx;
-#pragma unroll
-            for (int i = 0; i < N2; i++) {
-                const double c = S1b[i + 1];
-                const double n = jacobi_update<GS_LINEAR>(k, c, F1[i] - q[i], 0.0);
-                S2n[i] = (pz && rowc[i + 2] && okx) ? n : c;
-                if (st && i >= 1 && i <= 4 && rowc[i + 2])
-                    __builtin_nontemporal_store(n, out + x + roff[i + 2] + (int64_t)p * ldz);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < N2; i++) S2n[i] = 0.0;
-        }
-        // ---- r = f - A v'' at plane z-2, rows 0..4 (0 outside the interior) -> the ring ----
-        if (z - 2 >= zb && z - 2 <= rlast) {
-            double q[NR];
-#pragma unroll
-            for (int i = 0; i < NR; i++) {
-                const double c = S2b[i + 1];
-                const double xm = lane_from_left<true>(c, CL(N1 + N2 + i)), xp = lane_from_right<true>(c, CR(N1 + N2 + i));
-                q[i] = stencil_sum<UN>(k, c, xp, xm, S2b[i + 2], S2b[i], S2n[i + 1], S2a[i]);
-            }
-            div_hh_n(k, q);
-            const bool pz = pin(z - 2);
-            const int sl = rslot(z - 2);
-#pragma unroll
-            for (int i = 0; i < NR; i++) rring[sl][i][x] = (pz && rowc[i + 3] && okx) ? F2[i] - q[i] : 0.0;
-        }
-        // ---- rotate ----
-#pragma unroll
-        for (int i = 0; i < NR; i++) {
-            S2a[i] = S2b[i + 1];
-            F2[i] = F1[i + 1];
-        }
-#pragma unroll
-        for (int i = 0; i < N2; i++) {
-            S2b[i] = S2n[i];
-            S1a[i] = S1b[i + 1];
-            F1[i] = F0[i + 1];
-        }
-#pragma unroll
-        for (int i = 0; i < N1; i++) {
-            S1b[i] = S1n[i];
-            Vm[i] = Vc[i + 1];
-        }
-#pragma unroll
-        for (int i = 0; i < NV; i++) {
-            Vc[i] = Vn[i];
-            Vn[i] = VL[i];
-        }
-    }
-    if (partials) {
-        sumsq = wave_sum(sumsq);
-        if (lane == 0) red[wx] = sumsq;
-        __syncthreads();
-        if (tid == 0) {
-            double t = 0.0;
-            for (int i = 0; i < WX; i++) t += red[i];
-            partials[tile] = t;
-        }
-    }
-}
-
-// Shapes of the fused pair. Rows of <= 512 points: k_tb2y, 2 y-waves of TBY_RY rows each under the
-// 4 x-waves of a row (8 waves, ~218 VGPRs: two waves per SIMD; NEWTON carries the w rows too and takes
-// 2 rows per wave to stay clear of spills). Rows of <= 1024 points: k_tb2 at 2
-// rows per wave in blocks of <= 8 x-waves (measured on MI355X with tools/kbench.py --pairs: at 2 rows
-// a wave needs ~216 VGPRs, so two waves share a SIMD and hide each other's latency, which beats the
-// lower halo overhead of 3-6 rows at one wave per SIMD by 20-25%).
-constexpr int TBY_RY = 2, TBY_RY_NEWTON = 2, TBY_WX = 4, TB_RY_B = 2, TB_WX_B = 8;
-// prefetch distance of k_tb2y (plane steps): LINEAR keeps two steps in flight (215 VGPRs, still two
-// waves per SIMD; 0.662 vs 0.673 ms per 512^3 pair, profiles/r01m_summary.md), the other modes and
-// the fused prolongation one (VGPR budget: the LINEAR prolongation pair at distance 2 spills)
-constexpr int tby_pfd(int mode) { return mode == GS_LINEAR && GS_PRO_EXP != 3 ? 2 : 1; }
-// column blocks (XH): LINEAR at distance 2 too (247 VGPRs, no spill); GS_TBX_PFD=1 selects distance 1 (A/B)
-bool tbx_pfd2()
-{
-    static const bool two = !getenv("GS_TBX_PFD") || std::atoi(getenv("GS_TBX_PFD")) != 1;
-    return two;
-}
-
-// Column blocks (k_tb2y XH) for rows of more than 512 points in LINEAR / NONLINEAR mode: 1024-point rows
-// (BASELINE config #5) were k_tb2's one-y-wave shape before; GS_PAIR_XH=0 restores that (A/B).
-bool xh_enabled()
-{
-    static const bool on = !getenv("GS_PAIR_XH") || std::atoi(getenv("GS_PAIR_XH")) != 0;
-    return on;
-}
-
-// Geometry rule of the fused pair: the whole x-row in one block (or, XH, one column block of 512
-// points) and enough work for >= 128 blocks of 4-plane chunks; the z-chunk is then chosen for >= 1024
-// blocks (4..64 planes: at 512^3, 64-plane chunks measured 5-8% faster than 32 — fewer re-read
-// chunk-boundary planes). Returns 0 (impossible), 1 (possible) or 2 (possible and fills the GPU);
-// *y2: the k_tb2y whole-row shape, *xh: the k_tb2y column-block shape (neither: k_tb2).
-// Blocks of `threads` threads kernel `fn` keeps resident on the whole GPU (occupancy x CUs, cached).
-int64_t resident_blocks(const void* fn, int threads)
-{
-    static std::mutex m;
-    static std::map<std::pair<const void*, int>, int64_t> cache;
-    std::lock_guard<std::mutex> lk(m);
-    const auto key = std::make_pair(fn, threads);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    int per = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, 0) != hipSuccess || per < 1) per = 1;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        cus = 256;
-    (void)hipGetLastError();
-    return cache[key] = (int64_t)per * cus;
-}
-
-// Round-aware chunking for levels whose grid is a few rounds of resident blocks: the chunk length c
-// in [lo, hi] (even if `even`) maximising (blocks / (rounds x capacity)) x c / (c + halo) — whole
-// rounds, long chunks (each recomputes ~halo planes) — among those that still fill the GPU.
-// GS_FIT_ROUNDS=0 keeps the callers' rules (A/B). Returns 0 for "keep".
-int fit_chunk(int64_t tiles, int64_t planes, int64_t cap, int lo, int hi, bool even, double halo)
-{
-    static const bool off = getenv("GS_FIT_ROUNDS") && atoi(getenv("GS_FIT_ROUNDS")) == 0;
-    if (off || tiles < 1 || planes < 1 || cap < 1) return 0;
-    double best = -1.0;
-    int bc = 0;
-    for (int c = lo; c <= hi; c++) {
-        if (even && (c & 1)) continue;
-        const int64_t blocks = tiles * ((planes + c - 1) / c);
-        if (blocks < cap && bc != 0) continue; // would leave CUs idle where a shorter chunk does not
-        const int64_t rounds = (blocks + cap - 1) / cap;
-        const double score = (double)blocks / (double)(rounds * cap) * c / (c + halo);
-        if (score > best) {
-            best = score;
-            bc = c;
-        }
-    }
-    return bc;
-}
-
-// refit a plan's z-chunk (grid.y) for kernel `fn` at `threads` threads
-template <class K>
-void refit_chunks(K* fn, int threads, int64_t planes, int lo, int hi, bool even, double halo, int* zc, dim3* g)
-{
-    const int c = fit_chunk(g->x, planes, resident_blocks((const void*)fn, threads), lo, hi, even, halo);
-    if (c > 0) {
-        *zc = c;
-        g->y = (unsigned)((planes + c - 1) / c);
-    }
-}
-
-// compute units of the current device (cached per device)
-int64_t device_cus()
-{
-    static std::mutex m;
-    static std::map<int, int64_t> cache;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    std::lock_guard<std::mutex> lk(m);
-    auto it = cache.find(dev);
-    if (it != cache.end()) return it->second;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    (void)hipGetLastError();
-    return cache[dev] = cus;
-}
-
-// chunk length (planes) of pair launches over plane ranges past a slab's first plane; 0: the rules
-// for whole levels. Read at every call (tools/exchange_probe.py varies it in one process).
-int slab_zc()
-{
-    const char* e = getenv("GS_SLAB_ZC");
-    return e && *e ? std::atoi(e) : 0;
-}
-
-// the same for plane ranges from a level's first plane (whole single-GPU levels of >= 2^26 points); A/B
-int whole_zc()
-{
-    const char* e = getenv("GS_PAIR_ZC");
-    return e && *e ? std::atoi(e) : 0;
-}
-
-int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
-             int mode = GS_LINEAR, bool* xh = nullptr)
-{
-    if (!S || !L || !canonical_order(S) || L->nx < 1 || L->ny < 1 || L->nz < 1) return 0;
-    const bool two = L->nx <= 2 * WAVE * TBY_WX;
-    const bool colb = !two && mode != GS_NEWTON && xh_enabled() && L->nx <= (int64_t)1 << 20;
-    if (!two && !colb && L->nx > 2 * WAVE * TB_WX_B) return 0;
-    const int64_t nh = colb ? (L->nx + 2 * WAVE * TBY_WX - 1) / (2 * WAVE * TBY_WX) : 1;
-    const int rows = (two || colb) ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block
-    const int64_t tiles = (L->ny + rows - 1) / rows * nh;
-    // the block count (of 4-plane chunks) from which the pair is the level's smoother: 128 takes 64^3
-    // (256 blocks: ZV pair + prolongation pair 23.5 us vs 4 one-point sweeps + prolongation 24.7 us) and
-    // leaves 32^3 (64 blocks: 25.2 vs 23.9 us) to the one-point kernel (rocprofv3 V-cycle traces, r02:
-    // tools/rr_ab_session.sh pmb GS_PAIR_MIN_BLOCKS 512 128);
-    // GS_PAIR_MIN_BLOCKS overrides it (A/B)
-    static const int64_t minBlocks = getenv("GS_PAIR_MIN_BLOCKS") ? std::atoll(getenv("GS_PAIR_MIN_BLOCKS")) : 128;
-    const int fills = tiles * ((L->nz + 3) / 4) >= minBlocks ? 2 : 1;
-    int64_t c = tiles * L->nz / 1024;
-    c = c < 4 ? 4 : (c > 64 ? 64 : c);
-    // levels of >= 2^26 points: chunks for ~512 blocks, up to 128 planes (one 8-wave block per CU, two
-    // rounds at 512^3; fewer re-read chunk-boundary planes): 0.658 vs 0.674 ms per 512^3 pair
-    // (tools/kbench.py --pairs --zc 64,96,128). GS_PAIR_BIG_CHUNKS=0 keeps the 64-plane rule (A/B).
-    static const bool big_chunks = !getenv("GS_PAIR_BIG_CHUNKS") || std::atoi(getenv("GS_PAIR_BIG_CHUNKS")) != 0;
-    // (k_tb2, 1024-point rows: 5.99 vs 6.12 ms per 1024^3 pair, 0.774 vs 0.779 ms on a 1024x1024x128 slab)
-    if (big_chunks && L->nx * L->ny * L->nz >= ((int64_t)1 << 26)) {
-        const int64_t b = tiles * L->nz / 512;
-        c = b < 64 ? 64 : (b > 128 ? 128 : b);
-        // k_tb2y shapes whose tiles fit the CUs: chunks long enough for ONE round of blocks (every
-        // k_tb2y variant at this size runs one 8-wave block per CU). 512^3: 256 blocks of 256 planes,
-        // pair 0.587 vs 0.602 ms, V-cycle 2.16 vs 2.18 ms (tools/ab_multi.sh; 170- and 192-plane
-        // chunks, i.e. uneven rounds, are far slower). Only for plane ranges from the level's first plane
-        // (z0 = 0: whole single-GPU levels): the interior launch of an overlapped Z-slab sweep keeps two
-        // rounds, so that the ghost exchange running beside it (RCCL kernels on the comm stream) finds
-        // free CUs halfway through instead of waiting for every block of the interior to retire.
-        // GS_PAIR_ONE_ROUND=0 keeps the rule above (A/B).
-        static const bool one_round = !getenv("GS_PAIR_ONE_ROUND") || std::atoi(getenv("GS_PAIR_ONE_ROUND")) != 0;
-        const int64_t cus = device_cus();
-        if (one_round && (two || colb) && tiles <= cus && L->z0 == 0) {
-            const int64_t per = cus / tiles; // chunks per tile
-            int64_t c1 = (L->nz + per - 1) / per;
-            c1 += c1 & 1;
-            if (c1 > c) c = c1;
-        } else if (one_round && colb && tiles > cus && L->z0 == 0) {
-            // more tiles than CUs (1024^3: 512 column-block tiles): chunks for four rounds of blocks where
-            // that lengthens them (1024^3: 512 planes, pair 4.90 vs 5.00-5.06 ms, tools/zc_sweep.sh,
-            // profiles/r02k; a 1024x1024x128 slab keeps its 128-plane chunks, 0.622 vs 0.641 ms at 64)
-            const int64_t per = std::max<int64_t>(1, 4 * cus / tiles);
-            int64_t c1 = (L->nz + per - 1) / per;
-            c1 += c1 & 1;
-            if (c1 > c) c = c1;
-        }
-        // plane ranges past a slab's first plane (the interior launch of an overlapped Z-slab sweep):
-        // GS_SLAB_ZC-plane chunks, so that blocks retire often and the ghost exchange's kernels
-        // (RCCL's need a whole SIMD's registers) find a free CU soon after they are enqueued
-        if (L->z0 != 0) {
-            const int sz = slab_zc();
-            if (sz > 0) c = std::max(2, sz); // >= 2: the even rounding below must not reach 0
-        } else {
-            const int wz = whole_zc();
-            if (wz > 0) c = std::max(2, wz);
-        }
-    }
-    c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)
-    *zc = (int)c;
-    *grid = dim3((unsigned)tiles, (unsigned)((L->nz + c - 1) / c));
-    *block = dim3(WAVE, colb ? (unsigned)TBY_WX : (unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), (two || colb) ? 2 : 1);
-    if (y2) *y2 = two;
-    if (xh) *xh = colb;
-    return fills;
-}
-
-// Production shape of the register-blocked kernel (chosen by tools/kbench.py on MI355X,
-// profiles/r01a_kbench.json): 8 rows x 128 columns per wave, 2 waves per block, non-temporal f /
-// output streams. The z-chunk is chosen per launch so the grid keeps >= 2048 blocks (at most 32
-// planes, at least 4); a level too small for that many 4-plane chunks runs the one-point-per-thread
-// kernel instead (coarse levels are latency-bound: parallelism beats register blocking there).
-constexpr int RB_RY = 2, RB_W = 4, RB_ZCMAX = 32, RB_ZCMIN = 4;
-constexpr bool RB_NT = true;
-
-struct PassPlan {
-    bool rb;
-    int zc;
-    dim3 grid;
-};
-
-PassPlan pass_plan(const gs_stencil* S, const gs_level* L)
-{
-    PassPlan p{false, 0, dim3(1)};
-    if (!canonical_order(S)) {
-        p.grid = gn_grid(L);
-        return p;
-    }
-    const int64_t tiles = ((L->nx + 2 * WAVE - 1) / (2 * WAVE)) * ((L->ny + RB_RY * RB_W - 1) / (RB_RY * RB_W));
-    if (tiles * ((L->nz + RB_ZCMIN - 1) / RB_ZCMIN) < 1024) {
-        p.grid = gn_grid(L);
-        return p;
-    }
-    int64_t zc = L->nz * tiles / 2048;
-    zc = zc < RB_ZCMIN ? RB_ZCMIN : (zc > RB_ZCMAX ? RB_ZCMAX : zc);
-    p.rb = true;
-    p.zc = (int)zc;
-    p.grid = rb_grid(L, RB_RY, RB_W, p.zc);
-    return p;
-}
-
-template <int KIND, bool ADD>
-int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, double gamma, const double* v,
-                const double* f, const double* w, double* out, double* partials, hipStream_t st)
-{
-    // v == NULL: the zero iterate (sweeps only, not in NONLINEAR mode, whose coarse iterates are
-    // restrictions, never zero)
-    if (!S || bad_level(L) || !valid_stencil(S) || (!v && (KIND != 0 || mode == GS_NONLINEAR))) return GS_EINVAL;
-    if (mode < GS_LINEAR || mode > GS_NEWTON) return GS_EINVAL;
-    if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
-    const Coef k = make_coef(S, L, omega, gamma);
-    const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
-    const PassPlan plan = pass_plan(S, L);
-    if (plan.rb) {
-        const dim3 g = plan.grid, b(WAVE, RB_W);
-#define GS_RBU(M, Z, U) hipLaunchKernelGGL((k_rb<M, KIND, ADD, RB_RY, RB_W, true, RB_NT, false, false, Z, U>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz, plan.zc)
-#define GS_RB(M, Z) do { if (k.unit) GS_RBU(M, Z, true); else GS_RBU(M, Z, false); } while (0)
-        if (!v) {
-            if constexpr (KIND == 0 && !ADD) {
-                if (mode == GS_LINEAR) GS_RB(GS_LINEAR, true);
-                else GS_RB(GS_NEWTON, true);
-            }
-        } else if (mode == GS_LINEAR) GS_RB(GS_LINEAR, false);
-        else if (mode == GS_NONLINEAR) GS_RB(GS_NONLINEAR, false);
-        else GS_RB(GS_NEWTON, false);
-#undef GS_RB
-#undef GS_RBU
-    } else {
-        const dim3 g = plan.grid, b(GN_BX, GN_BY);
-#define GS_GN(M) hipLaunchKernelGGL((k_generic<M, KIND, ADD>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
-        if (mode == GS_LINEAR) GS_GN(GS_LINEAR);
-        else if (mode == GS_NONLINEAR) GS_GN(GS_NONLINEAR);
-        else GS_GN(GS_NEWTON);
-#undef GS_GN
-    }
-    return launch_status();
-}
-
-// ---- tuning variants of the LINEAR sweep (tools/kbench.py) -------------------------------------
-using RbKernel = void (*)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
-                          int64_t, int);
-struct Variant {
-    const char* name;
-    int ry, wy, zc;
-    bool oneD;
-    RbKernel kern;
-};
-#define GS_VX(RY, W, ZC, NT, X, NTV, TAG) \
-    {"rb ry" #RY " w" #W " zc" #ZC " " TAG, RY, W, ZC, X, k_rb<GS_LINEAR, 0, false, RY, W, true, NT, X, NTV>}
-const Variant kVariants[] = {
-    GS_VX(2, 4, 32, true, false, false, "dpp nt (production shape)"),
-    GS_VX(2, 4, 32, false, false, false, "dpp"),
-    GS_VX(2, 4, 32, true, true, false, "dpp nt xcd"),
-    GS_VX(2, 4, 32, true, false, true, "dpp nt ntv"),
-    GS_VX(2, 4, 16, true, false, false, "dpp nt"),
-    GS_VX(2, 4, 64, true, false, false, "dpp nt"),
-    GS_VX(2, 8, 32, true, false, false, "dpp nt"),
-    GS_VX(2, 2, 32, true, false, false, "dpp nt"),
-    GS_VX(1, 8, 32, true, false, false, "dpp nt"),
-    GS_VX(4, 4, 32, true, false, false, "dpp nt"),
-    GS_VX(4, 2, 32, true, false, false, "dpp nt"),
-    GS_VX(8, 2, 32, true, false, false, "dpp nt"),
-};
-#undef GS_VX
-constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-
-// Bandwidth ceilings. KIND 0 read a, 1 write out, 2 copy a->out, 3 triad out = a + 0.8 b.
-// UNROLL independent dwordx4 per thread per iteration, NT non-temporal loads/stores.
-template <int KIND, int UNROLL, bool NT>
-__global__ __launch_bounds__(256) void k_bw(double* __restrict__ out, const double* __restrict__ a,
-                                            const double* __restrict__ b, int64_t n2, double* __restrict__ sink)
-{
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    double acc = 0.0;
-    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n2; i0 += stride * UNROLL) {
-        double2 va[UNROLL], vb[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) {
-            const int64_t i = i0 + u * stride;
-            if (i < n2) {
-                if (KIND != 1) va[u] = ld2s<NT>(a + 2 * i);
-                if (KIND == 3) vb[u] = ld2s<NT>(b + 2 * i);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) {
-            const int64_t i = i0 + u * stride;
-            if (i >= n2) continue;
-            if (KIND == 0) acc += va[u].x + va[u].y;
-            else if (KIND == 1) st2s<NT>(out + 2 * i, 1.0, 2.0);
-            else if (KIND == 2) st2s<NT>(out + 2 * i, va[u].x, va[u].y);
-            else st2s<NT>(out + 2 * i, va[u].x + 0.8 * vb[u].x, va[u].y + 0.8 * vb[u].y);
-        }
-    }
-    if (KIND == 0 && acc == -1.2345e300) *sink = acc; // keeps the loads alive
-}
-
-// A copy with the resource footprint of RCCL's gfx950 transport kernels (ncclDevKernel_Generic: 256
-// VGPRs, 37664 B of LDS per 256-thread workgroup): the clobber of v255 makes the allocator reserve
-// every VGPR. Stands in for the ghost exchange in tools/exchange_probe.py (when does a workgroup
-// that needs a whole SIMD's registers get a CU while the interior pair holds the GPU?).
-__global__ __launch_bounds__(256) void k_fatcopy(double* __restrict__ out, const double* __restrict__ a, int64_t n2)
-{
-    __shared__ double pad[4708];
-    asm volatile("" ::: "v255");
-    for (int i = threadIdx.x; i < 4708; i += 256) pad[i] = 0.0;
-    __syncthreads();
-    const double z = pad[(threadIdx.x * 17) % 4708];
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
-        const double2 x = ld2s<true>(a + 2 * i);
-        st2s<true>(out + 2 * i, x.x + z, x.y + z);
-    }
-}
-
-// One wave that sleeps `iters` x s_sleep(127) (~3.4 us each at 2.4 GHz) and touches no memory: a delay
-// on a stream, e.g. between the boundary planes and the interior launch of an overlapped Z-slab sweep
-// so that the exchange's kernels are dispatched first (tools/exchange_probe.py).
-__global__ __launch_bounds__(64) void k_sleep(int64_t iters)
-{
-    for (int64_t i = 0; i < iters; i++) __builtin_amdgcn_s_sleep(127);
-}
-
-// div_hh against the plain division (tests: bitwise equality over all magnitudes)
-__global__ __launch_bounds__(256) void k_div_check(const double* __restrict__ a, int64_t n, Coef k,
-                                                   double* __restrict__ fast, double* __restrict__ ref)
-{
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fast[i] = div_hh(k, a[i]);
-    ref[i] = a[i] / k.hh;
-}
-
-__global__ __launch_bounds__(256) void k_triad(double* __restrict__ out, const double* __restrict__ a,
-                                               const double* __restrict__ b, int64_t n2)
-{
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
-        const double2 x = reinterpret_cast<const double2*>(a)[i], y = reinterpret_cast<const double2*>(b)[i];
-        reinterpret_cast<double2*>(out)[i] = make_double2(x.x + 0.8 * y.x, x.y + 0.8 * y.y);
-    }
-}
-
-} // namespace
+// gs_kernels.hip — the product library libgpusolve_hip.so: the extern "C" launchers declared in
+// include/gpusolve_hip.h over the gfx950 kernels of gs_device.hpp. Diagnostics (tuning variants,
+// bandwidth probes, the rejected k_prr) live in gs_diag.hip -> libgpusolve_diag.so.
+#include "gs_device.hpp"
 
 // =============================================================================================
 extern "C" {
@@ -2890,53 +213,6 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     return launch_status();
 }
 
-// k_prr geometry: the whole row in one block (<= 512 points), 4-row tiles, chunks of coarse planes for
-// ~512 blocks (one 8-wave block per CU, two rounds at 512^3; 4..64 coarse planes: the chunk ends
-// recompute five planes of the pipeline)
-static bool prr_plan(const gs_stencil* S, const gs_level* fl, const gs_level* cl, int mode, int* zc, dim3* g, dim3* b)
-{
-    if (!S || !valid_stencil(S) || !canonical_order(S) || mode != GS_LINEAR || bad_level(fl) || bad_level(cl) ||
-        !make_coef(S, fl, 0.0, 0.0).unit || // the unit-neighbour stencil sum (the general one spills here)
-        fl->z0 != 0 || cl->z0 != 0 || fl->nx < 1 || fl->nx > WAVE * PRR_WX || fl->ny < 1 || fl->nz < 2 ||
-        cl->nx != fl->nx / 2 || cl->ny != fl->ny / 2 || cl->nz != fl->nz / 2 || cl->nx < 1 || cl->ny < 1)
-        return false;
-    const int64_t tiles = (fl->ny + PRR_T - 1) / PRR_T;
-    int64_t c = (cl->nz * tiles + 511) / 512;
-    c = c < 4 ? 4 : (c > 64 ? 64 : c);
-    *zc = (int)c;
-    *g = dim3((unsigned)tiles, (unsigned)((cl->nz + c - 1) / c));
-    *b = dim3(WAVE, (unsigned)((fl->nx + WAVE - 1) / WAVE));
-    return true;
-}
-
-int gs_jacobi_sweep2_restrict_supported(const gs_stencil* S, const gs_level* fl, const gs_level* cl, int mode)
-{
-    int zc;
-    dim3 g, b;
-    return prr_plan(S, fl, cl, mode, &zc, &g, &b) ? 1 : 0;
-}
-
-int64_t gs_jacobi_sweep2_restrict_num_partials(const gs_stencil* S, const gs_level* fl, const gs_level* cl)
-{
-    int zc;
-    dim3 g, b;
-    return prr_plan(S, fl, cl, GS_LINEAR, &zc, &g, &b) ? (int64_t)g.x * g.y : 0;
-}
-
-int gs_jacobi_sweep2_restrict(const gs_stencil* S, const gs_level* fl, double omega, const double* v_in,
-                              double* v_out, const double* f, double* partials, double* ca, double* cb,
-                              const gs_level* cl, hipStream_t st)
-{
-    int zc;
-    dim3 g, b;
-    if (!prr_plan(S, fl, cl, GS_LINEAR, &zc, &g, &b) || !v_in || !v_out || !f || !ca || v_in == v_out)
-        return GS_EINVAL;
-    const Coef k = make_coef(S, fl, omega, 0.0);
-    hipLaunchKernelGGL((k_prr<true>), g, b, 0, st, k, v_in, f, v_out, partials, ca, cb, (int)fl->nx, (int)fl->ny,
-                       (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, zc);
-    return launch_status();
-}
-
 int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L)
 {
     if (!S || !L) return 0;
@@ -2983,7 +259,7 @@ int gs_residual_restrict(const gs_stencil* S, const gs_level* fl, int mode, doub
 
 int gs_residual_restrict_slab_supported(const gs_stencil* S, const gs_level* fl)
 {
-    static const bool ldsOnly = getenv("GS_RR_LDS") != nullptr;
+    const bool ldsOnly = kKnobs.rrLds;
     return S && fl && !bad_level(fl) && valid_stencil(S) && canonical_order(S) && !ldsOnly &&
            ((fl->nx + 1) / 2 + WAVE - 1) / WAVE <= RR2_WXMAX;
 }
@@ -3004,7 +280,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         return GS_EINVAL;
     const Coef k = make_coef(S, fl, 0.0, gamma);
     const int64_t wxs = ((fl->nx + 1) / 2 + WAVE - 1) / WAVE; // x-waves covering coarse columns 1..(fnx+1)/2
-    static const bool ldsOnly = getenv("GS_RR_LDS") != nullptr;   // A/B switch for tools/ measurements
+    const bool ldsOnly = kKnobs.rrLds; // A/B switch for tools/ measurements
     const bool rr2 = !ldsOnly && canonical_order(S) && zoff == 0 && wxs <= RR2_WXMAX;
     if (zhi && !rr2) return GS_EINVAL; // the slab form exists for the register kernel only
     if (rr2) {
@@ -3012,7 +288,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         // LINEAR levels of >= 2^26 points: two coarse rows per block (231 VGPRs, 2 waves per SIMD): 0.507 vs
         // 0.529 ms at 512^3, but 0.072 vs 0.068 ms at 256^3 (gpurun_out/rrnr2, tools/rr_ab.py);
         // NONLINEAR / NEWTON: one row (VGPR budget). GS_RR_NR=1|2 forces the choice (A/B, tests).
-        static const int nr_env = getenv("GS_RR_NR") ? std::atoi(getenv("GS_RR_NR")) : 0;
+        const int nr_env = kKnobs.rrNr;
         const bool big = fl->nx * fl->ny * fl->nz >= ((int64_t)1 << RR2_NR2_LOG2_POINTS);
         // (NEWTON with two rows spills 19 VGPRs: 40.5 vs 38.9 ms per 512^3 Newton iteration, gpurun_out/rrn)
         const int nr = mode == GS_LINEAR && (nr_env == 2 || (nr_env == 0 && big)) ? 2 : 1;
@@ -3025,7 +301,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
         // two-row blocks: the rows no neighbouring block reads are non-temporal loads (0.490 vs 0.505 ms at
         // 512^3, r02 tools/rr_ab_session.sh rrntu); GS_RR_NTU=0 keeps them cached (A/B)
-        static const int ntu_env = getenv("GS_RR_NTU") ? atoi(getenv("GS_RR_NTU")) : 1;
+        const int ntu_env = kKnobs.rrNtu;
         const bool ntu = ntu_env == 2 || (ntu_env == 1 && nr == 2);
 #define GS_RR2V(M, N, U, T) hipLaunchKernelGGL((k_rr2<M, false, N, U, T>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
 #define GS_RR2U(M, N, U) do { if (ntu) GS_RR2V(M, N, U, true); else GS_RR2V(M, N, U, false); } while (0)
@@ -3180,122 +456,6 @@ const char* gs_build_info(void)
            "rounds) / k_tb2 (NEWTON rows > 512), sweeps k_rb(ry2 w4 zc<=32 dpp nt), fused residual+restriction "
            "(2 coarse rows per block from 2^26 points), unit-neighbour stencil sums, 1-pt/thread small levels, "
            "one-workgroup coarse cycle; fp-contract=off";
-}
-
-int gs_debug_num_variants(void) { return kNumVariants; }
-
-const char* gs_debug_variant_name(int variant)
-{
-    return (variant >= 0 && variant < kNumVariants) ? kVariants[variant].name : "";
-}
-
-int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
-                           double* v_out, const double* f, hipStream_t st)
-{
-    if (variant < 0 || variant >= kNumVariants || !S || bad_level(L) || !canonical_order(S) || !v_in || !v_out ||
-        !f || v_in == v_out)
-        return GS_EINVAL;
-    if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
-    const Variant& V = kVariants[variant];
-    const Coef k = make_coef(S, L, omega, 0.0);
-    hipLaunchKernelGGL(V.kern, rb_grid(L, V.ry, V.wy, V.zc, V.oneD), dim3(WAVE, V.wy), 0, st, k, v_in, f, nullptr,
-                       v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, V.zc);
-    return launch_status();
-}
-
-// Fused-pair shapes for tools/kbench.py --pairs (LINEAR): output rows per wave x max waves per
-// block (the launch bound, hence the VGPR budget: 4 waves -> 512, 8 waves -> 256 per lane).
-struct PairVariant {
-    const char* name;
-    int ry, wxmax, wy;
-    void (*kern)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
-                 int64_t, int, int, int, const double*, const double*, int, int, int, int64_t, int64_t, const double*);
-};
-#define GS_PV(RY, WX) {"tb2 ry" #RY " wx" #WX, RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true>}
-#define GS_PVF(RY, WX) {"tb2 ry" #RY " wx" #WX " f-cached", RY, WX, 1, k_tb2<GS_LINEAR, RY, WX, true, false>}
-#define GS_PVY(RY, NTF, SPEC, TAG) {"tb2y ry" #RY " wx4 wy2" TAG, RY, 4, 2, k_tb2y<GS_LINEAR, RY, 4, true, NTF, false, SPEC>}
-const PairVariant kPairVariants[] = {GS_PVF(2, 4),
-                                     GS_PVF(2, 8),
-                                     GS_PV(2, 4),
-                                     GS_PVY(2, false, false, " f-cached"),
-                                     GS_PVY(3, false, false, " f-cached"),
-                                     GS_PVY(2, false, true, " f-cached spec"),
-                                     GS_PVY(3, false, true, " f-cached spec"),
-                                     GS_PVY(3, true, false, " f-nt"),
-                                     {"tb2y ry2 wx4 wy2 f-cached spec pfd2", 2, 4, 2,
-                                      k_tb2y<GS_LINEAR, 2, 4, true, false, false, true, 0, 2>}};
-#undef GS_PVY
-#undef GS_PVF
-#undef GS_PV
-constexpr int kNumPairVariants = (int)(sizeof(kPairVariants) / sizeof(kPairVariants[0]));
-
-int gs_debug_num_pair_variants(void) { return kNumPairVariants; }
-const char* gs_debug_pair_variant_name(int variant)
-{
-    return (variant >= 0 && variant < kNumPairVariants) ? kPairVariants[variant].name : "";
-}
-
-int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
-                          double* v_out, const double* f, int zc, hipStream_t st)
-{
-    if (variant < 0 || variant >= kNumPairVariants || !S || bad_level(L) || !canonical_order(S) || !v_in ||
-        !v_out || !f || v_in == v_out || zc < 0)
-        return GS_EINVAL;
-    const PairVariant& V = kPairVariants[variant];
-    const int64_t wx = (L->nx + 2 * WAVE - 1) / (2 * WAVE);
-    if (L->nx < 1 || L->ny < 1 || L->nz < 1 || wx > V.wxmax) return GS_EINVAL;
-    const int64_t tiles = (L->ny + V.ry * V.wy - 1) / (V.ry * V.wy);
-    if (zc == 0) {
-        int64_t c = tiles * L->nz / 1024;
-        zc = (int)(c < 4 ? 4 : (c > 32 ? 32 : c));
-    }
-    const Coef k = make_coef(S, L, omega, 0.0);
-    hipLaunchKernelGGL(V.kern, dim3((unsigned)tiles, (unsigned)((L->nz + zc - 1) / zc)), dim3(WAVE, (unsigned)wx, V.wy), 0,
-                       st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc,
-                       0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0, nullptr);
-    return launch_status();
-}
-
-int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
-                double* sink, hipStream_t st)
-{
-    if (kind == 5) { // k_sleep: n iterations of s_sleep(127), one wave
-        if (n < 0) return GS_EINVAL;
-        hipLaunchKernelGGL(k_sleep, dim3(1), dim3(64), 0, st, n);
-        return launch_status();
-    }
-    if (n < 0 || (n & 1) || kind < 0 || kind > 4 || blocks <= 0) return GS_EINVAL;
-    if (kind == 4) { // copy at RCCL's transport-kernel footprint (k_fatcopy)
-        hipLaunchKernelGGL(k_fatcopy, dim3(blocks), dim3(256), 0, st, out, a, n / 2);
-        return launch_status();
-    }
-    using K = void (*)(double*, const double*, const double*, int64_t, double*);
-    static const K tab[4][2][2] = {
-        {{k_bw<0, 1, false>, k_bw<0, 1, true>}, {k_bw<0, 4, false>, k_bw<0, 4, true>}},
-        {{k_bw<1, 1, false>, k_bw<1, 1, true>}, {k_bw<1, 4, false>, k_bw<1, 4, true>}},
-        {{k_bw<2, 1, false>, k_bw<2, 1, true>}, {k_bw<2, 4, false>, k_bw<2, 4, true>}},
-        {{k_bw<3, 1, false>, k_bw<3, 1, true>}, {k_bw<3, 4, false>, k_bw<3, 4, true>}},
-    };
-    hipLaunchKernelGGL(tab[kind][unroll > 1][nt != 0], dim3(blocks), dim3(256), 0, st, out, a, b, n / 2, sink);
-    return launch_status();
-}
-
-int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, double* ref, hipStream_t st)
-{
-    if (!a || !fast || !ref || n < 0) return GS_EINVAL;
-    if (n == 0) return 0;
-    Coef k{};
-    k.hh = hh;
-    k.fastdiv = hh >= 0x1p-120 && hh <= 1.0;
-    hipLaunchKernelGGL(k_div_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, n, k, fast, ref);
-    return launch_status();
-}
-
-int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t n, hipStream_t st)
-{
-    if (!out || !a || !b || n < 0 || (n & 1)) return GS_EINVAL;
-    hipLaunchKernelGGL(k_triad, dim3(4096), dim3(256), 0, st, out, a, b, n / 2);
-    return launch_status();
 }
 
 } // extern "C"

@@ -1,4 +1,5 @@
-"""ctypes declarations of the two C ABIs (include/gpusolve_hip.h, include/gpusolve_driver.h).
+"""ctypes declarations of the C ABIs (include/gpusolve_hip.h, include/gpusolve_driver.h, and the
+diagnostics library's include/gpusolve_diag.h, which only tools/ and tests/ load).
 
 The shared libraries are built in-tree by gpu-solve_amd/Makefile (``__graft_entry__.build()``).
 There is no fallback: if a library is missing, loading raises ``ImportError`` naming the build step.
@@ -10,6 +11,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # gpu-so
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
 BIN_DIR = os.path.join(PKG_ROOT, "bin")
 KERNEL_LIB = os.path.join(LIB_DIR, "libgpusolve_hip.so")
+DIAG_LIB = os.path.join(LIB_DIR, "libgpusolve_diag.so")  # tools/ and tests/ only (include/gpusolve_diag.h)
 DRIVER_LIB = os.path.join(LIB_DIR, "libgpusolve_driver.so")
 EXECUTABLE = os.path.join(BIN_DIR, "GpuSolve-hip")
 
@@ -64,12 +66,6 @@ KERNEL_API = {
                                               C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(gs_level),
                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, i64,
                                               C.c_void_p]),
-    "gs_jacobi_sweep2_restrict_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level),
-                                                      C.POINTER(gs_level), C.c_int]),
-    "gs_jacobi_sweep2_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
-                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                            C.POINTER(gs_level), C.c_void_p]),
-    "gs_jacobi_sweep2_restrict_num_partials": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.POINTER(gs_level)]),
     "gs_residual": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double, C.c_void_p,
                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_residual_num_partials": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),
@@ -98,18 +94,6 @@ KERNEL_API = {
     "gs_coarse_cycle": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_coarse_level), C.c_int, C.c_int, C.c_double,
                                   C.c_double, C.c_int, C.c_int, C.c_void_p]),
     "gs_strerror": (C.c_char_p, [C.c_int]),
-    "gs_debug_num_variants": (C.c_int, []),
-    "gs_debug_variant_name": (C.c_char_p, [C.c_int]),
-    "gs_debug_sweep_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double,
-                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
-    "gs_debug_div_check": (C.c_int, [C.c_void_p, i64, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
-    "gs_debug_num_pair_variants": (C.c_int, []),
-    "gs_debug_pair_variant_name": (C.c_char_p, [C.c_int]),
-    "gs_debug_pair_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
-                                        C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
-    "gs_debug_stream_triad": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p]),
-    "gs_debug_bw": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p,
-                              C.c_void_p]),
     "gs_build_info": (C.c_char_p, []),
 }
 
@@ -150,6 +134,28 @@ DRIVER_API = {
     "gs_last_error": (C.c_char_p, []),
 }
 
+# libgpusolve_diag.so (include/gpusolve_diag.h): tuning variants, bandwidth probes, k_prr — not the product
+DIAG_API = {
+    "gs_jacobi_sweep2_restrict_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level),
+                                                      C.POINTER(gs_level), C.c_int]),
+    "gs_jacobi_sweep2_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.POINTER(gs_level), C.c_void_p]),
+    "gs_jacobi_sweep2_restrict_num_partials": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.POINTER(gs_level)]),
+    "gs_debug_num_variants": (C.c_int, []),
+    "gs_debug_variant_name": (C.c_char_p, [C.c_int]),
+    "gs_debug_sweep_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gs_debug_div_check": (C.c_int, [C.c_void_p, i64, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gs_debug_num_pair_variants": (C.c_int, []),
+    "gs_debug_pair_variant_name": (C.c_char_p, [C.c_int]),
+    "gs_debug_pair_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    "gs_debug_stream_triad": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p]),
+    "gs_debug_bw": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p,
+                              C.c_void_p]),
+}
+
 _cache = {}
 
 
@@ -170,6 +176,12 @@ def _load(path, api):
 def kernels():
     """The thin C-ABI launcher library (libgpusolve_hip.so)."""
     return _load(KERNEL_LIB, KERNEL_API)
+
+
+def diag():
+    """The diagnostics library (libgpusolve_diag.so): measurement and tuning code, never the product path."""
+    kernels()
+    return _load(DIAG_LIB, DIAG_API)
 
 
 def driver():

@@ -135,19 +135,6 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
                                 const double* v_in, const double* coarse_v, const double* coarse_sub,
                                 const gs_level* coarse, double* v_out, const double* f, const double* w, int zlo,
                                 int zhi, double* ws, int64_t ws_elems, hipStream_t stream);
-/* The first pre-smoothing pair of a 2-sweep pre-smoothing, the residual of its result and the full
- * weighting in one pass: v_out = S(S(v_in)), coarse_a (and coarse_b if not NULL) = R(f - A(v_out)) on
- * the coarse interior, partials (may be NULL) = gs_jacobi_sweep2_restrict_num_partials per-block sums
- * of r^2 of f - A(v_in). Bit-identical to gs_jacobi_sweep2 followed by gs_residual_restrict (the norm
- * in this kernel's block order). Replaces CpuSolver.cpp:94-99 (jacobi(pre = 2), compResidual,
- * restrict). Supported (gs_jacobi_sweep2_restrict_supported != 0) for LINEAR levels with the unit
- * 7-point stencil (canonical order, neighbour weights -1, |s0| >= 1), rows <= 512 points, z0 = 0, and
- * coarse = fine / 2 per axis; GS_EINVAL otherwise. */
-int gs_jacobi_sweep2_restrict_supported(const gs_stencil* S, const gs_level* fine, const gs_level* coarse, int mode);
-int gs_jacobi_sweep2_restrict(const gs_stencil* S, const gs_level* fine, double omega, const double* v_in,
-                              double* v_out, const double* f, double* partials, double* coarse_a, double* coarse_b,
-                              const gs_level* coarse, hipStream_t stream);
-int64_t gs_jacobi_sweep2_restrict_num_partials(const gs_stencil* S, const gs_level* fine, const gs_level* coarse);
 /* Which fused-pair kernel (and shape) gs_jacobi_sweep2 launches for this level and mode ("" if none). */
 const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int mode);
 
@@ -230,29 +217,7 @@ int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int m
 
 const char* gs_strerror(int code);
 
-/* ---- tuning / diagnostics (tools/kbench.py) ----
- * Alternative tilings of the LINEAR fused sweep (bit-identical results), and a streaming
- * out = a + 0.8*b kernel (24 B per element, the smoother's byte pattern) for the achievable
- * HBM ceiling. n must be even and the arrays 16-B aligned. */
-int gs_debug_num_variants(void);
-const char* gs_debug_variant_name(int variant);
-int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
-                           double* v_out, const double* f, hipStream_t stream);
-/* fast[i] = the kernels' a[i] / hh (3-operation path where it applies), ref[i] = plain division. */
-int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, double* ref, hipStream_t stream);
-/* Fused-pair shape variants (LINEAR, level boundaries on both z sides; zc = 0: default chunk). */
-int gs_debug_num_pair_variants(void);
-const char* gs_debug_pair_variant_name(int variant);
-int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, double omega, const double* v_in,
-                          double* v_out, const double* f, int zc, hipStream_t stream);
-int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t n, hipStream_t stream);
-/* Streaming ceilings: kind 0 read a, 1 write out, 2 copy, 3 triad; unroll 1 or 4 dwordx4 per thread,
- * nt = non-temporal, `blocks` workgroups of 256 threads (grid-stride). Kind 4: a non-temporal copy
- * at the resource footprint of RCCL's transport kernels (256 VGPRs, 37 KB of LDS per workgroup;
- * unroll / nt ignored), the stand-in exchange of tools/exchange_probe.py. Kind 5: one wave that sleeps n x
- * s_sleep(127) (~3.4 us each), touching no memory (out / a / b / blocks ignored). */
-int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
-                double* sink, hipStream_t stream);
+/* (tuning variants, bandwidth probes and the rejected k_prr: include/gpusolve_diag.h) */
 /* Library build tag (kernel variant names), for logs. */
 const char* gs_build_info(void);
 

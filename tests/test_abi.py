@@ -14,6 +14,7 @@ from conftest import REPO
 HEADERS = {
     os.path.join(REPO, "include", "gpusolve_hip.h"): gsv._abi.KERNEL_LIB,
     os.path.join(REPO, "include", "gpusolve_driver.h"): gsv._abi.DRIVER_LIB,
+    os.path.join(REPO, "include", "gpusolve_diag.h"): gsv._abi.DIAG_LIB,
 }
 DECL = re.compile(r"^[A-Za-z_][\w \t\*]*?\b(gs_\w+)\s*\(", re.M)
 
@@ -39,9 +40,40 @@ def test_every_declared_symbol_is_exported(header):
     assert not missing, missing
 
 
+def test_product_library_exports_exactly_its_header():
+    """libgpusolve_hip.so exports include/gpusolve_hip.h's entry points and nothing else: the tuning
+    variants, bandwidth probes and k_prr live in libgpusolve_diag.so (include/gpusolve_diag.h)."""
+    names = set(declared(os.path.join(REPO, "include", "gpusolve_hip.h")))
+    got = {n for n in exported(gsv._abi.KERNEL_LIB) if n.startswith("gs_")}
+    assert got == names, got ^ names
+    diag = set(declared(os.path.join(REPO, "include", "gpusolve_diag.h")))
+    assert not (diag & names)
+    assert {n for n in exported(gsv._abi.DIAG_LIB) if n.startswith("gs_")} == diag
+
+
+def test_product_sources_read_no_environment_on_launch():
+    """No getenv in the launchers or the device code (the A/B switches are read once at load time, into
+    gs_device.hpp's Knobs; the driver's at grid creation), and no timing-only build macros."""
+    csrc = os.path.join(REPO, "gpu-solve_amd", "csrc")
+    kern = open(os.path.join(csrc, "gs_kernels.hip")).read()
+    dev = open(os.path.join(csrc, "gs_device.hpp")).read()
+    assert "getenv" not in kern
+    body = dev[dev.index("struct Knobs"):]
+    body = body[body.index("const Knobs kKnobs;"):]
+    assert "getenv" not in body
+    assert "GS_PRO_EXP" not in dev + kern and "GS_PRO_HALF" not in dev + kern
+    grid = open(os.path.join(csrc, "gs_grid.cpp")).read()
+    ctor_end = grid.index("HipGridData::~HipGridData()")
+    # after the constructor only trace mode's stop switch (no device) reads the environment
+    assert [l.strip() for l in grid[ctor_end:].splitlines() if "getenv" in l] == [
+        'const char* e = std::getenv("GS_TRACE_STOP_AFTER"); // read per call: tests switch it']
+
+
 def test_python_binding_covers_headers():
     names = set(declared(os.path.join(REPO, "include", "gpusolve_hip.h")))
     assert names == set(gsv._abi.KERNEL_API), names ^ set(gsv._abi.KERNEL_API)
+    names = set(declared(os.path.join(REPO, "include", "gpusolve_diag.h")))
+    assert names == set(gsv._abi.DIAG_API), names ^ set(gsv._abi.DIAG_API)
     names = set(declared(os.path.join(REPO, "include", "gpusolve_driver.h")))
     assert names == set(gsv._abi.DRIVER_API), names ^ set(gsv._abi.DRIVER_API)
 

@@ -28,7 +28,7 @@ def test_div_hh_bitwise(n):
     a = numerators(rng)
     d = torch.from_numpy(a).cuda()
     fast, ref = torch.empty_like(d), torch.empty_like(d)
-    rc = gsv.kernels().gs_debug_div_check(d.data_ptr(), d.numel(), hh, fast.data_ptr(), ref.data_ptr(),
+    rc = gsv.diag().gs_debug_div_check(d.data_ptr(), d.numel(), hh, fast.data_ptr(), ref.data_ptr(),
                                          torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()

@@ -54,9 +54,9 @@ def test_pair_restrict_equals_pair_then_restrict(shape):
     cn = (nx // 2, ny // 2, nz // 2)
     c1, c2, c2b = DevField(*cn, fill=-7.0), DevField(*cn, fill=-7.0), DevField(*cn, fill=-7.0)
     L, CL = v.level(h), c1.level(2 * h)
-    assert k().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(L), C.byref(CL), 0) == 1
+    assert gsv.diag().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(L), C.byref(CL), 0) == 1
     n1 = k().gs_jacobi_sweep2_num_partials(C.byref(S), C.byref(L), 0)
-    n2 = k().gs_jacobi_sweep2_restrict_num_partials(C.byref(S), C.byref(L), C.byref(CL))
+    n2 = gsv.diag().gs_jacobi_sweep2_restrict_num_partials(C.byref(S), C.byref(L), C.byref(CL))
     assert n1 > 0 and n2 > 0
     p1 = torch.zeros(n1, dtype=torch.float64, device="cuda")
     p2 = torch.zeros(n2, dtype=torch.float64, device="cuda")
@@ -64,7 +64,7 @@ def test_pair_restrict_equals_pair_then_restrict(shape):
                                  p1.data_ptr(), st()))
     ok(k().gs_residual_restrict(C.byref(S), C.byref(L), 0, 1.0, out1.ptr, f.ptr, None, c1.ptr, None, C.byref(CL),
                                 st()))
-    ok(k().gs_jacobi_sweep2_restrict(C.byref(S), C.byref(L), 0.8, v.ptr, out2.ptr, f.ptr, p2.data_ptr(), c2.ptr,
+    ok(gsv.diag().gs_jacobi_sweep2_restrict(C.byref(S), C.byref(L), 0.8, v.ptr, out2.ptr, f.ptr, p2.data_ptr(), c2.ptr,
                                      c2b.ptr, C.byref(CL), st()))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out2.to_xyz(), out1.to_xyz())
@@ -78,13 +78,13 @@ def test_pair_restrict_supported_cases():
     S = gsv.Stencil().to_abi()
     v, c = DevField(64, 16, 16), DevField(32, 8, 8)
     L, CL = v.level(1.0 / 17), c.level(2.0 / 17)
-    assert k().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(L), C.byref(CL), 0) == 1
+    assert gsv.diag().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(L), C.byref(CL), 0) == 1
     for mode in (1, 2):  # LINEAR only
-        assert k().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(L), C.byref(CL), mode) == 0
+        assert gsv.diag().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(L), C.byref(CL), mode) == 0
     wide, cw = DevField(513, 4, 4), DevField(256, 2, 2)  # rows > 512 points
-    assert k().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(wide.level(0.2)), C.byref(cw.level(0.4)), 0) == 0
+    assert gsv.diag().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(wide.level(0.2)), C.byref(cw.level(0.4)), 0) == 0
     other = DevField(32, 8, 9)  # coarse not fine / 2
-    assert k().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(L), C.byref(other.level(0.1)), 0) == 0
+    assert gsv.diag().gs_jacobi_sweep2_restrict_supported(C.byref(S), C.byref(L), C.byref(other.level(0.1)), 0) == 0
     gen = gsv.Stencil()
     gen.values = [6.5, -1, -1, -1, -1, -1, -1.5]  # not the unit-neighbour stencil
-    assert k().gs_jacobi_sweep2_restrict_supported(C.byref(gen.to_abi()), C.byref(L), C.byref(CL), 0) == 0
+    assert gsv.diag().gs_jacobi_sweep2_restrict_supported(C.byref(gen.to_abi()), C.byref(L), C.byref(CL), 0) == 0

@@ -56,6 +56,7 @@ def main():
     import gpusolve as gsv
     from gpusolve.devfield import DevField
     k = gsv.kernels()
+    kd = gsv.diag()
     hip = C.CDLL("libamdhip64.so")
     v, o, f = DevField(NX, NY, NZ, fill=0.5), DevField(NX, NY, NZ), DevField(NX, NY, NZ, fill=1.0)
     S = gsv.Stencil().to_abi()
@@ -111,7 +112,7 @@ def main():
             bnd_s.wait_stream(bnd2_s)
         if blocks:
             comm_s.wait_stream(bnd_s)
-            assert k.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
+            assert kd.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
                                  comm_s.cuda_stream) == 0
         if ist is not main_s:
             ist.wait_event(ev)
@@ -119,7 +120,7 @@ def main():
             ist.wait_stream(bnd_s)
         if delay:  # the interior waits for the boundary planes, then a sleeping wave on its own stream
             ist.wait_stream(bnd_s)
-            assert k.gs_debug_bw(5, 1, 1, 1, None, None, None, delay, None, ist.cuda_stream) == 0
+            assert kd.gs_debug_bw(5, 1, 1, 1, None, None, None, delay, None, ist.cuda_stream) == 0
         pair(3, NZ - 2, ist)
         if ist is not main_s:
             main_s.wait_stream(ist)
@@ -146,7 +147,7 @@ def main():
                 main_s.wait_event(evb[(k_ - 1) & 1])
             pair(3, NZ - 2, main_s)
             if blocks:
-                assert k.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
+                assert kd.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
                                      comm_s.cuda_stream) == 0
             ev_x = torch.cuda.Event()
             ev_x.record(comm_s)
@@ -170,30 +171,18 @@ def main():
         settings += [("first-mask", b, "0") for b in (0, 8, 32)]
     for _ in range(2):
         for v_, b, zc in settings:
-            os.environ["GS_SLAB_ZC"] = zc
             step2(v_, b)
     torch.cuda.synchronize()
     for v_, b, zc in settings:
-        os.environ["GS_SLAB_ZC"] = zc
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(main_s)
         for _ in range(reps):
             step2(v_, b)
         e1.record(main_s)
         torch.cuda.synchronize()
-        res[f"{v_} interior_zc={zc} exchange={'fat x%d' % b if b else 'none'}"] = round(e0.elapsed_time(e1) / reps, 4)
-    os.environ["GS_SLAB_ZC"] = "0"
-    # interior alone: unmasked / masked; chunk lengths
-    for zc in ("32",):
-        os.environ["GS_SLAB_ZC"] = zc
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(main_s)
-        for _ in range(reps):
-            pair(3, NZ - 2, main_s)
-        e1.record(main_s)
-        torch.cuda.synchronize()
-        res[f"interior alone, zc={zc}"] = round(e0.elapsed_time(e1) / reps, 4)
-    os.environ["GS_SLAB_ZC"] = "0"
+        res[f"{v_} interior_zc={os.environ.get('GS_SLAB_ZC', '0')} exchange={'fat x%d' % b if b else 'none'}"] = round(e0.elapsed_time(e1) / reps, 4)
+    # interior alone (unmasked / masked). The chunk length of the launches past a slab's first plane is
+    # GS_SLAB_ZC, read once when the library loads: run the probe under different values for an A/B
     for r in streams:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st = streams[r]

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--zc", type=str, default="0", help="fused-pair z-chunks to try (comma list, 0 = auto)")
     a = ap.parse_args()
     k = gsv.kernels()
+    kd = gsv.diag()
     nx = a.n
     ny = a.ny or a.n
     nz = a.nz or a.n
@@ -54,9 +55,9 @@ def main():
     inner.copy_(torch.rand(inner.shape, generator=g, device="cuda", dtype=torch.float64) * 1e-3)
     torch.cuda.synchronize()
 
-    nv = k.gs_debug_num_variants()
+    nv = kd.gs_debug_num_variants()
     variants = [int(x) for x in a.variants.split(",")] if a.variants else list(range(nv))
-    names = {i: k.gs_debug_variant_name(i).decode() for i in range(nv)}
+    names = {i: kd.gs_debug_variant_name(i).decode() for i in range(nv)}
 
     # reference output: production kernel (gs_jacobi_sweep)
     ref = DevField(nx, ny, nz)
@@ -68,7 +69,7 @@ def main():
         alt.zyx[:, :, :].zero_() if False else None
         # the sweep writes the interior only: give alt the same zero boundary
         alt.buf.zero_()
-        rc = k.gs_debug_sweep_variant(i, C.byref(S), C.byref(L), 0.8, v.ptr, alt.ptr, f.ptr, st)
+        rc = kd.gs_debug_sweep_variant(i, C.byref(S), C.byref(L), 0.8, v.ptr, alt.ptr, f.ptr, st)
         assert rc == 0, k.gs_strerror(rc)
         torch.cuda.synchronize()
         same = bool(torch.equal(alt.zyx[:, :, :nx + 2], ref.zyx[:, :, :nx + 2]))
@@ -80,11 +81,11 @@ def main():
         for i in variants:
             a_, b_ = v, alt
             for _ in range(2):
-                k.gs_debug_sweep_variant(i, C.byref(S), C.byref(L), 0.8, a_.ptr, b_.ptr, f.ptr, st)
+                kd.gs_debug_sweep_variant(i, C.byref(S), C.byref(L), 0.8, a_.ptr, b_.ptr, f.ptr, st)
                 a_, b_ = b_, a_
             ev[0].record()
             for _ in range(a.sweeps):
-                k.gs_debug_sweep_variant(i, C.byref(S), C.byref(L), 0.8, a_.ptr, b_.ptr, f.ptr, st)
+                kd.gs_debug_sweep_variant(i, C.byref(S), C.byref(L), 0.8, a_.ptr, b_.ptr, f.ptr, st)
                 a_, b_ = b_, a_
             ev[1].record()
             torch.cuda.synchronize()
@@ -105,14 +106,14 @@ def main():
         assert k.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, ref1.ptr, ref2.ptr, f.ptr, None, st) == 0
         torch.cuda.synchronize()
         pv = {}
-        cases = [("production", -1, 0)] + [(k.gs_debug_pair_variant_name(i).decode() + f" zc{zc}", i, int(zc))
-                                            for i in range(k.gs_debug_num_pair_variants())
+        cases = [("production", -1, 0)] + [(kd.gs_debug_pair_variant_name(i).decode() + f" zc{zc}", i, int(zc))
+                                            for i in range(kd.gs_debug_num_pair_variants())
                                             for zc in a.zc.split(",")]
 
         def launch(i, zc, src, dst):
             if i < 0:
                 return k.gs_jacobi_sweep2(C.byref(S), C.byref(L), 0, 0.8, 1.0, src.ptr, dst.ptr, f.ptr, None, 0, 0, st)
-            return k.gs_debug_pair_variant(i, C.byref(S), C.byref(L), 0.8, src.ptr, dst.ptr, f.ptr, zc, st)
+            return kd.gs_debug_pair_variant(i, C.byref(S), C.byref(L), 0.8, src.ptr, dst.ptr, f.ptr, zc, st)
         for name, i, zc in cases:
             alt.buf.zero_()
             rc = launch(i, zc, v, alt)
@@ -148,12 +149,12 @@ def main():
     B = torch.rand(n, dtype=torch.float64, device="cuda")
     O = torch.empty(n, dtype=torch.float64, device="cuda")
     for _ in range(3):
-        k.gs_debug_stream_triad(O.data_ptr(), A.data_ptr(), B.data_ptr(), n, st)
+        kd.gs_debug_stream_triad(O.data_ptr(), A.data_ptr(), B.data_ptr(), n, st)
     ts = []
     for _ in range(a.rounds):
         ev[0].record()
         for _ in range(a.sweeps):
-            k.gs_debug_stream_triad(O.data_ptr(), A.data_ptr(), B.data_ptr(), n, st)
+            kd.gs_debug_stream_triad(O.data_ptr(), A.data_ptr(), B.data_ptr(), n, st)
         ev[1].record()
         torch.cuda.synchronize()
         ts.append(ev[0].elapsed_time(ev[1]) / a.sweeps)
@@ -170,7 +171,7 @@ def main():
                 for nt in (0, 1):
                     for blocks in (1024, 2048, 4096, 8192, 16384):
                         def run():
-                            k.gs_debug_bw(kind, unroll, nt, blocks, O.data_ptr(), A.data_ptr(), B.data_ptr(), n,
+                            kd.gs_debug_bw(kind, unroll, nt, blocks, O.data_ptr(), A.data_ptr(), B.data_ptr(), n,
                                           sink.data_ptr(), st)
                         run()
                         ts = []

@@ -38,6 +38,7 @@ def main():
     import gpusolve as gsv
     from gpusolve.devfield import DevField
     k = gsv.kernels()
+    kd = gsv.diag()
     n = 512
     v, o, f = DevField(n, n, n, fill=0.5), DevField(n, n, n), DevField(n, n, n, fill=1.0)
     S = gsv.Stencil().to_abi()
@@ -55,7 +56,7 @@ def main():
             assert k.gs_jacobi_sweep2(C.byref(S), C.byref(L), 0, 0.8, 1.0, v.ptr, o.ptr, f.ptr, None, 0, 0,
                                       main_s.cuda_stream) == 0
             time.sleep(50e-6)
-            assert k.gs_debug_bw(2, 1, 1, 16, O.data_ptr(), A.data_ptr(), B.data_ptr(), m, sink.data_ptr(),
+            assert kd.gs_debug_bw(2, 1, 1, 16, O.data_ptr(), A.data_ptr(), B.data_ptr(), m, sink.data_ptr(),
                                  side.cuda_stream) == 0
             torch.cuda.synchronize()
     print("priority range", least, greatest)

@@ -25,6 +25,7 @@ def main():
     a = ap.parse_args()
     n = a.size
     kl = gsv.kernels()
+    kd = gsv.diag()
     p = gsv.GridParams(gridDim=(n, n, n))
     S = p.stencil.to_abi()
     v, v2, f, r = (DevField(n, n, n) for _ in range(4))
@@ -39,7 +40,7 @@ def main():
         if "single" in a.which:
             assert kl.gs_jacobi_sweep(C.byref(S), C.byref(L), 0, 0.8, 1.0, v.ptr, v2.ptr, f.ptr, None, st) == 0
         for i in filter(None, a.pair_variants.split(",")):
-            assert kl.gs_debug_pair_variant(int(i), C.byref(S), C.byref(L), 0.8, v.ptr, v2.ptr, f.ptr, a.zc, st) == 0
+            assert kd.gs_debug_pair_variant(int(i), C.byref(S), C.byref(L), 0.8, v.ptr, v2.ptr, f.ptr, a.zc, st) == 0
         if "rr" in a.which.split(","):
             c = DevField(n // 2, n // 2, n // 2)
             Lc = c.level(2.0 / (n + 1))

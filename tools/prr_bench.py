@@ -15,13 +15,14 @@ from gpusolve.devfield import DevField  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 k = gsv.kernels()
+kd = gsv.diag()
 S = gsv.Stencil().to_abi()
 h = 1.0 / (n + 1)
 v, f, out = DevField(n, n, n, fill=0.5), DevField(n, n, n, fill=1.0), DevField(n, n, n)
 c = DevField(n // 2, n // 2, n // 2)
 L, CL = v.level(h), c.level(2 * h)
 p1 = torch.zeros(k.gs_jacobi_sweep2_num_partials(C.byref(S), C.byref(L), 0), dtype=torch.float64, device="cuda")
-p2 = torch.zeros(k.gs_jacobi_sweep2_restrict_num_partials(C.byref(S), C.byref(L), C.byref(CL)), dtype=torch.float64,
+p2 = torch.zeros(kd.gs_jacobi_sweep2_restrict_num_partials(C.byref(S), C.byref(L), C.byref(CL)), dtype=torch.float64,
                  device="cuda")
 st = torch.cuda.current_stream()
 
@@ -34,7 +35,7 @@ def two():
 
 
 def fused():
-    assert k.gs_jacobi_sweep2_restrict(C.byref(S), C.byref(L), 0.8, v.ptr, out.ptr, f.ptr, p2.data_ptr(), c.ptr,
+    assert kd.gs_jacobi_sweep2_restrict(C.byref(S), C.byref(L), 0.8, v.ptr, out.ptr, f.ptr, p2.data_ptr(), c.ptr,
                                        None, C.byref(CL), st.cuda_stream) == 0
 
 
