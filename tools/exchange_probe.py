@@ -164,9 +164,11 @@ def main():
         pipe_steps(b, reps)
         e1.record(main_s)
         torch.cuda.synchronize()
-        res[f"pipelined x{reps} exchange={'fat x%d' % b if b else 'none'}"] = round(e0.elapsed_time(e1) / reps, 4)
+        res[f"pipelined x{reps} interior_zc={os.environ.get('GS_SLAB_ZC', '0')} exchange={'fat x%d' % b if b else 'none'}"] = round(e0.elapsed_time(e1) / reps, 4)
     settings = [(v_, b, "0") for v_ in ("cur", "first", "delay-1", "delay-3", "delay-6", "delay-12")
                 for b in (0, 8, 32)]
+    if os.environ.get("PROBE_ONLY_PIPE"):  # the r03 driver's schedule only (A/B of GS_SLAB_ZC per process)
+        settings = []
     if os.environ.get("PROBE_MASK"):
         settings += [("first-mask", b, "0") for b in (0, 8, 32)]
     for _ in range(2):
