@@ -1154,6 +1154,160 @@ __global__ __launch_bounds__(256) void k_pro_strip(const double* __restrict__ v,
     es[(((int64_t)b * (nz + 4) + p + 1) * 4 + col) * (ny + 2) + y] = val;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Small levels (LINEAR, canonical stencil): a level's whole down-leg step or up-leg step in ONE launch
+// of LDS-tiled blocks that recompute their halos instead of exchanging them. A 32^3 or 16^3 level is
+// pure launch latency (~4.5 us per operator on a chip it cannot fill): the reference's pre-smoothing
+// (2 sweeps), residual and restriction take one launch instead of three to five, the prolongation,
+// correction and 2 post-smoothing sweeps one instead of three. A block owns a TS^3 tile of fine points
+// (TS = 8: a 4^3 tile of coarse points) and evaluates every stage on the tile plus the halo the later
+// stages read (v: 15^3 -> sweep 1: 13^3 -> sweep 2: 11^3 -> residual: 9^3 -> restriction), every point
+// with the expression of the kernel it replaces (op_value / jacobi_update / the restriction's 27 terms
+// in the reference's order / prolong_value), so every output is bit-identical to the unfused sequence.
+// Points outside the level's interior keep their loaded value (a stored sweep leaves boundary values
+// as they are) and have r = 0 (the reference never writes r there); loads are clamped to the padded
+// array, whose clamped copies only ever feed such boundary points.
+constexpr int TS = 8, TS_T = 256;
+
+// one Jacobi sweep over a tile: dst (edge dN) from src (edge dN + 2; dst i <-> src i + 1), f from a tile
+// of edge fN (dst i <-> f i + fo); global index of dst point 0 per axis: g0
+template <bool UN>
+__device__ __forceinline__ void tile_sweep(const Coef& k, const double* src, double* dst, int dN, const double* F,
+                                           int fN, int fo, int gx0, int gy0, int gz0, int nx, int ny, int nz)
+{
+    const int sN = dN + 2, total = dN * dN * dN;
+    for (int t = threadIdx.x; t < total; t += TS_T) {
+        const int i = t % dN, j = (t / dN) % dN, l = t / (dN * dN);
+        const int gx = gx0 + i, gy = gy0 + j, gz = gz0 + l;
+        const int q = (i + 1) + sN * ((j + 1) + sN * (l + 1));
+        const double c = src[q];
+        double nv = c;
+        if (gx >= 1 && gx <= nx && gy >= 1 && gy <= ny && gz >= 1 && gz <= nz) {
+            const double a = op_value<GS_LINEAR, UN>(k, c, src[q + 1], src[q - 1], src[q + sN], src[q - sN],
+                                                       src[q + sN * sN], src[q - sN * sN], 0.0);
+            nv = jacobi_update<GS_LINEAR>(k, c, F[(i + fo) + fN * ((j + fo) + fN * (l + fo))] - a, 0.0);
+        }
+        dst[t] = nv;
+    }
+}
+
+// a tile of a padded field, clamped to the padded array (ZV: identically zero)
+template <bool ZV>
+__device__ __forceinline__ void tile_load(const double* __restrict__ g, double* dst, int N, int gx0, int gy0, int gz0,
+                                          int nx, int ny, int nz, int64_t ldy, int64_t ldz)
+{
+    for (int t = threadIdx.x; t < N * N * N; t += TS_T) {
+        if (ZV) {
+            dst[t] = 0.0;
+            continue;
+        }
+        const int i = t % N, j = (t / N) % N, l = t / (N * N);
+        const int x = min(max(gx0 + i, 0), nx + 1), y = min(max(gy0 + j, 0), ny + 1), z = min(max(gz0 + l, 0), nz + 1);
+        dst[t] = g[x + (int64_t)y * ldy + (int64_t)z * ldz];
+    }
+}
+
+// pre-smoothing pair + residual + full weighting of a small LINEAR level: v_out = S(S(v)) on the tile's
+// fine points, coarse f = R(f - A v_out) on its coarse points (CpuSolver.cpp:88-99 with preSmoothing 2;
+// ZV: v = 0, the coarse level's first sweeps after CpuSolver.cpp:100-101)
+template <bool ZV, bool UN>
+__global__ __launch_bounds__(TS_T) void k_tile_pre_rr(Coef k, const double* __restrict__ v, const double* __restrict__ f,
+                                                      double* __restrict__ vout, double* __restrict__ cf, int nx, int ny,
+                                                      int nz, int64_t ldy, int64_t ldz, int cnx, int cny, int cnz,
+                                                      int64_t cldy, int64_t cldz)
+{
+    constexpr int NV = TS + 7, N1 = TS + 5, N2 = TS + 3, NR = TS + 1, NF = TS + 5;
+    __shared__ double sv[NV * NV * NV], s1[N1 * N1 * N1], s2[N2 * N2 * N2], sf[NF * NF * NF];
+    double* sr = sv; // the residual tile reuses v's storage once sweep 1 is done
+    const int tx = 1 + TS * (int)blockIdx.x, ty = 1 + TS * (int)blockIdx.y, tz = 1 + TS * (int)blockIdx.z;
+    tile_load<ZV>(v, sv, NV, tx - 3, ty - 3, tz - 3, nx, ny, nz, ldy, ldz);
+    tile_load<false>(f, sf, NF, tx - 2, ty - 2, tz - 2, nx, ny, nz, ldy, ldz);
+    __syncthreads();
+    tile_sweep<UN>(k, sv, s1, N1, sf, NF, 0, tx - 2, ty - 2, tz - 2, nx, ny, nz);
+    __syncthreads();
+    tile_sweep<UN>(k, s1, s2, N2, sf, NF, 1, tx - 1, ty - 1, tz - 1, nx, ny, nz);
+    __syncthreads();
+    // the tile's own fine points of v'' (interior only)
+    for (int t = threadIdx.x; t < TS * TS * TS; t += TS_T) {
+        const int i = t % TS, j = (t / TS) % TS, l = t / (TS * TS);
+        const int x = tx + i, y = ty + j, z = tz + l;
+        if (x <= nx && y <= ny && z <= nz)
+            vout[x + (int64_t)y * ldy + (int64_t)z * ldz] = s2[(i + 1) + N2 * ((j + 1) + N2 * (l + 1))];
+    }
+    // r = f - A v'' on fine points tx .. tx + TS (the restriction's 3-point windows); 0 off the interior
+    for (int t = threadIdx.x; t < NR * NR * NR; t += TS_T) {
+        const int i = t % NR, j = (t / NR) % NR, l = t / (NR * NR);
+        const int gx = tx + i, gy = ty + j, gz = tz + l;
+        double r = 0.0;
+        if (gx >= 1 && gx <= nx && gy >= 1 && gy <= ny && gz >= 1 && gz <= nz) {
+            const int q = (i + 1) + N2 * ((j + 1) + N2 * (l + 1));
+            const double c = s2[q];
+            const double a = op_value<GS_LINEAR, UN>(k, c, s2[q + 1], s2[q - 1], s2[q + N2], s2[q - N2],
+                                                       s2[q + N2 * N2], s2[q - N2 * N2], 0.0);
+            r = sf[(i + 2) + NF * ((j + 2) + NF * (l + 2))] - a;
+        }
+        sr[t] = r;
+    }
+    __syncthreads();
+    // coarse points X = (tx + 1) / 2 + 0..TS/2-1 (fine centre 2X = tx + 1 + 2u): the 27 terms in the
+    // reference's order (CpuSolver.cpp:225-231)
+    constexpr int TC = TS / 2;
+    if (threadIdx.x < TC * TC * TC) {
+        const int u = threadIdx.x % TC, w = (threadIdx.x / TC) % TC, o = threadIdx.x / (TC * TC);
+        const int X = (tx + 1) / 2 + u, Y = (ty + 1) / 2 + w, Z = (tz + 1) / 2 + o;
+        if (X <= cnx && Y <= cny && Z <= cnz) {
+            double acc = 0.0;
+#pragma unroll
+            for (int a = -1; a <= 1; a++)
+#pragma unroll
+                for (int b = -1; b <= 1; b++)
+#pragma unroll
+                    for (int c = -1; c <= 1; c++) {
+                        const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) * ((2.0 - (b < 0 ? -b : b)) / 2.0) *
+                                           ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                        acc += wgt * sr[(1 + 2 * u + a) + NR * ((1 + 2 * w + b) + NR * (1 + 2 * o + c))];
+                    }
+            cf[X + (int64_t)Y * cldy + (int64_t)Z * cldz] = acc;
+        }
+    }
+}
+
+// prolongation + correction + 2 post-smoothing sweeps of a small LINEAR level: v_out = S(S(v + P c)) on the
+// tile's fine points (CpuSolver.cpp:127-134 with the first two post-smoothing sweeps)
+template <bool UN>
+__global__ __launch_bounds__(TS_T) void k_tile_pro2(Coef k, const double* __restrict__ v, const double* __restrict__ c,
+                                                    const double* __restrict__ f, double* __restrict__ vout, int nx,
+                                                    int ny, int nz, int64_t ldy, int64_t ldz, int64_t cldy, int64_t cldz)
+{
+    constexpr int NU = TS + 4, N1 = TS + 2, NF = TS + 2;
+    __shared__ double su[NU * NU * NU], s1[N1 * N1 * N1], sf[NF * NF * NF];
+    const int tx = 1 + TS * (int)blockIdx.x, ty = 1 + TS * (int)blockIdx.y, tz = 1 + TS * (int)blockIdx.z;
+    for (int t = threadIdx.x; t < NU * NU * NU; t += TS_T) {
+        const int i = t % NU, j = (t / NU) % NU, l = t / (NU * NU);
+        const int gx = tx - 2 + i, gy = ty - 2 + j, gz = tz - 2 + l;
+        const int x = min(max(gx, 0), nx + 1), y = min(max(gy, 0), ny + 1), z = min(max(gz, 0), nz + 1);
+        double u = v[x + (int64_t)y * ldy + (int64_t)z * ldz];
+        if (gx >= 1 && gx <= nx && gy >= 1 && gy <= ny && gz >= 1 && gz <= nz)
+            u = u + prolong_value<false>(c, nullptr, gx, gy, gz, cldy, cldz, 0);
+        su[t] = u;
+    }
+    tile_load<false>(f, sf, NF, tx - 1, ty - 1, tz - 1, nx, ny, nz, ldy, ldz);
+    __syncthreads();
+    tile_sweep<UN>(k, su, s1, N1, sf, NF, 0, tx - 1, ty - 1, tz - 1, nx, ny, nz);
+    __syncthreads();
+    for (int t = threadIdx.x; t < TS * TS * TS; t += TS_T) {
+        const int i = t % TS, j = (t / TS) % TS, l = t / (TS * TS);
+        const int gx = tx + i, gy = ty + j, gz = tz + l;
+        if (gx > nx || gy > ny || gz > nz) continue;
+        const int q = (i + 1) + N1 * ((j + 1) + N1 * (l + 1));
+        const double cc = s1[q];
+        const double a = op_value<GS_LINEAR, UN>(k, cc, s1[q + 1], s1[q - 1], s1[q + N1], s1[q - N1], s1[q + N1 * N1],
+                                                   s1[q - N1 * N1], 0.0);
+        vout[gx + (int64_t)gy * ldy + (int64_t)gz * ldz] =
+            jacobi_update<GS_LINEAR>(k, cc, sf[(i + 1) + NF * ((j + 1) + NF * (l + 1))] - a, 0.0);
+    }
+}
+
 // Unfused reference-shaped interpolate (whole padded fine array), used by parity tests.
 __global__ __launch_bounds__(256) void k_interpolate(const double* __restrict__ c, double* __restrict__ e, int fPx,
                                                      int fPy, int fPz, int64_t fldy, int64_t fldz, int64_t cldy,

@@ -173,6 +173,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         sw.zeroGuess = !on("GS_NO_ZERO_GUESS");
         sw.pipeline = !on("GS_NO_PIPELINE");
         if (const char* e = std::getenv("GS_NEWTON_PRO_POINTS")) sw.newtonProPoints = std::strtoll(e, nullptr, 10);
+        if (const char* e = std::getenv("GS_TILE_POINTS")) sw.tilePoints = std::strtoll(e, nullptr, 10);
     }
     std::vector<int64_t> nzs, pts;
     for (int l = 0; l < nlev; l++) {
@@ -224,6 +225,8 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         thin.nz = L.minPlanes;
         L.fusedPairs = sw.fusedSweeps && gs_jacobi_sweep2_supported_mode(&stencilAbi, &thin, (int)mode) == 2 &&
                        (!L.distributed || L.minPlanes >= 2);
+        L.tiled = !L.distributed && pts[l] <= sw.tilePoints &&
+                  gs_tiled_supported(&stencilAbi, &L.geom, (int)mode) != 0;
     }
     // The coarse end of the V-cycle runs as one gs_coarse_cycle launch from the first level of at
     // most GS_COARSE_POINTS points that is not Z-slab partitioned; 0 = off. Default 512 = 8^3: a 16^3
@@ -803,6 +806,22 @@ void HipSolver::upLeg(HipGridData& grid, std::size_t i)
     auto& F = grid.getLevel(i - 1);
     grid.clock.mark(s, (int)(i - 1), true);
     materialize(grid, i); // only if the level had no sweep at all
+    if (i - 1 >= 1 && F.tiled && !C.distributed && grid.postSmoothing >= 2) {
+        // a small level: prolongation, correction and the first two post-smoothing sweeps in one launch
+        materialize(grid, i - 1);
+        if (grid.trace)
+            grid.rec("tiledpro", {{"L", (long long)(i - 1)}});
+        else
+            check(gs_prolong_smooth2_tiled(&grid.stencilAbi, &F.geom, grid.omega, F.v.data(), C.v.data(), &C.geom,
+                                           F.vAlt.data(), F.f.data(), s),
+                  "gs_prolong_smooth2_tiled");
+        F.v.swap(F.vAlt);
+        if (grid.trace) grid.rec("swap", {{"L", (long long)(i - 1)}});
+        F.vZero = false;
+        jacobi(grid, i - 1, grid.postSmoothing - 2);
+        grid.clock.mark(s, (int)(i - 1), false);
+        return;
+    }
     if (grid.sw.fusedProlong && F.fusedPairs && grid.postSmoothing >= 2 && proWorthIt(grid, i - 1) && proSlabOk(grid, i - 1) &&
         gs_jacobi_sweep2_prolong_supported(&grid.stencilAbi, &F.geom, (int)grid.mode)) {
         // the first two post-smoothing sweeps of v^h + P v^2h in one pass (the corrected
@@ -863,9 +882,24 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
             pre -= (std::size_t)*pending;
             *pending = 0;
         }
-        jacobi(grid, i, pre);
         auto& L = grid.getLevel(i);
         auto& C = grid.getLevel(i + 1);
+        if (i >= 1 && pre == 2 && L.tiled && !C.distributed) {
+            // a small level: the pre-smoothing pair, residual and restriction in one tiled launch
+            if (grid.trace)
+                grid.rec("tiledpre", {{"L", (long long)i}, {"vzero", L.vZero}});
+            else
+                check(gs_smooth2_restrict_tiled(&grid.stencilAbi, &L.geom, grid.omega, L.vZero ? nullptr : L.v.data(),
+                                                L.vAlt.data(), L.f.data(), C.f.data(), &C.geom, s),
+                      "gs_smooth2_restrict_tiled");
+            L.v.swap(L.vAlt);
+            if (grid.trace) grid.rec("swap", {{"L", (long long)i}});
+            L.vZero = false;
+            C.vZero = true; // LINEAR: v^2h = 0 (CpuSolver.cpp:100-101), not stored
+            grid.clock.mark(s, (int)i, false);
+            continue;
+        }
+        jacobi(grid, i, pre);
         // f^2h = R (f^h - A v^h) in one pass: the fine residual is never stored
         bool fused = false;
         if (grid.sw.fusedRR) {

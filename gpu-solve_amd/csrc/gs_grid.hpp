@@ -107,6 +107,7 @@ public:
         bool distributed = false;
         bool fusedPairs = false; // smoothing runs as fused sweep pairs (gs_jacobi_sweep2)
         bool vZero = false;      // v is identically zero but not stored: the next sweep reads no v
+        bool tiled = false;      // small LINEAR level: down- and up-leg steps as one tiled launch each
         int64_t lo = 1, hi = 0; // this rank's owned global planes (== 1..nz when not distributed)
         int64_t minPlanes = 0;  // fewest planes any rank owns on this level
         std::vector<int64_t> ranksLo, ranksHi; // every rank's owned planes (gather of replicated levels)
@@ -145,6 +146,8 @@ public:
         bool fusedRR = true;       // GS_NO_FUSED_RR: residual stored, then restricted
         bool zeroGuess = true;     // GS_NO_ZERO_GUESS: coarse v = 0 stored instead of flagged
         bool pipeline = true;      // GS_NO_PIPELINE: no overlap of the norm wait with the next cycle
+        int64_t tilePoints = (int64_t)1 << 18; // GS_TILE_POINTS: levels of at most this many points (replicated,
+                                               // LINEAR) run the tiled one-launch down/up-leg steps; 0 = off
         int64_t newtonProPoints = (int64_t)1 << 26; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
                                                      // prolongation pair from this many points per rank
     } sw;
