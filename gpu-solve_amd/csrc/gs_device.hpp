@@ -1167,7 +1167,7 @@ __global__ __launch_bounds__(256) void k_pro_strip(const double* __restrict__ v,
 // Points outside the level's interior keep their loaded value (a stored sweep leaves boundary values
 // as they are) and have r = 0 (the reference never writes r there); loads are clamped to the padded
 // array, whose clamped copies only ever feed such boundary points.
-constexpr int TS = 8, TS_T = 256;
+constexpr int TS = 8, TS_T = 1024; // 1024 threads: ~3 points per thread and stage (256: 12-14 us per launch, latency-bound)
 
 // one Jacobi sweep over a tile: dst (edge dN) from src (edge dN + 2; dst i <-> src i + 1), f from a tile
 // of edge fN (dst i <-> f i + fo); global index of dst point 0 per axis: g0

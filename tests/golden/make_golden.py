@@ -127,6 +127,12 @@ def huge_cases():
     }
 
 
+def huge10_cases():
+    """Config #5's grid as the solver runs it: 1024^3 linear 2+2, TEN V-cycles (round-3 verdict: the
+    2-cycle anchors pin little of a converging history)."""
+    return {"m0_n1024_2+2_x10": case(1024, maxiter=10)}
+
+
 def gen_histories(cases, path, vmem_kb=None):
     res = {}
     if os.path.exists(path) and vmem_kb:  # resumable: the huge cases take minutes each
@@ -319,12 +325,16 @@ def main():
     ap.add_argument("--config3", action="store_true", help="only the 10-cycle 511^3/512^3 anchors")
     ap.add_argument("--only-paths", action="store_true", help="only the config-path quoting transcripts")
     ap.add_argument("--huge", action="store_true", help="only the 1023^3/1024^3 anchors (~55 GiB of host RAM)")
+    ap.add_argument("--huge10", action="store_true", help="only the 10-cycle 1024^3 anchor (~55 GiB, long)")
     a = ap.parse_args()
     if a.config3:
         gen_histories(config3_cases(), os.path.join(HERE, "config3_histories.json"), vmem_kb=60 << 20)
         return
     if a.huge:
         gen_histories(huge_cases(), os.path.join(HERE, "huge_histories.json"), vmem_kb=60 << 20)
+        return
+    if a.huge10:
+        gen_histories(huge10_cases(), os.path.join(HERE, "huge10_histories.json"), vmem_kb=60 << 20)
         return
     for exe in (PROBE, REFEXE):
         if not os.path.exists(exe):
