@@ -1169,11 +1169,12 @@ __global__ __launch_bounds__(256) void k_pro_strip(const double* __restrict__ v,
 // array, whose clamped copies only ever feed such boundary points.
 constexpr int TS = 8, TS_T = 1024; // 1024 threads: ~3 points per thread and stage (256: 12-14 us per launch, latency-bound)
 
-// one Jacobi sweep over a tile: dst (edge dN) from src (edge dN + 2; dst i <-> src i + 1), f from a tile
-// of edge fN (dst i <-> f i + fo); global index of dst point 0 per axis: g0
-template <bool UN>
+// one Jacobi sweep over a tile: dst (edge dN) from src (edge dN + 2; dst i <-> src i + 1), f (and, NEWTON,
+// the linearisation point w) from tiles of edge fN (dst i <-> f i + fo); global index of dst point 0: g0
+template <int MODE, bool UN>
 __device__ __forceinline__ void tile_sweep(const Coef& k, const double* src, double* dst, int dN, const double* F,
-                                           int fN, int fo, int gx0, int gy0, int gz0, int nx, int ny, int nz)
+                                           const double* W, int fN, int fo, int gx0, int gy0, int gz0, int nx, int ny,
+                                           int nz)
 {
     const int sN = dN + 2, total = dN * dN * dN;
     for (int t = threadIdx.x; t < total; t += TS_T) {
@@ -1183,9 +1184,11 @@ __device__ __forceinline__ void tile_sweep(const Coef& k, const double* src, dou
         const double c = src[q];
         double nv = c;
         if (gx >= 1 && gx <= nx && gy >= 1 && gy <= ny && gz >= 1 && gz <= nz) {
-            const double a = op_value<GS_LINEAR, UN>(k, c, src[q + 1], src[q - 1], src[q + sN], src[q - sN],
-                                                       src[q + sN * sN], src[q - sN * sN], 0.0);
-            nv = jacobi_update<GS_LINEAR>(k, c, F[(i + fo) + fN * ((j + fo) + fN * (l + fo))] - a, 0.0);
+            const int qf = (i + fo) + fN * ((j + fo) + fN * (l + fo));
+            const double w = MODE == GS_NEWTON ? W[qf] : 0.0;
+            const double a = op_value<MODE, UN>(k, c, src[q + 1], src[q - 1], src[q + sN], src[q - sN],
+                                                 src[q + sN * sN], src[q - sN * sN], w);
+            nv = jacobi_update<MODE>(k, c, F[qf] - a, w);
         }
         dst[t] = nv;
     }
@@ -1207,25 +1210,28 @@ __device__ __forceinline__ void tile_load(const double* __restrict__ g, double* 
     }
 }
 
-// pre-smoothing pair + residual + full weighting of a small LINEAR level: v_out = S(S(v)) on the tile's
-// fine points, coarse f = R(f - A v_out) on its coarse points (CpuSolver.cpp:88-99 with preSmoothing 2;
-// ZV: v = 0, the coarse level's first sweeps after CpuSolver.cpp:100-101)
-template <bool ZV, bool UN>
+// pre-smoothing pair + residual + full weighting of a small level: v_out = S(S(v)) on the tile's fine
+// points, coarse f = R(f - A v_out) on its coarse points (CpuSolver.cpp:88-99 with preSmoothing 2; ZV:
+// v = 0, the coarse level's first sweeps after CpuSolver.cpp:100-101). MODE LINEAR, or NEWTON with the
+// level's newtonV as w (the operator and the update linearised there, CpuSolver.cpp:63-66, :166-172).
+template <int MODE, bool ZV, bool UN>
 __global__ __launch_bounds__(TS_T) void k_tile_pre_rr(Coef k, const double* __restrict__ v, const double* __restrict__ f,
-                                                      double* __restrict__ vout, double* __restrict__ cf, int nx, int ny,
-                                                      int nz, int64_t ldy, int64_t ldz, int cnx, int cny, int cnz,
-                                                      int64_t cldy, int64_t cldz)
+                                                      const double* __restrict__ w, double* __restrict__ vout,
+                                                      double* __restrict__ cf, int nx, int ny, int nz, int64_t ldy,
+                                                      int64_t ldz, int cnx, int cny, int cnz, int64_t cldy, int64_t cldz)
 {
     constexpr int NV = TS + 7, N1 = TS + 5, N2 = TS + 3, NR = TS + 1, NF = TS + 5;
-    __shared__ double sv[NV * NV * NV], s1[N1 * N1 * N1], s2[N2 * N2 * N2], sf[NF * NF * NF];
+    constexpr int NW = MODE == GS_NEWTON ? NF : 1;
+    __shared__ double sv[NV * NV * NV], s1[N1 * N1 * N1], s2[N2 * N2 * N2], sf[NF * NF * NF], sw[NW * NW * NW];
     double* sr = sv; // the residual tile reuses v's storage once sweep 1 is done
     const int tx = 1 + TS * (int)blockIdx.x, ty = 1 + TS * (int)blockIdx.y, tz = 1 + TS * (int)blockIdx.z;
     tile_load<ZV>(v, sv, NV, tx - 3, ty - 3, tz - 3, nx, ny, nz, ldy, ldz);
     tile_load<false>(f, sf, NF, tx - 2, ty - 2, tz - 2, nx, ny, nz, ldy, ldz);
+    if (MODE == GS_NEWTON) tile_load<false>(w, sw, NF, tx - 2, ty - 2, tz - 2, nx, ny, nz, ldy, ldz);
     __syncthreads();
-    tile_sweep<UN>(k, sv, s1, N1, sf, NF, 0, tx - 2, ty - 2, tz - 2, nx, ny, nz);
+    tile_sweep<MODE, UN>(k, sv, s1, N1, sf, sw, NF, 0, tx - 2, ty - 2, tz - 2, nx, ny, nz);
     __syncthreads();
-    tile_sweep<UN>(k, s1, s2, N2, sf, NF, 1, tx - 1, ty - 1, tz - 1, nx, ny, nz);
+    tile_sweep<MODE, UN>(k, s1, s2, N2, sf, sw, NF, 1, tx - 1, ty - 1, tz - 1, nx, ny, nz);
     __syncthreads();
     // the tile's own fine points of v'' (interior only)
     for (int t = threadIdx.x; t < TS * TS * TS; t += TS_T) {
@@ -1241,10 +1247,11 @@ __global__ __launch_bounds__(TS_T) void k_tile_pre_rr(Coef k, const double* __re
         double r = 0.0;
         if (gx >= 1 && gx <= nx && gy >= 1 && gy <= ny && gz >= 1 && gz <= nz) {
             const int q = (i + 1) + N2 * ((j + 1) + N2 * (l + 1));
+            const int qf = (i + 2) + NF * ((j + 2) + NF * (l + 2));
             const double c = s2[q];
-            const double a = op_value<GS_LINEAR, UN>(k, c, s2[q + 1], s2[q - 1], s2[q + N2], s2[q - N2],
-                                                       s2[q + N2 * N2], s2[q - N2 * N2], 0.0);
-            r = sf[(i + 2) + NF * ((j + 2) + NF * (l + 2))] - a;
+            const double a = op_value<MODE, UN>(k, c, s2[q + 1], s2[q - 1], s2[q + N2], s2[q - N2], s2[q + N2 * N2],
+                                                 s2[q - N2 * N2], MODE == GS_NEWTON ? sw[qf] : 0.0);
+            r = sf[qf] - a;
         }
         sr[t] = r;
     }
@@ -1253,8 +1260,8 @@ __global__ __launch_bounds__(TS_T) void k_tile_pre_rr(Coef k, const double* __re
     // reference's order (CpuSolver.cpp:225-231)
     constexpr int TC = TS / 2;
     if (threadIdx.x < TC * TC * TC) {
-        const int u = threadIdx.x % TC, w = (threadIdx.x / TC) % TC, o = threadIdx.x / (TC * TC);
-        const int X = (tx + 1) / 2 + u, Y = (ty + 1) / 2 + w, Z = (tz + 1) / 2 + o;
+        const int u = threadIdx.x % TC, o2 = (threadIdx.x / TC) % TC, o = threadIdx.x / (TC * TC);
+        const int X = (tx + 1) / 2 + u, Y = (ty + 1) / 2 + o2, Z = (tz + 1) / 2 + o;
         if (X <= cnx && Y <= cny && Z <= cnz) {
             double acc = 0.0;
 #pragma unroll
@@ -1265,22 +1272,24 @@ __global__ __launch_bounds__(TS_T) void k_tile_pre_rr(Coef k, const double* __re
                     for (int c = -1; c <= 1; c++) {
                         const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) * ((2.0 - (b < 0 ? -b : b)) / 2.0) *
                                            ((2.0 - (c < 0 ? -c : c)) / 2.0);
-                        acc += wgt * sr[(1 + 2 * u + a) + NR * ((1 + 2 * w + b) + NR * (1 + 2 * o + c))];
+                        acc += wgt * sr[(1 + 2 * u + a) + NR * ((1 + 2 * o2 + b) + NR * (1 + 2 * o + c))];
                     }
             cf[X + (int64_t)Y * cldy + (int64_t)Z * cldz] = acc;
         }
     }
 }
 
-// prolongation + correction + 2 post-smoothing sweeps of a small LINEAR level: v_out = S(S(v + P c)) on the
-// tile's fine points (CpuSolver.cpp:127-134 with the first two post-smoothing sweeps)
-template <bool UN>
+// prolongation + correction + 2 post-smoothing sweeps of a small level: v_out = S(S(v + P c)) on the tile's
+// fine points (CpuSolver.cpp:127-134 with the first two post-smoothing sweeps); MODE as above
+template <int MODE, bool UN>
 __global__ __launch_bounds__(TS_T) void k_tile_pro2(Coef k, const double* __restrict__ v, const double* __restrict__ c,
-                                                    const double* __restrict__ f, double* __restrict__ vout, int nx,
-                                                    int ny, int nz, int64_t ldy, int64_t ldz, int64_t cldy, int64_t cldz)
+                                                    const double* __restrict__ f, const double* __restrict__ w,
+                                                    double* __restrict__ vout, int nx, int ny, int nz, int64_t ldy,
+                                                    int64_t ldz, int64_t cldy, int64_t cldz)
 {
     constexpr int NU = TS + 4, N1 = TS + 2, NF = TS + 2;
-    __shared__ double su[NU * NU * NU], s1[N1 * N1 * N1], sf[NF * NF * NF];
+    constexpr int NW = MODE == GS_NEWTON ? NF : 1;
+    __shared__ double su[NU * NU * NU], s1[N1 * N1 * N1], sf[NF * NF * NF], sw[NW * NW * NW];
     const int tx = 1 + TS * (int)blockIdx.x, ty = 1 + TS * (int)blockIdx.y, tz = 1 + TS * (int)blockIdx.z;
     for (int t = threadIdx.x; t < NU * NU * NU; t += TS_T) {
         const int i = t % NU, j = (t / NU) % NU, l = t / (NU * NU);
@@ -1292,19 +1301,21 @@ __global__ __launch_bounds__(TS_T) void k_tile_pro2(Coef k, const double* __rest
         su[t] = u;
     }
     tile_load<false>(f, sf, NF, tx - 1, ty - 1, tz - 1, nx, ny, nz, ldy, ldz);
+    if (MODE == GS_NEWTON) tile_load<false>(w, sw, NF, tx - 1, ty - 1, tz - 1, nx, ny, nz, ldy, ldz);
     __syncthreads();
-    tile_sweep<UN>(k, su, s1, N1, sf, NF, 0, tx - 1, ty - 1, tz - 1, nx, ny, nz);
+    tile_sweep<MODE, UN>(k, su, s1, N1, sf, sw, NF, 0, tx - 1, ty - 1, tz - 1, nx, ny, nz);
     __syncthreads();
     for (int t = threadIdx.x; t < TS * TS * TS; t += TS_T) {
         const int i = t % TS, j = (t / TS) % TS, l = t / (TS * TS);
         const int gx = tx + i, gy = ty + j, gz = tz + l;
         if (gx > nx || gy > ny || gz > nz) continue;
         const int q = (i + 1) + N1 * ((j + 1) + N1 * (l + 1));
+        const int qf = (i + 1) + NF * ((j + 1) + NF * (l + 1));
         const double cc = s1[q];
-        const double a = op_value<GS_LINEAR, UN>(k, cc, s1[q + 1], s1[q - 1], s1[q + N1], s1[q - N1], s1[q + N1 * N1],
-                                                   s1[q - N1 * N1], 0.0);
-        vout[gx + (int64_t)gy * ldy + (int64_t)gz * ldz] =
-            jacobi_update<GS_LINEAR>(k, cc, sf[(i + 1) + NF * ((j + 1) + NF * (l + 1))] - a, 0.0);
+        const double wv = MODE == GS_NEWTON ? sw[qf] : 0.0;
+        const double a = op_value<MODE, UN>(k, cc, s1[q + 1], s1[q - 1], s1[q + N1], s1[q - N1], s1[q + N1 * N1],
+                                             s1[q - N1 * N1], wv);
+        vout[gx + (int64_t)gy * ldy + (int64_t)gz * ldz] = jacobi_update<MODE>(k, cc, sf[qf] - a, wv);
     }
 }
 

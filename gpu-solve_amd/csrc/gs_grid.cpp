@@ -812,8 +812,9 @@ void HipSolver::upLeg(HipGridData& grid, std::size_t i)
         if (grid.trace)
             grid.rec("tiledpro", {{"L", (long long)(i - 1)}});
         else
-            check(gs_prolong_smooth2_tiled(&grid.stencilAbi, &F.geom, grid.omega, F.v.data(), C.v.data(), &C.geom,
-                                           F.vAlt.data(), F.f.data(), s),
+            check(gs_prolong_smooth2_tiled(&grid.stencilAbi, &F.geom, (int)grid.mode, grid.omega, grid.gamma,
+                                           F.v.data(), C.v.data(), &C.geom, F.vAlt.data(), F.f.data(),
+                                           F.newtonV ? F.newtonV.data() : nullptr, s),
                   "gs_prolong_smooth2_tiled");
         F.v.swap(F.vAlt);
         if (grid.trace) grid.rec("swap", {{"L", (long long)(i - 1)}});
@@ -889,13 +890,14 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
             if (grid.trace)
                 grid.rec("tiledpre", {{"L", (long long)i}, {"vzero", L.vZero}});
             else
-                check(gs_smooth2_restrict_tiled(&grid.stencilAbi, &L.geom, grid.omega, L.vZero ? nullptr : L.v.data(),
-                                                L.vAlt.data(), L.f.data(), C.f.data(), &C.geom, s),
+                check(gs_smooth2_restrict_tiled(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.omega, grid.gamma,
+                                                L.vZero ? nullptr : L.v.data(), L.vAlt.data(), L.f.data(),
+                                                L.newtonV ? L.newtonV.data() : nullptr, C.f.data(), &C.geom, s),
                       "gs_smooth2_restrict_tiled");
             L.v.swap(L.vAlt);
             if (grid.trace) grid.rec("swap", {{"L", (long long)i}});
             L.vZero = false;
-            C.vZero = true; // LINEAR: v^2h = 0 (CpuSolver.cpp:100-101), not stored
+            C.vZero = true; // LINEAR / NEWTON: v^2h = 0 (CpuSolver.cpp:100-101), not stored
             grid.clock.mark(s, (int)i, false);
             continue;
         }

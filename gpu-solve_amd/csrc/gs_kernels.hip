@@ -213,47 +213,53 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     return launch_status();
 }
 
-// the small-level tiled kernels (gs_device.hpp k_tile_*): LINEAR, canonical stencil order, whole levels
+// the small-level tiled kernels (gs_device.hpp k_tile_*): LINEAR / NEWTON, canonical stencil order, whole levels
 int gs_tiled_supported(const gs_stencil* S, const gs_level* L, int mode)
 {
-    return S && valid_stencil(S) && canonical_order(S) && mode == GS_LINEAR && !bad_level(L) && L->z0 == 0 &&
-           L->nx >= 1 && L->ny >= 1 && L->nz >= 1;
+    return S && valid_stencil(S) && canonical_order(S) && (mode == GS_LINEAR || mode == GS_NEWTON) && !bad_level(L) &&
+           L->z0 == 0 && L->nx >= 1 && L->ny >= 1 && L->nz >= 1;
 }
 
-int gs_smooth2_restrict_tiled(const gs_stencil* S, const gs_level* fl, double omega, const double* v_in, double* v_out,
-                              const double* f, double* coarse_f, const gs_level* cl, hipStream_t st)
+int gs_smooth2_restrict_tiled(const gs_stencil* S, const gs_level* fl, int mode, double omega, double gamma,
+                              const double* v_in, double* v_out, const double* f, const double* w, double* coarse_f,
+                              const gs_level* cl, hipStream_t st)
 {
-    if (!gs_tiled_supported(S, fl, GS_LINEAR) || bad_level(cl) || cl->z0 != 0 || !v_out || !f || !coarse_f ||
-        v_in == v_out || cl->nx != fl->nx / 2 || cl->ny != fl->ny / 2 || cl->nz != fl->nz / 2)
+    if (!gs_tiled_supported(S, fl, mode) || bad_level(cl) || cl->z0 != 0 || !v_out || !f || !coarse_f ||
+        v_in == v_out || (mode == GS_NEWTON && !w) || cl->nx != fl->nx / 2 || cl->ny != fl->ny / 2 ||
+        cl->nz != fl->nz / 2)
         return GS_EINVAL;
-    const Coef k = make_coef(S, fl, omega, 0.0);
+    const Coef k = make_coef(S, fl, omega, gamma);
     const dim3 g((unsigned)((fl->nx + TS - 1) / TS), (unsigned)((fl->ny + TS - 1) / TS), (unsigned)((fl->nz + TS - 1) / TS));
-#define GS_TPR(Z, U) hipLaunchKernelGGL((k_tile_pre_rr<Z, U>), g, dim3(TS_T), 0, st, k, v_in, f, v_out, coarse_f, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz)
-    if (!v_in) {
-        if (k.unit) GS_TPR(true, true);
-        else GS_TPR(true, false);
-    } else {
-        if (k.unit) GS_TPR(false, true);
-        else GS_TPR(false, false);
-    }
+#define GS_TPR(M, Z, U) hipLaunchKernelGGL((k_tile_pre_rr<M, Z, U>), g, dim3(TS_T), 0, st, k, v_in, f, w, v_out, coarse_f, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz)
+#define GS_TPRM(M) do { \
+        if (!v_in) { if (k.unit) GS_TPR(M, true, true); else GS_TPR(M, true, false); } \
+        else { if (k.unit) GS_TPR(M, false, true); else GS_TPR(M, false, false); } } while (0)
+    if (mode == GS_NEWTON) GS_TPRM(GS_NEWTON);
+    else GS_TPRM(GS_LINEAR);
+#undef GS_TPRM
 #undef GS_TPR
     return launch_status();
 }
 
-int gs_prolong_smooth2_tiled(const gs_stencil* S, const gs_level* fl, double omega, const double* v_in,
-                             const double* coarse_v, const gs_level* cl, double* v_out, const double* f, hipStream_t st)
+int gs_prolong_smooth2_tiled(const gs_stencil* S, const gs_level* fl, int mode, double omega, double gamma,
+                             const double* v_in, const double* coarse_v, const gs_level* cl, double* v_out,
+                             const double* f, const double* w, hipStream_t st)
 {
-    if (!gs_tiled_supported(S, fl, GS_LINEAR) || bad_level(cl) || cl->z0 != 0 || !v_in || !coarse_v || !v_out || !f ||
-        v_in == v_out || (fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 || (fl->nz + 1) / 2 > cl->nz + 1)
+    if (!gs_tiled_supported(S, fl, mode) || bad_level(cl) || cl->z0 != 0 || !v_in || !coarse_v || !v_out || !f ||
+        v_in == v_out || (mode == GS_NEWTON && !w) || (fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 ||
+        (fl->nz + 1) / 2 > cl->nz + 1)
         return GS_EINVAL;
-    const Coef k = make_coef(S, fl, omega, 0.0);
+    const Coef k = make_coef(S, fl, omega, gamma);
     const dim3 g((unsigned)((fl->nx + TS - 1) / TS), (unsigned)((fl->ny + TS - 1) / TS), (unsigned)((fl->nz + TS - 1) / TS));
-    if (k.unit)
-        hipLaunchKernelGGL((k_tile_pro2<true>), g, dim3(TS_T), 0, st, k, v_in, coarse_v, f, v_out, (int)fl->nx, (int)fl->ny,
-                           (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz);
-    else
-        hipLaunchKernelGGL((k_tile_pro2<false>), g, dim3(TS_T), 0, st, k, v_in, coarse_v, f, v_out, (int)fl->nx, (int)fl->ny,
-                           (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz);
+#define GS_TP2(M, U) hipLaunchKernelGGL((k_tile_pro2<M, U>), g, dim3(TS_T), 0, st, k, v_in, coarse_v, f, w, v_out, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz)
+    if (mode == GS_NEWTON) {
+        if (k.unit) GS_TP2(GS_NEWTON, true);
+        else GS_TP2(GS_NEWTON, false);
+    } else {
+        if (k.unit) GS_TP2(GS_LINEAR, true);
+        else GS_TP2(GS_LINEAR, false);
+    }
+#undef GS_TP2
     return launch_status();
 }
 

@@ -135,22 +135,23 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
                                 const double* v_in, const double* coarse_v, const double* coarse_sub,
                                 const gs_level* coarse, double* v_out, const double* f, const double* w, int zlo,
                                 int zhi, double* ws, int64_t ws_elems, hipStream_t stream);
-/* Small levels (LINEAR, canonical stencil order, whole levels: z0 = 0), where every operator is launch
- * latency: a level's down-leg step and up-leg step each in ONE launch of 8^3-point LDS tiles that
- * recompute their halos (no exchange between blocks), bit-identical to the unfused sequences.
+/* Small levels (LINEAR or NEWTON, canonical stencil order, whole levels: z0 = 0), where every operator
+ * is launch latency: a level's down-leg step and up-leg step each in ONE launch of 8^3-point LDS tiles
+ * that recompute their halos (no exchange between blocks), bit-identical to the unfused sequences.
  *   gs_smooth2_restrict_tiled  v_out = S(S(v_in)) (v_in NULL: v = 0), coarse_f = R(f - A v_out)
  *                              == two jacobi sweeps + compResidual + restrict     CpuSolver.cpp:88-99,141-180,211-238
  *                              (coarse = fine / 2 per axis)
  *   gs_prolong_smooth2_tiled   v_out = S(S(v_in + P coarse_v))
  *                              == interpolate + v += e + two jacobi sweeps        CpuSolver.cpp:127-134,240-290
- * v_in and v_out are distinct fields of the level's layout; only interior points of v_out are written. */
+ * w: the level's newtonV in NEWTON mode (else ignored). v_in and v_out are distinct fields of the level's
+ * layout; only interior points of v_out are written. */
 int gs_tiled_supported(const gs_stencil* S, const gs_level* L, int mode);
-int gs_smooth2_restrict_tiled(const gs_stencil* S, const gs_level* fine, double omega, const double* v_in,
-                              double* v_out, const double* f, double* coarse_f, const gs_level* coarse,
-                              hipStream_t stream);
-int gs_prolong_smooth2_tiled(const gs_stencil* S, const gs_level* fine, double omega, const double* v_in,
-                             const double* coarse_v, const gs_level* coarse, double* v_out, const double* f,
-                             hipStream_t stream);
+int gs_smooth2_restrict_tiled(const gs_stencil* S, const gs_level* fine, int mode, double omega, double gamma,
+                              const double* v_in, double* v_out, const double* f, const double* w, double* coarse_f,
+                              const gs_level* coarse, hipStream_t stream);
+int gs_prolong_smooth2_tiled(const gs_stencil* S, const gs_level* fine, int mode, double omega, double gamma,
+                             const double* v_in, const double* coarse_v, const gs_level* coarse, double* v_out,
+                             const double* f, const double* w, hipStream_t stream);
 /* Which fused-pair kernel (and shape) gs_jacobi_sweep2 launches for this level and mode ("" if none). */
 const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int mode);
 

@@ -130,7 +130,7 @@ def huge_cases():
 def huge10_cases():
     """Config #5's grid as the solver runs it: 1024^3 linear 2+2, TEN V-cycles (round-3 verdict: the
     2-cycle anchors pin little of a converging history)."""
-    return {"m0_n1024_2+2_x10": case(1024, maxiter=10)}
+    return {"m0_n1024_2+2_x10": case(1024, maxiter=10), "m0_n1023_2+2_x10": case(1023, maxiter=10)}
 
 
 def gen_histories(cases, path, vmem_kb=None):
