@@ -54,8 +54,8 @@ def parse():
                     help="after --warmup, keep running untimed sweeps until this much wall time has passed")
     ap.add_argument("--size", type=int, default=512, help="per-rank cube edge (BASELINE config #3: 512)")
     ap.add_argument("--vcycles", type=int, default=20, help="timed V-cycles after one warm-up cycle (0: skip)")
-    ap.add_argument("--cpu-sweeps", type=int, default=6, help="cpu_baseline sample size (0: skip)")
-    ap.add_argument("--cpu-vcycles", type=int, default=1, help="cpu_baseline V-cycles (0: skip)")
+    ap.add_argument("--cpu-sweeps", type=int, default=10, help="cpu_baseline sample size (0: skip)")
+    ap.add_argument("--cpu-vcycles", type=int, default=2, help="cpu_baseline V-cycles after one warm-up cycle (0: skip)")
     ap.add_argument("--config5", type=int, default=1,
                     help="N=1: also time config #5's 1024^3 grid on this GPU (the strong-scaling denominator)")
     ap.add_argument("--newton-iters", type=int, default=2,
