@@ -28,19 +28,19 @@ cat "$OUT/bench.json"
 # is a level-0 launch, so its average is the bench's kernel_ms)
 step rocprof-kernel-trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python bench.py --steps "$STEPS" --warmup "$WARM" --cpu-sweeps 0 --newton-iters 0 --vcycles 0 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail -20 "$OUT/bench_prof.err"; exit 1; }
+    python bench.py --steps "$STEPS" --warmup "$WARM" --cpu-sweeps 0 --newton-iters 0 --vcycles 0 --config5 0 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { tail -20 "$OUT/bench_prof.err"; exit 1; }
 
 # the V-cycle's kernels (tools/vc_breakdown.py reads the trace)
 step rocprof-vcycle
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_vc" -o run --output-format csv -- \
-    python bench.py --steps 2 --warmup 2 --cpu-sweeps 0 --newton-iters 0 --vcycles 10 > "$OUT/bench_vc.json" 2> "$OUT/bench_vc.err" || { tail -20 "$OUT/bench_vc.err"; exit 1; }
+    python bench.py --steps 2 --warmup 2 --cpu-sweeps 0 --newton-iters 0 --vcycles 10 --config5 0 > "$OUT/bench_vc.json" 2> "$OUT/bench_vc.err" || { tail -20 "$OUT/bench_vc.err"; exit 1; }
 
 step rocprof-pmc-fetch
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-    python bench.py --steps 5 --cpu-sweeps 0 --newton-iters 0 --vcycles 0 > "$OUT/pmc_fetch.log" 2>&1 || { tail -20 "$OUT/pmc_fetch.log"; exit 1; }
+    python bench.py --steps 5 --cpu-sweeps 0 --newton-iters 0 --vcycles 0 --config5 0 > "$OUT/pmc_fetch.log" 2>&1 || { tail -20 "$OUT/pmc_fetch.log"; exit 1; }
 
 step rocprof-pmc-write
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
-    python bench.py --steps 5 --cpu-sweeps 0 --newton-iters 0 --vcycles 0 > "$OUT/pmc_write.log" 2>&1 || { tail -20 "$OUT/pmc_write.log"; exit 1; }
+    python bench.py --steps 5 --cpu-sweeps 0 --newton-iters 0 --vcycles 0 --config5 0 > "$OUT/pmc_write.log" 2>&1 || { tail -20 "$OUT/pmc_write.log"; exit 1; }
 
 step done

@@ -22,8 +22,16 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def sweep_kernel(name):
-    """The level-0 smoother of bench.py: the fused pair (k_tb2y / k_tb2) or, without it, the one-sweep k_rb."""
-    return "k_tb2y<0," in name or "k_tb2<0," in name
+    """The level-0 smoother of bench.py's headline: the fused LINEAR pair (k_tb2y whole-row shape, not the
+    column blocks of config #5's 1024-point rows, not the prolongation / zero-iterate forms, or k_tb2) or,
+    without it, the one-sweep k_rb."""
+    if "k_tb2<0," in name:
+        return True
+    if "k_tb2y<0," not in name:
+        return False
+    args = [a.strip() for a in name[name.index("k_tb2y<") + 7:].split(">")[0].split(",")]
+    # k_tb2y<MODE, RY, WXMAX, NT, NTF, ZV, SPEC, PRO, PFD, XH, UN>
+    return len(args) < 10 or (args[5] == "false" and args[7] == "0" and args[9] == "false")
 
 
 def single_kernel(name):
