@@ -1143,24 +1143,19 @@ __global__ __launch_bounds__(256) void k_pro_strip(const double* __restrict__ v,
                                                    int ny, int nz, int64_t ldy, int64_t ldz, int64_t cldy,
                                                    int64_t cldz, int bw, int zlo, int zhi)
 {
-    // one thread per (row, plane) of a boundary computes its four columns: the v row segment is one 32-B
-    // run, and the coarse values under it are shared by the four points
-    const int y = blockIdx.x * 256 + threadIdx.x;
+    // four lanes per row (one per column), 64 rows per block: a wave's v load touches 16 rows' 32-B runs
+    // and its coarse loads ~8 rows' lines (one thread per row and four columns, r03j: 159 us per 1024^3
+    // launch, address-unit bound — every lane of a load on its own cache line)
+    const int col = (int)threadIdx.x & 3;
+    const int y = blockIdx.x * 64 + ((int)threadIdx.x >> 2);
     if (y > ny + 1) return;
     const int p = (int)blockIdx.y - 1;
     const int b = (int)blockIdx.z;
-    const int x0 = 1 + (b + 1) * bw - 2;
+    const int x = 1 + (b + 1) * bw - 2 + col;
     const bool pok = (p >= 1 && p <= nz) || (zlo && p <= 0) || (zhi && p > nz);
-    const bool yin = y >= 1 && y <= ny;
-    const double* vr = v + (int64_t)y * ldy + (int64_t)p * ldz;
-    double* er = es + ((int64_t)b * (nz + 4) + p + 1) * 4 * (ny + 2) + y;
-#pragma unroll
-    for (int col = 0; col < 4; col++) {
-        const int x = x0 + col;
-        double val = vr[x];
-        if (pok && yin && x >= 1 && x <= nx) val = val + prolong_value<SUB>(c, sub, x, y, p, cldy, cldz, 0);
-        er[(int64_t)col * (ny + 2)] = val;
-    }
+    double val = v[x + (int64_t)y * ldy + (int64_t)p * ldz];
+    if (pok && y >= 1 && y <= ny && x >= 1 && x <= nx) val = val + prolong_value<SUB>(c, sub, x, y, p, cldy, cldz, 0);
+    es[(((int64_t)b * (nz + 4) + p + 1) * 4 + col) * (ny + 2) + y] = val;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -201,7 +201,7 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     const Coef k = make_coef(S, L, omega, gamma);
     if (xh && need > 0) {
         const int bw = 2 * WAVE * TBY_WX, nb = (int)((L->nx + bw - 1) / bw - 1);
-        hipLaunchKernelGGL(k_pro_strip<false>, dim3((unsigned)((L->ny + 2 + 255) / 256), (unsigned)(L->nz + 4), (unsigned)nb),
+        hipLaunchKernelGGL(k_pro_strip<false>, dim3((unsigned)((L->ny + 2 + 63) / 64), (unsigned)(L->nz + 4), (unsigned)nb),
                            dim3(256), 0, st, v_in, coarse_v, nullptr, ws, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy,
                            L->ldz, cl->ldy, cl->ldz, bw, zlo ? 1 : 0, zhi ? 1 : 0);
     }

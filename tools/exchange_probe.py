@@ -126,6 +126,63 @@ def main():
             main_s.wait_stream(ist)
         main_s.wait_stream(comm_s if blocks else bnd_s)
 
+    def pipe_steps2(blocks, nsteps):
+        """pipe_steps with the two boundary launches on two high-priority streams (concurrent)."""
+        evb = [None, None]
+        ev_x = None
+        for k_ in range(nsteps):
+            ev_a = torch.cuda.Event()
+            ev_a.record(main_s)
+            for st_ in (bnd_s, bnd2_s):
+                st_.wait_event(ev_a)
+                if ev_x is not None:
+                    st_.wait_event(ev_x)
+            pair(1, 2, bnd_s)
+            pair(NZ - 1, NZ, bnd2_s)
+            bnd_s.wait_stream(bnd2_s)
+            evb[k_ & 1] = torch.cuda.Event()
+            evb[k_ & 1].record(bnd_s)
+            comm_s.wait_event(evb[k_ & 1])
+            if k_ > 0:
+                main_s.wait_event(evb[(k_ - 1) & 1])
+            pair(3, NZ - 2, main_s)
+            if blocks:
+                assert kd.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
+                                      comm_s.cuda_stream) == 0
+            ev_x = torch.cuda.Event()
+            ev_x.record(comm_s)
+        main_s.wait_event(ev_x)
+        main_s.wait_event(evb[(nsteps - 1) & 1])
+
+    def pipe_steps_b(blocks, nsteps, B, serial=False):
+        """pipe_steps with B-plane boundary ranges (planes 1..B, NZ-B+1..NZ; interior B+1..NZ-B); serial: the
+        boundary launches on the compute stream ahead of the interior (no concurrency between the two)."""
+        evb = [None, None]
+        ev_x = None
+        bs = main_s if serial else bnd_s
+        for k_ in range(nsteps):
+            if not serial:
+                ev_a = torch.cuda.Event()
+                ev_a.record(main_s)
+                bs.wait_event(ev_a)
+            if ev_x is not None:
+                bs.wait_event(ev_x)
+            pair(1, B, bs)
+            pair(NZ - B + 1, NZ, bs)
+            evb[k_ & 1] = torch.cuda.Event()
+            evb[k_ & 1].record(bs)
+            comm_s.wait_event(evb[k_ & 1])
+            if k_ > 0 and not serial:
+                main_s.wait_event(evb[(k_ - 1) & 1])
+            pair(B + 1, NZ - B, main_s)
+            if blocks:
+                assert kd.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
+                                      comm_s.cuda_stream) == 0
+            ev_x = torch.cuda.Event()
+            ev_x.record(comm_s)
+        main_s.wait_event(ev_x)
+        main_s.wait_event(evb[(nsteps - 1) & 1])
+
     def pipe_steps(blocks, nsteps):
         """r03 driver (HipSolver::jacobi): a sequence of overlapped steps in which the compute stream never
         waits for an exchange. Boundary k waits for interior k-1 and exchange k-1; the interior k waits for
@@ -155,6 +212,42 @@ def main():
         main_s.wait_event(evb[(nsteps - 1) & 1])
 
     res = {}
+    # the boundary launches alone (B planes each side)
+    for B in (2, 4):
+        for _ in range(2):
+            pair(1, B, main_s)
+            pair(NZ - B + 1, NZ, main_s)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(main_s)
+        for _ in range(reps):
+            pair(1, B, main_s)
+            pair(NZ - B + 1, NZ, main_s)
+        e1.record(main_s)
+        torch.cuda.synchronize()
+        res[f"boundary alone B={B}"] = round(e0.elapsed_time(e1) / reps, 4)
+    for B, serial in ((2, True), (4, False), (4, True), (6, False)):
+        for b in (0, 32):
+            for _ in range(2):
+                pipe_steps_b(b, reps, B, serial)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main_s)
+            pipe_steps_b(b, reps, B, serial)
+            e1.record(main_s)
+            torch.cuda.synchronize()
+            res[f"pipelined B={B}{' serial' if serial else ''} exchange={'fat x%d' % b if b else 'none'}"] = \
+                round(e0.elapsed_time(e1) / reps, 4)
+    for b in (0, 32):
+        for _ in range(2):
+            pipe_steps2(b, reps)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(main_s)
+        pipe_steps2(b, reps)
+        e1.record(main_s)
+        torch.cuda.synchronize()
+        res[f"pipelined-2bnd x{reps} exchange={'fat x%d' % b if b else 'none'}"] = round(e0.elapsed_time(e1) / reps, 4)
     for b in (0, 8, 32):
         for _ in range(2):
             pipe_steps(b, reps)
