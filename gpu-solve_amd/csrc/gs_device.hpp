@@ -541,6 +541,109 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
     }
 }
 
+// compF right after findError's update (NewtonSolver.cpp:105-107 then :48-81): w' = w + e (newtonV +=
+// v, the expression of k_axpy with a = 1) is formed from both operands wherever the stencil reads it and
+// stored once for the block's own points, and the NONLINEAR residual f = F - N(w') with its per-block
+// sum of squares is written in the same pass: 40 instead of 48 B per point (k_axpy + k_rb KIND 1).
+// Same shape, grid, term order and partial-sum order as k_rb<NONLINEAR, 1> under pass_plan, so f, the
+// partials and the norm are bit-identical to the two launches; the caller guarantees that wout's
+// non-interior cells already hold what k_axpy would leave there (zeros on a whole level).
+template <int RY, int W, bool UN>
+__global__ __launch_bounds__(WAVE* W) void k_newton_upd(Coef k, const double* __restrict__ w,
+                                                         const double* __restrict__ e, const double* __restrict__ F,
+                                                         double* __restrict__ wout, double* __restrict__ fout,
+                                                         double* __restrict__ partials, int nx, int ny, int nz,
+                                                         int64_t ldy, int64_t ldz, int ZC)
+{
+    __shared__ double red[W];
+    const int lane = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int64_t tile = blockIdx.x + gridDim.x * ((int64_t)blockIdx.y + gridDim.y * (int64_t)blockIdx.z);
+    const int x0 = 1 + blockIdx.x * (2 * WAVE);
+    const int x = x0 + 2 * lane;
+    const int xl = min(x, nx + 1);
+    const int y0 = 1 + (blockIdx.y * W + wv) * RY;
+    const int zb = 1 + blockIdx.z * ZC;
+    const int ze = min(zb + ZC - 1, nz);
+    const int xle = x0 - 1;
+    const int xre = min(x0 + 2 * WAVE, nx + 1);
+    const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
+    int64_t roff[RY + 2];
+#pragma unroll
+    for (int r = 0; r < RY + 2; r++) roff[r] = (int64_t)min(y0 - 1 + r, ny + 1) * ldy;
+    auto lw2 = [&](int64_t o) {
+        const double2 a = ld2(w + o), b = ld2(e + o);
+        return make_double2(a.x + b.x, a.y + b.y);
+    };
+    auto lw1 = [&](int64_t o) { return w[o] + e[o]; };
+    // the ring of k_rb: plane z+1's halo rows, F, edges and plane z+2's rows in slot ph
+    double2 P[RY], C[RY], NL[2][RY], FL[2][RY], HL[2][2];
+    double EL[2][RY], ER[2][RY];
+    double sumsq = 0.0;
+    auto load_slot = [&](const int s, const int64_t z1, const int64_t z2) {
+#pragma unroll
+        for (int r = 0; r < RY; r++) {
+            NL[s][r] = lw2(xl + roff[r + 1] + z2);
+            FL[s][r] = ld2s<true>(F + xl + roff[r + 1] + z1);
+            EL[s][r] = lw1(xle + roff[r + 1] + z1);
+            ER[s][r] = lw1(xre + roff[r + 1] + z1);
+        }
+        HL[s][0] = lw2(xl + roff[0] + z1);
+        HL[s][1] = lw2(xl + roff[RY + 1] + z1);
+    };
+    if (zb <= ze) {
+        const int64_t zo = (int64_t)zb * ldz;
+#pragma unroll
+        for (int r = 0; r < RY; r++) {
+            P[r] = lw2(xl + roff[r + 1] + zo - ldz);
+            C[r] = lw2(xl + roff[r + 1] + zo);
+        }
+        load_slot(1, zo, zo + ldz);
+    }
+    for (int z0 = zb; z0 <= ze; z0 += 2) {
+#pragma unroll
+        for (int ph = 0; ph < 2; ph++) {
+            const int z = z0 + ph;
+            const bool real = z <= ze;
+            const int cs = ph ^ 1;
+            const int64_t zo = (int64_t)z * ldz;
+            load_slot(ph, (int64_t)min(z + 1, nz + 1) * ldz, (int64_t)min(z + 2, nz + 1) * ldz);
+#pragma unroll
+            for (int r = 0; r < RY; r++) {
+                const double2 c = C[r], ym = r == 0 ? HL[cs][0] : C[r - 1], yp = r == RY - 1 ? HL[cs][1] : C[r + 1];
+                const double2 zm = P[r], zp = NL[cs][r];
+                const double xm0 = lane_from_left<true>(c.y, EL[cs][r]);
+                const double xp1 = lane_from_right<true>(c.x, ER[cs][r]);
+                const double a0 = op_value<GS_NONLINEAR, UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, 0.0);
+                const double a1 = op_value<GS_NONLINEAR, UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, 0.0);
+                const double r0 = FL[cs][r].x - a0, r1 = FL[cs][r].y - a1;
+                const bool rowok = real && y0 + r <= ny;
+                if (rowok && okx0) sumsq += r0 * r0;
+                if (rowok && okx1) sumsq += r1 * r1;
+                if (rowok) {
+                    const int64_t q = x + roff[r + 1] + zo;
+                    if (okx1) {
+                        st2s<true>(fout + q, r0, r1);
+                        st2s<true>(wout + q, c.x, c.y);
+                    } else if (okx0) {
+                        fout[q] = r0;
+                        wout[q] = c.x;
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RY; r++) {
+                P[r] = C[r];
+                C[r] = NL[cs][r];
+            }
+        }
+    }
+    if (partials) {
+        const double t = block_sum<W>(sumsq, red);
+        if (threadIdx.x == 0 && threadIdx.y == 0) partials[tile] = t;
+    }
+}
+
 dim3 rb_grid(const gs_level* L, int RY, int W, int ZC, bool oneD = false)
 {
     const dim3 g((unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), (unsigned)((L->ny + RY * W - 1) / (RY * W)),
@@ -1371,6 +1474,19 @@ __global__ __launch_bounds__(256) void k_rhs(double* __restrict__ f, int mode, d
         f[p] = 2.0 * ((y - y * y) * (z - z * z) + (x - x * x) * (z - z * z) + (x - x * x) * (y - y * y)) +
                gamma * ux * uy * uz * exp(ux * uy * uz);
     }
+}
+
+// dst = src over n doubles (Vector3 copy-assignment): one dwordx4 per thread and iteration, both
+// streams non-temporal (the 1 GB newtonF copy of a 512^3 Newton solve at the box's copy rate instead of
+// hipMemcpyAsync's ~2.7 TB/s); n odd: the last element by thread 0
+__global__ __launch_bounds__(256) void k_copy(double* __restrict__ dst, const double* __restrict__ src, int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, n2 = n / 2;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
+        const double2 t = ld2s<true>(src + 2 * i);
+        st2s<true>(dst + 2 * i, t.x, t.y);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) dst[n - 1] = src[n - 1];
 }
 
 __global__ __launch_bounds__(256) void k_axpy(double* __restrict__ y, const double* __restrict__ x, double a,

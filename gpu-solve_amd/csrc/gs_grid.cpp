@@ -172,6 +172,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         sw.fusedRR = !on("GS_NO_FUSED_RR");
         sw.zeroGuess = !on("GS_NO_ZERO_GUESS");
         sw.pipeline = !on("GS_NO_PIPELINE");
+        sw.newtonFusedUpdate = !on("GS_NO_NEWTON_FUSED_UPDATE");
         if (const char* e = std::getenv("GS_NEWTON_PRO_POINTS")) sw.newtonProPoints = std::strtoll(e, nullptr, 10);
         if (const char* e = std::getenv("GS_TILE_POINTS")) sw.tilePoints = std::strtoll(e, nullptr, 10);
     }
@@ -1054,9 +1055,7 @@ void NewtonSolver::solve(HipGridData& grid)
     if (grid.trace)
         grid.rec("copy", {{"L", 0}}, "f>newtonF");
     else
-        check((int)hipMemcpyAsync(grid.newtonF.data(), L0.f.data(), sizeof(double) * L0.f.span(),
-                                  hipMemcpyDeviceToDevice, s),
-              "hipMemcpyAsync");
+        check(gs_copy(grid.newtonF.data(), L0.f.data(), L0.f.span(), s), "gs_copy");
     const double initialResidual = compF(grid);
     if (history) history->push_back(initialResidual);
     if (print) std::cout << "Inital newton residual: " << initialResidual << '\n';
@@ -1068,8 +1067,7 @@ void NewtonSolver::solve(HipGridData& grid)
         // v = 0 (NewtonSolver.cpp:22), not stored: the inner solve's first (speculative) sweep is a
         // zero-iterate kernel that reads no v; anything else that reads v materializes it first
         L0.vZero = true;
-        findError(grid);
-        const double res = compF(grid);
+        const double res = findError(grid) ? compFUpdate(grid) : compF(grid);
         if (history) history->push_back(res);
         if (print) {
             std::cout << "newton iter: " << i << " residual: " << res << ' ';
@@ -1093,8 +1091,33 @@ double NewtonSolver::compF(HipGridData& grid)
     return HipSolver::finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L0.geom));
 }
 
+// newtonV += v and the compF after it as one pass (gs_newton_F_update) on a level this rank holds whole:
+// the sum goes to level 0's vAlt — zero outside the interior like newtonV + v, and dead once the inner
+// solve has returned (its pending speculative sweep is dropped; the next inner solve starts from the
+// zero iterate) — which then becomes newtonV. Bit-identical to gs_axpy + gs_newton_F.
+bool NewtonSolver::fusedUpdate(const HipGridData& grid)
+{
+    const auto& L0 = grid.getLevel(0);
+    return grid.sw.newtonFusedUpdate && !(L0.distributed && grid.nranks() > 1) &&
+           gs_newton_F_update_supported(&grid.stencilAbi, &L0.geom) != 0;
+}
+
+double NewtonSolver::compFUpdate(HipGridData& grid)
+{
+    auto& L0 = grid.getLevel(0);
+    if (grid.trace)
+        grid.rec("newtonFupdate", {{"L", 0}});
+    else
+        check(gs_newton_F_update(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
+                                 grid.newtonF.data(), L0.vAlt.data(), L0.f.data(), grid.partials(), grid.stream()),
+              "gs_newton_F_update");
+    L0.newtonV.swap(L0.vAlt);
+    grid.halo(L0, L0.f, grid.stream());
+    return HipSolver::finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L0.geom));
+}
+
 // NewtonSolver.cpp:83-108
-void NewtonSolver::findError(HipGridData& grid)
+bool NewtonSolver::findError(HipGridData& grid)
 {
     for (std::size_t i = 1; i + 1 < grid.numLevels(); i++)
         HipSolver::restrict(grid, grid.getLevel(i - 1).newtonV, i - 1, grid.getLevel(i).newtonV);
@@ -1113,10 +1136,12 @@ void NewtonSolver::findError(HipGridData& grid)
     grid.maxiter = origIter;
     grid.tol = origTol;
 
+    if (fusedUpdate(grid)) return true; // compFUpdate adds v
     auto& L0 = grid.getLevel(0);
     // whole local array, ghost planes included: both operands' ghosts are current, so the sum's are
     if (grid.trace) grid.rec("axpy", {{"L", 0}}, "newtonV+=v");
     else check(gs_axpy(L0.newtonV.data(), L0.v.data(), 1.0, L0.v.span(), grid.stream()), "gs_axpy");
+    return false;
 }
 
 // "[gs] mlups=... gbps=... pct_peak=... vcycle_ms=... cycles=... level_ms=a,b,..." over the V-cycles

@@ -146,6 +146,7 @@ public:
         bool fusedRR = true;       // GS_NO_FUSED_RR: residual stored, then restricted
         bool zeroGuess = true;     // GS_NO_ZERO_GUESS: coarse v = 0 stored instead of flagged
         bool pipeline = true;      // GS_NO_PIPELINE: no overlap of the norm wait with the next cycle
+        bool newtonFusedUpdate = true; // GS_NO_NEWTON_FUSED_UPDATE: newtonV += v, then compF (two passes)
         int64_t tilePoints = (int64_t)1 << 18; // GS_TILE_POINTS: levels of at most this many points (replicated,
                                                // LINEAR) run the tiled one-launch down/up-leg steps; 0 = off
         int64_t newtonProPoints = (int64_t)1 << 26; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
@@ -251,7 +252,10 @@ class NewtonSolver {
 public:
     static void solve(HipGridData& grid);
     static double compF(HipGridData& grid);
-    static void findError(HipGridData& grid);
+    // findError's newtonV += v, left to compFUpdate when fusedUpdate() (returns whether it was deferred)
+    static bool findError(HipGridData& grid);
+    static double compFUpdate(HipGridData& grid);
+    static bool fusedUpdate(const HipGridData& grid);
     static thread_local std::vector<double>* history;
 };
 

@@ -439,6 +439,39 @@ int gs_newton_F(const gs_stencil* S, const gs_level* L, double gamma, const doub
     return gs_residual(S, L, GS_NONLINEAR, gamma, w, F, nullptr, f, partials, st);
 }
 
+int gs_newton_F_update_supported(const gs_stencil* S, const gs_level* L)
+{
+    return (S && !bad_level(L) && valid_stencil(S) && L->nx > 0 && L->ny > 0 && L->nz > 0 && pass_plan(S, L).rb) ? 1
+                                                                                                               : 0;
+}
+
+int gs_newton_F_update(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* e,
+                       const double* F, double* w_out, double* f, double* partials, hipStream_t st)
+{
+    if (!w || !e || !F || !w_out || !f || w_out == w || w_out == e || !gs_newton_F_update_supported(S, L))
+        return GS_EINVAL;
+    const Coef k = make_coef(S, L, 0.0, gamma);
+    const PassPlan plan = pass_plan(S, L); // the grid and partial layout of gs_newton_F (k_rb KIND 1)
+    const dim3 b(WAVE, RB_W);
+    if (k.unit)
+        hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, true>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials,
+                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc);
+    else
+        hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, false>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials,
+                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc);
+    return launch_status();
+}
+
+int gs_copy(double* dst, const double* src, int64_t n, hipStream_t st)
+{
+    if (!dst || !src || n < 0) return GS_EINVAL;
+    if (n == 0 || dst == src) return 0;
+    if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) // dwordx4 alignment
+        return (int)hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToDevice, st);
+    hipLaunchKernelGGL(k_copy, dim3(1024), dim3(256), 0, st, dst, src, n);
+    return launch_status();
+}
+
 int gs_axpy(double* y, const double* x, double a, int64_t n, hipStream_t st)
 {
     if (!y || !x || n < 0) return GS_EINVAL;

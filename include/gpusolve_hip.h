@@ -17,6 +17,8 @@
  *   gs_apply_op          CpuSolver::applyStencil               src/cpu/CpuSolver.cpp:182-208
  *   gs_apply_op_add      applyStencil then f += r (FAS)        src/cpu/CpuSolver.cpp:110-112
  *   gs_newton_F          NewtonSolver::compF                   src/cpu/NewtonSolver.cpp:48-81
+ *   gs_newton_F_update   findError's newtonV += v, then compF  src/cpu/NewtonSolver.cpp:105-107, 48-81
+ *   gs_copy              Vector3 copy-assignment (newtonF = f) src/cpu/NewtonSolver.cpp:12
  *   gs_axpy              Vector3::operator+= / -=              src/cpu/Vector3.cpp:34-53
  *   gs_coarse_cycle      CpuSolver::vcycle below a level (one launch) src/cpu/CpuSolver.cpp:92-135
  *
@@ -204,6 +206,20 @@ int gs_apply_op_add(const gs_stencil* S, const gs_level* L, double gamma, const 
 /* Newton outer residual f = F - [A(w)/h^2 + gamma*w*exp(w)] (+ partial sums of f^2 as gs_residual). */
 int gs_newton_F(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* F, double* f,
                 double* partials, hipStream_t stream);
+
+/* findError's newtonV += v followed by compF (NewtonSolver.cpp:105-107, then :48-81) in one pass:
+ * w_out = w + e at every interior point and f = F - [A(w_out)/h^2 + gamma*w_out*exp(w_out)] (+ the
+ * partial sums of f^2 of gs_newton_F, same count and order), bit-identical to gs_axpy(w, e, 1) then
+ * gs_newton_F. w_out must be a third field whose non-interior cells already hold w + e there (zeros
+ * on a whole level, the Dirichlet boundary). Shapes without the register-blocked pass (tiny levels,
+ * non-canonical stencils): _supported() == 0 and EINVAL. */
+int gs_newton_F_update_supported(const gs_stencil* S, const gs_level* L);
+int gs_newton_F_update(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* e,
+                       const double* F, double* w_out, double* f, double* partials, hipStream_t stream);
+
+/* dst[i] = src[i] for i < n (Vector3 copy-assignment: NewtonSolver.cpp:12 newtonF = f), non-temporal
+ * streams; the buffers must not overlap unless dst == src. */
+int gs_copy(double* dst, const double* src, int64_t n, hipStream_t stream);
 
 /* y[i] += a*x[i] for i < n (a = +-1 is exact: the reference's Vector3 += / -=). */
 int gs_axpy(double* y, const double* x, double a, int64_t n, hipStream_t stream);

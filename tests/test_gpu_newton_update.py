@@ -1,0 +1,136 @@
+"""findError's newtonV += v fused into the compF that follows it (gs_newton_F_update, NewtonSolver.cpp:105-107
+then :48-81). The one-pass kernel must equal gs_axpy(w, e, 1) + gs_newton_F bit for bit: w_out over the whole
+padded array, f on the interior, every per-block partial and the finished norm. Inside whole Newton solves
+the driver's fused path (default) must leave every level's v / newtonV and the residual history identical
+to the two-pass path (GS_NO_NEWTON_FUSED_UPDATE), which test_gpu_solver.py pins to the reference."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import gpusolve as gsv  # noqa: E402
+from gpusolve.devfield import DevField  # noqa: E402
+
+
+def k():
+    assert torch.cuda.is_available(), "GPU tests need a GPU (no CPU fallback exists)"
+    return gsv.kernels()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ok(rc):
+    assert rc == 0, k().gs_strerror(rc).decode()
+
+
+def interior_random(rng, dims, scale):
+    a = np.zeros(tuple(d + 2 for d in dims))
+    a[1:-1, 1:-1, 1:-1] = rng.uniform(-scale, scale, dims)
+    return a
+
+
+@pytest.mark.parametrize("dims,values", [
+    ((512, 128, 64), (6, -1, -1, -1, -1, -1, -1)),
+    ((300, 150, 71), (6, -1, -1, -1, -1, -1, -1)),  # ragged x-blocks and rows, odd plane count
+    ((260, 130, 130), (6.5, -1.25, -0.75, -1, -1, -1.5, -0.5)),  # non-unit stencil
+    ((512, 64, 130), (6, -1, -1, -1, -1, -1, -1)),
+])  # (the register-blocked pass needs >= 1024 blocks of 4-plane chunks)
+def test_fused_update_equals_axpy_then_compF(dims, values):
+    S = gsv.Stencil(list(values), list(gsv.CANONICAL_OFFSETS)).to_abi()
+    rng = np.random.default_rng(sum(dims))
+    w0, e0 = interior_random(rng, dims, 0.7), interior_random(rng, dims, 0.3)
+    F0 = rng.uniform(-2, 2, tuple(d + 2 for d in dims))  # NONLINEAR rhs: the whole padded array
+    h = 1.0 / (dims[1] + 1)
+    gamma = 1.0
+    w, e, F = DevField(*dims).from_xyz(w0), DevField(*dims).from_xyz(e0), DevField(*dims).from_xyz(F0)
+    L = w.level(h)
+    assert k().gs_newton_F_update_supported(C.byref(S), C.byref(L)) == 1
+    n = k().gs_residual_num_partials(C.byref(S), C.byref(L))
+    # reference sequence: newtonV += v over the span, then compF
+    w_ref = DevField(*dims).from_xyz(w0)
+    f_ref = DevField(*dims, fill=np.nan)
+    p_ref = torch.zeros(n, dtype=torch.float64, device="cuda")
+    ok(k().gs_axpy(w_ref.ptr, e.ptr, 1.0, w_ref.span, stream()))
+    ok(k().gs_newton_F(C.byref(S), C.byref(L), gamma, w_ref.ptr, F.ptr, f_ref.ptr, p_ref.data_ptr(), stream()))
+    # fused: w_out starts as zeros (the driver's vAlt), f as NaN outside what the pass writes
+    w_out = DevField(*dims)
+    f_got = DevField(*dims, fill=np.nan)
+    p_got = torch.full((n,), np.nan, dtype=torch.float64, device="cuda")
+    ok(k().gs_newton_F_update(C.byref(S), C.byref(L), gamma, w.ptr, e.ptr, F.ptr, w_out.ptr, f_got.ptr,
+                              p_got.data_ptr(), stream()))
+    np.testing.assert_array_equal(w_out.to_xyz(), w_ref.to_xyz())
+    np.testing.assert_array_equal(f_got.to_xyz()[1:-1, 1:-1, 1:-1], f_ref.to_xyz()[1:-1, 1:-1, 1:-1])
+    np.testing.assert_array_equal(p_got.cpu().numpy(), p_ref.cpu().numpy())
+    # the operands are read only
+    np.testing.assert_array_equal(w.to_xyz(), w0)
+    np.testing.assert_array_equal(e.to_xyz(), e0)
+
+
+def test_fused_update_refuses_what_it_cannot_run():
+    S = gsv.Stencil([6, -1, -1, -1, -1, -1, -1], list(gsv.CANONICAL_OFFSETS)).to_abi()
+    w = DevField(8, 8, 8)
+    L = w.level(1.0 / 9)
+    assert k().gs_newton_F_update_supported(C.byref(S), C.byref(L)) == 0  # tiny level: the 1-point pass
+    x, y, z = DevField(8, 8, 8), DevField(8, 8, 8), DevField(8, 8, 8)
+    assert k().gs_newton_F_update(C.byref(S), C.byref(L), 1.0, w.ptr, x.ptr, x.ptr, y.ptr, z.ptr, None,
+                                  stream()) == gsv._abi.GS_EINVAL
+    big, b2, b3 = DevField(256, 64, 40), DevField(256, 64, 40), DevField(256, 64, 40)
+    Lb = big.level(1.0 / 65)
+    assert k().gs_newton_F_update_supported(C.byref(S), C.byref(Lb)) == 1
+    # w_out aliasing an operand is refused
+    assert k().gs_newton_F_update(C.byref(S), C.byref(Lb), 1.0, big.ptr, b2.ptr, b3.ptr, big.ptr, b3.ptr, None,
+                                  stream()) == gsv._abi.GS_EINVAL
+
+
+class env:
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        self.old = {k_: os.environ.get(k_) for k_ in self.kw}
+        os.environ.update({k_: str(v) for k_, v in self.kw.items()})
+
+    def __exit__(self, *a):
+        for k_, v in self.old.items():
+            if v is None:
+                del os.environ[k_]
+            else:
+                os.environ[k_] = v
+
+
+def solve(params):
+    with gsv.HipGridData(params) as g:
+        hist = gsv.NewtonSolver.solve(g)
+        fields = {(l, n): g.field(l, n) for l in range(g.numLevels()) for n in ("v", "newtonV", "f")}
+    return hist, fields
+
+
+@pytest.mark.parametrize("dims,pre,post,iters", [((256, 128, 128), 2, 2, 3), ((300, 150, 71), 3, 1, 2),
+                                                 ((64, 64, 64), 2, 2, 2)])  # 64^3: no fused pass
+def test_newton_solve_fused_update_bit_identical(dims, pre, post, iters):
+    p = gsv.GridParams(maxiter=iters, tol=0.0, gridDim=dims, mode=gsv.GS_NEWTON, preSmoothing=pre,
+                       postSmoothing=post)
+    with env(GS_NO_NEWTON_FUSED_UPDATE=1):
+        h_ref, f_ref = solve(p)
+    h_got, f_got = solve(p)
+    assert h_got == h_ref
+    for key, a in f_ref.items():
+        np.testing.assert_array_equal(f_got[key], a, err_msg=str(key))
+
+
+@pytest.mark.parametrize("n,off", [(1 << 20, 0), (1000003, 0), (4097, 1), (0, 0)])
+def test_copy(n, off):
+    """gs_copy (NewtonSolver.cpp:12 newtonF = f): every element, odd lengths, and an 8-B-aligned (not 16-B)
+    operand that takes the hipMemcpyAsync path."""
+    src = torch.randn(n + 2, dtype=torch.float64, device="cuda")
+    dst = torch.full((n + 2,), np.nan, dtype=torch.float64, device="cuda")
+    ok(k().gs_copy(dst.data_ptr() + 8 * off, src.data_ptr() + 8 * off, n, stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(dst[off: off + n], src[off: off + n])
+    assert torch.isnan(dst[off + n:]).all() and torch.isnan(dst[:off]).all()
