@@ -1478,15 +1478,22 @@ __global__ __launch_bounds__(256) void k_rhs(double* __restrict__ f, int mode, d
 
 // dst = src over n doubles (Vector3 copy-assignment): one dwordx4 per thread and iteration, both
 // streams non-temporal (the 1 GB newtonF copy of a 512^3 Newton solve at the box's copy rate instead of
-// hipMemcpyAsync's ~2.7 TB/s); n odd: the last element by thread 0
-__global__ __launch_bounds__(256) void k_copy(double* __restrict__ dst, const double* __restrict__ src, int64_t n)
+// hipMemcpyAsync's ~2.7 TB/s). head (0 or 1) leading elements bring both pointers to 16 B (a field's
+// origin is 8 B past a 16-B boundary); they and an odd tail are copied by thread 0
+__global__ __launch_bounds__(256) void k_copy(double* __restrict__ dst, const double* __restrict__ src, int64_t n,
+                                              int head)
 {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x, n2 = n / 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, n2 = (n - head) / 2;
+    const double* s = src + head;
+    double* d = dst + head;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
-        const double2 t = ld2s<true>(src + 2 * i);
-        st2s<true>(dst + 2 * i, t.x, t.y);
+        const double2 t = ld2s<true>(s + 2 * i);
+        st2s<true>(d + 2 * i, t.x, t.y);
     }
-    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) dst[n - 1] = src[n - 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (head) dst[0] = src[0];
+        if ((n - head) & 1) dst[n - 1] = src[n - 1];
+    }
 }
 
 __global__ __launch_bounds__(256) void k_axpy(double* __restrict__ y, const double* __restrict__ x, double a,
@@ -1902,8 +1909,10 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
 // that column (loads) and sweep 1 of plane z-1 at that column, evaluated lane-parallel one local row per
 // lane (lane j <-> local row j, y-neighbours by lane shifts, x-neighbours loaded) with the same point
 // expression, so every output is bit-identical to two gs_jacobi_sweep calls.
+// TS (diagnostics only, gs_debug_pair_timestamps): es is a buffer of 4 doubles per tile that receives the
+// block's start and end wall clock (100 MHz), its hardware block index and its HW_ID register
 template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0,
-          int PFD = 1, bool XH = false, bool UN = false>
+          int PFD = 1, bool XH = false, bool UN = false, bool TS = false>
 __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* __restrict__ v,
                                                            const double* __restrict__ f, const double* __restrict__ w,
                                                            double* __restrict__ out, double* __restrict__ partials,
@@ -1913,6 +1922,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                                                            int64_t cldy, int64_t cldz, const double* __restrict__ es)
 {
     static_assert(PRO == 0 || (SPEC && !ZV && RY % 2 == 0), "fused prolongation: per-wave code, even RY");
+    static_assert(!TS || (PRO == 0 && !XH), "timestamps: plain pairs (es carries the buffer)");
+    const uint64_t tstart = TS ? wall_clock64() : 0;
     static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR) && MODE != GS_NEWTON && RY + 2 <= WAVE),
                   "column blocks: LINEAR / NONLINEAR pairs, LINEAR prolongation pairs");
     constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
@@ -2373,6 +2384,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             double t = 0.0;
             for (int i = 0; i < 2 * WX; i++) t += red[i];
             partials[tile] = t;
+        }
+    }
+    if constexpr (TS) {
+        if (tid == 0) {
+            double* t = const_cast<double*>(es) + 4 * tile;
+            t[0] = (double)tstart;
+            t[1] = (double)wall_clock64();
+            t[2] = (double)(blockIdx.x + (int64_t)gridDim.x * blockIdx.y);
+            t[3] = (double)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4); // HW_ID: CU / SH / SE
         }
     }
 }

@@ -493,6 +493,39 @@ int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, d
     return launch_status();
 }
 
+// The production LINEAR pair (k_tb2y, PFD 2, plan of gs_jacobi_sweep2 unless zc > 0) with a per-block
+// record in ts (4 doubles per block: start / end wall clock at 100 MHz, hardware block index, HW_ID):
+// how evenly one round of blocks finishes (tools/pair_tail.py)
+int gs_debug_pair_timestamps(const gs_stencil* S, const gs_level* L, double omega, const double* v_in, double* v_out,
+                             const double* f, int zc, double* ts, hipStream_t st)
+{
+    int zcp;
+    dim3 g, b;
+    bool y2 = false, xh = false;
+    if (!S || bad_level(L) || !valid_stencil(S) || !v_in || !v_out || !f || !ts || v_in == v_out || zc < 0 ||
+        !tb2_plan(S, L, &zcp, &g, &b, &y2, GS_LINEAR, &xh) || !y2)
+        return GS_EINVAL;
+    if (zc > 0) {
+        zcp = zc;
+        g.y = (unsigned)((L->nz + zc - 1) / zc);
+    }
+    const Coef k = make_coef(S, L, omega, 0.0);
+#define GS_TSP(U) hipLaunchKernelGGL((k_tb2y<GS_LINEAR, TBY_RY, TBY_WX, true, false, false, true, 0, 2, false, U, true>), g, b, 0, st, k, v_in, f, nullptr, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zcp, 0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0, ts)
+    if (k.unit) GS_TSP(true);
+    else GS_TSP(false);
+#undef GS_TSP
+    return launch_status();
+}
+
+int64_t gs_debug_pair_blocks(const gs_stencil* S, const gs_level* L, int zc)
+{
+    int zcp;
+    dim3 g, b;
+    if (!S || bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zcp, &g, &b, nullptr, GS_LINEAR)) return 0;
+    if (zc > 0) g.y = (unsigned)((L->nz + zc - 1) / zc);
+    return (int64_t)g.x * g.y;
+}
+
 int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
                 double* sink, hipStream_t st)
 {

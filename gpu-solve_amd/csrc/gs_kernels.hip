@@ -466,9 +466,10 @@ int gs_copy(double* dst, const double* src, int64_t n, hipStream_t st)
 {
     if (!dst || !src || n < 0) return GS_EINVAL;
     if (n == 0 || dst == src) return 0;
-    if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) // dwordx4 alignment
+    const uintptr_t a = reinterpret_cast<uintptr_t>(dst), b = reinterpret_cast<uintptr_t>(src);
+    if (((a ^ b) & 15) || (a & 7)) // no common dwordx4 alignment
         return (int)hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToDevice, st);
-    hipLaunchKernelGGL(k_copy, dim3(1024), dim3(256), 0, st, dst, src, n);
+    hipLaunchKernelGGL(k_copy, dim3(1024), dim3(256), 0, st, dst, src, n, (a & 15) ? 1 : 0);
     return launch_status();
 }
 

@@ -50,6 +50,12 @@ int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t
 int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
                 double* sink, hipStream_t stream);
 
+/* The production LINEAR pair with per-block timestamps (4 doubles per block in ts: start and end wall
+ * clock at 100 MHz, hardware block index, HW_ID); zc > 0 overrides the plan's z-chunk. */
+int gs_debug_pair_timestamps(const gs_stencil* S, const gs_level* L, double omega, const double* v_in, double* v_out,
+                             const double* f, int zc, double* ts, hipStream_t stream);
+int64_t gs_debug_pair_blocks(const gs_stencil* S, const gs_level* L, int zc);
+
 #ifdef __cplusplus
 }
 #endif

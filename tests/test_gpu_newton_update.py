@@ -80,8 +80,8 @@ def test_fused_update_refuses_what_it_cannot_run():
     x, y, z = DevField(8, 8, 8), DevField(8, 8, 8), DevField(8, 8, 8)
     assert k().gs_newton_F_update(C.byref(S), C.byref(L), 1.0, w.ptr, x.ptr, x.ptr, y.ptr, z.ptr, None,
                                   stream()) == gsv._abi.GS_EINVAL
-    big, b2, b3 = DevField(256, 64, 40), DevField(256, 64, 40), DevField(256, 64, 40)
-    Lb = big.level(1.0 / 65)
+    big, b2, b3 = DevField(512, 128, 64), DevField(512, 128, 64), DevField(512, 128, 64)
+    Lb = big.level(1.0 / 129)
     assert k().gs_newton_F_update_supported(C.byref(S), C.byref(Lb)) == 1
     # w_out aliasing an operand is refused
     assert k().gs_newton_F_update(C.byref(S), C.byref(Lb), 1.0, big.ptr, b2.ptr, b3.ptr, big.ptr, b3.ptr, None,
@@ -111,7 +111,8 @@ def solve(params):
     return hist, fields
 
 
-@pytest.mark.parametrize("dims,pre,post,iters", [((256, 128, 128), 2, 2, 3), ((300, 150, 71), 3, 1, 2),
+@pytest.mark.parametrize("dims,pre,post,iters", [((255, 127, 127), 2, 2, 3), ((256, 128, 128), 2, 2, 3),
+                                                 ((300, 150, 71), 3, 1, 2),
                                                  ((64, 64, 64), 2, 2, 2)])  # 64^3: no fused pass
 def test_newton_solve_fused_update_bit_identical(dims, pre, post, iters):
     p = gsv.GridParams(maxiter=iters, tol=0.0, gridDim=dims, mode=gsv.GS_NEWTON, preSmoothing=pre,
@@ -119,18 +120,20 @@ def test_newton_solve_fused_update_bit_identical(dims, pre, post, iters):
     with env(GS_NO_NEWTON_FUSED_UPDATE=1):
         h_ref, f_ref = solve(p)
     h_got, f_got = solve(p)
-    assert h_got == h_ref
+    np.testing.assert_array_equal(h_got, h_ref)  # (power-of-two sizes diverge: inf / NaN compare equal here)
     for key, a in f_ref.items():
         np.testing.assert_array_equal(f_got[key], a, err_msg=str(key))
 
 
-@pytest.mark.parametrize("n,off", [(1 << 20, 0), (1000003, 0), (4097, 1), (0, 0)])
-def test_copy(n, off):
-    """gs_copy (NewtonSolver.cpp:12 newtonF = f): every element, odd lengths, and an 8-B-aligned (not 16-B)
-    operand that takes the hipMemcpyAsync path."""
+@pytest.mark.parametrize("n,doff,soff", [(1 << 20, 0, 0), (1000003, 0, 0), (4097, 1, 1), (4096, 1, 1), (1, 1, 1),
+                                          (777, 0, 1), (0, 0, 0)])
+def test_copy(n, doff, soff):
+    """gs_copy (NewtonSolver.cpp:12 newtonF = f): every element and nothing else, for odd lengths, for operands
+    8 B past a 16-B boundary (a field's origin: one head element, then dwordx4) and for operands without a
+    common 16-B alignment (the hipMemcpyAsync path)."""
     src = torch.randn(n + 2, dtype=torch.float64, device="cuda")
     dst = torch.full((n + 2,), np.nan, dtype=torch.float64, device="cuda")
-    ok(k().gs_copy(dst.data_ptr() + 8 * off, src.data_ptr() + 8 * off, n, stream()))
+    ok(k().gs_copy(dst.data_ptr() + 8 * doff, src.data_ptr() + 8 * soff, n, stream()))
     torch.cuda.synchronize()
-    assert torch.equal(dst[off: off + n], src[off: off + n])
-    assert torch.isnan(dst[off + n:]).all() and torch.isnan(dst[:off]).all()
+    assert torch.equal(dst[doff: doff + n], src[soff: soff + n])
+    assert torch.isnan(dst[doff + n:]).all() and torch.isnan(dst[:doff]).all()
