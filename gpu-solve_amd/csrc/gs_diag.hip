@@ -517,6 +517,29 @@ int gs_debug_pair_timestamps(const gs_stencil* S, const gs_level* L, double omeg
     return launch_status();
 }
 
+// Timing only: the production LINEAR pair marching the planes in descending order (reverse != 0: every
+// field viewed through plane nz + 1 - z, a negative plane pitch). The z-terms then enter the stencil sum
+// swapped, so the values are NOT the sweep's; the launch moves the same bytes in the opposite plane
+// order (tools/mall_probe.py: does a launch that starts where its predecessor ended find those planes in
+// the Infinity Cache?)
+int gs_debug_pair_reverse(const gs_stencil* S, const gs_level* L, double omega, const double* v_in, double* v_out,
+                          const double* f, int reverse, hipStream_t st)
+{
+    int zc;
+    dim3 g, b;
+    bool y2 = false, xh = false;
+    if (!S || bad_level(L) || !valid_stencil(S) || !v_in || !v_out || !f || v_in == v_out ||
+        !tb2_plan(S, L, &zc, &g, &b, &y2, GS_LINEAR, &xh) || !y2)
+        return GS_EINVAL;
+    const Coef k = make_coef(S, L, omega, 0.0);
+    const int64_t sh = reverse ? (L->nz + 1) * L->ldz : 0, ldz = reverse ? -L->ldz : L->ldz;
+#define GS_RVP(U) hipLaunchKernelGGL((k_tb2y<GS_LINEAR, TBY_RY, TBY_WX, true, false, false, true, 0, 2, false, U>), g, b, 0, st, k, v_in + sh, f + sh, nullptr, v_out + sh, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, ldz, zc, 0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0, nullptr)
+    if (k.unit) GS_RVP(true);
+    else GS_RVP(false);
+#undef GS_RVP
+    return launch_status();
+}
+
 int64_t gs_debug_pair_blocks(const gs_stencil* S, const gs_level* L, int zc)
 {
     int zcp;

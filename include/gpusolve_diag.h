@@ -56,6 +56,11 @@ int gs_debug_pair_timestamps(const gs_stencil* S, const gs_level* L, double omeg
                              const double* f, int zc, double* ts, hipStream_t stream);
 int64_t gs_debug_pair_blocks(const gs_stencil* S, const gs_level* L, int zc);
 
+/* Timing only: the production LINEAR pair with the planes marched in descending order (reverse != 0; the
+ * z-terms enter the sum swapped, so the values are not the sweep's). */
+int gs_debug_pair_reverse(const gs_stencil* S, const gs_level* L, double omega, const double* v_in, double* v_out,
+                          const double* f, int reverse, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
