@@ -532,10 +532,16 @@ int gs_debug_pair_reverse(const gs_stencil* S, const gs_level* L, double omega, 
         !tb2_plan(S, L, &zc, &g, &b, &y2, GS_LINEAR, &xh) || !y2)
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, 0.0);
-    const int64_t sh = reverse ? (L->nz + 1) * L->ldz : 0, ldz = reverse ? -L->ldz : L->ldz;
-#define GS_RVP(U) hipLaunchKernelGGL((k_tb2y<GS_LINEAR, TBY_RY, TBY_WX, true, false, false, true, 0, 2, false, U>), g, b, 0, st, k, v_in + sh, f + sh, nullptr, v_out + sh, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, ldz, zc, 0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0, nullptr)
-    if (k.unit) GS_RVP(true);
-    else GS_RVP(false);
+    const int64_t sh = (reverse & 1) ? (L->nz + 1) * L->ldz : 0, ldz = (reverse & 1) ? -L->ldz : L->ldz;
+#define GS_RVP(U, NT) hipLaunchKernelGGL((k_tb2y<GS_LINEAR, TBY_RY, TBY_WX, NT, false, false, true, 0, 2, false, U>), g, b, 0, st, k, v_in + sh, f + sh, nullptr, v_out + sh, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, ldz, zc, 0, 0, nullptr, nullptr, 0, 0, 0, (int64_t)0, (int64_t)0, nullptr)
+    // reverse bit 1: ordinary (not non-temporal) stores of the output
+    if (reverse & 2) {
+        if (k.unit) GS_RVP(true, false);
+        else GS_RVP(false, false);
+    } else {
+        if (k.unit) GS_RVP(true, true);
+        else GS_RVP(false, true);
+    }
 #undef GS_RVP
     return launch_status();
 }

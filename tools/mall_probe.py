@@ -32,23 +32,24 @@ def main():
     L = v.level(1.0 / (n + 1))
     st = torch.cuda.current_stream().cuda_stream
 
-    def run(alternate):
+    def run(key):
+        alternate, cached = "alternating" in key, "cached" in key
         src, dst = v, w
         for i in range(a.pairs):
             rc = kd.gs_debug_pair_reverse(C.byref(S), C.byref(L), 0.8, src.ptr, dst.ptr, f.ptr,
-                                          1 if (alternate and i % 2) else 0, st)
+                                          (1 if (alternate and i % 2) else 0) | (2 if cached else 0), st)
             assert rc == 0, rc
             src, dst = dst, src
 
-    res = {"ascending": [], "alternating": []}
+    res = {"ascending": [], "alternating": [], "ascending cached-stores": [], "alternating cached-stores": []}
     for _ in range(2):
-        run(False)
-        run(True)
+        for key in res:
+            run(key)
     for _ in range(a.rounds):
         for key in res:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            run(key == "alternating")
+            run(key)
             e1.record()
             torch.cuda.synchronize()
             res[key].append(e0.elapsed_time(e1) / a.pairs)
