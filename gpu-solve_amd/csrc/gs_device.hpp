@@ -1924,7 +1924,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     static_assert(PRO == 0 || (SPEC && !ZV && RY % 2 == 0), "fused prolongation: per-wave code, even RY");
     static_assert(!TS || (PRO == 0 && !XH), "timestamps: plain pairs (es carries the buffer)");
     const uint64_t tstart = TS ? wall_clock64() : 0;
-    static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR) && MODE != GS_NEWTON && RY + 2 <= WAVE),
+    static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR) && RY + 2 <= WAVE),
                   "column blocks: LINEAR / NONLINEAR pairs, LINEAR prolongation pairs");
     constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
     constexpr int NE = NV + RY; // x-edge values per wave side: v rows 0..RY, sweep-1 rows 1..RY
@@ -2014,6 +2014,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // XH edge column: v at plane z+1 (EA), its x-neighbours (EXm, EXp) and f at plane z, per slot;
     // EP / EC: v at planes z-1 / z; ES1c: sweep 1 at plane z-1
     double EA[XH ? NS : 1], EXm[XH ? NS : 1], EXp[XH ? NS : 1], EF[XH ? NS : 1], EP = 0.0, EC = 0.0, ES1c = 0.0;
+    double EW[(XH && MODE == GS_NEWTON) ? NS : 1]; // NEWTON: newtonV at the edge column, plane z
     auto load_slot = [&](const int s, const int z, const int zv) {
 #pragma unroll
         for (int j = 0; j < NV; j++) {
@@ -2034,6 +2035,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                     EXp[s] = ldv1<ZV>(eat(v, 1, z));
                 }
                 EF[s] = *eat(f, 0, z);
+                if constexpr (MODE == GS_NEWTON) EW[s] = *eat(w, 0, z);
             }
         }
     };
@@ -2234,8 +2236,16 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         const double c = EC;
                         const double lm = lane_from_left<true>(EC, 0.0), lp = lane_from_right<true>(EC, 0.0);
                         const double ym = M ? lp : lm, yp = M ? lm : lp;
-                        const double a = op_value<MODE, UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP, 0.0);
-                        const double nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
+                        double nv;
+                        if constexpr (MODE == GS_NEWTON) { // the interior rows' NEWTON expressions, exp once
+                            const double we = EW[cs], A = k.gamma * (1 + we), E = exp(we);
+                            const double a = newton_op(div_hh(k, stencil_sum<UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP)),
+                                                       c, A, E);
+                            nv = newton_update(k, c, EF[cs] - a, A, E);
+                        } else {
+                            const double a = op_value<MODE, UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP, 0.0);
+                            nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
+                        }
                         ES1n = (!pz || !erowc) ? c : nv;
                     }
                 }
@@ -2500,7 +2510,10 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
 {
     if (!S || !L || !canonical_order(S) || L->nx < 1 || L->ny < 1 || L->nz < 1) return 0;
     const bool two = L->nx <= 2 * WAVE * TBY_WX;
-    const bool colb = !two && mode != GS_NEWTON && xh_enabled() && L->nx <= (int64_t)1 << 20;
+    // NEWTON: column blocks only where k_tb2 has no shape (rows > 1024 points): the NEWTON column-block pair
+    // carries the edge column's newtonV too and spills (~45 VGPRs), k_tb2 does not
+    const bool colb = !two && xh_enabled() && L->nx <= (int64_t)1 << 20 &&
+                      (mode != GS_NEWTON || L->nx > 2 * WAVE * TB_WX_B);
     if (!two && !colb && L->nx > 2 * WAVE * TB_WX_B) return 0;
     const int64_t nh = colb ? (L->nx + 2 * WAVE * TBY_WX - 1) / (2 * WAVE * TBY_WX) : 1;
     const int rows = (two || colb) ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block

@@ -122,7 +122,9 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
             if (zv) GS_TBX(GS_LINEAR, true, 1);
             else if (tbx_pfd2()) GS_TBX(GS_LINEAR, false, 2);
             else GS_TBX(GS_LINEAR, false, 1);
-        } else GS_TBX(GS_NONLINEAR, false, 1);
+        } else if (mode == GS_NONLINEAR) GS_TBX(GS_NONLINEAR, false, 1);
+        else if (zv) GS_TBX(GS_NEWTON, true, 1);
+        else GS_TBX(GS_NEWTON, false, 1);
     } else if (y2) {
         if (mode == GS_LINEAR) {
             if (zv) GS_TBY(GS_LINEAR, true);

@@ -137,3 +137,23 @@ def test_copy(n, doff, soff):
     torch.cuda.synchronize()
     assert torch.equal(dst[doff: doff + n], src[soff: soff + n])
     assert torch.isnan(dst[doff + n:]).all() and torch.isnan(dst[:doff]).all()
+
+
+@pytest.mark.parametrize("dims", [(1100, 20, 18), (700, 12, 10)])
+def test_newton_long_rows_vs_oracle(dims):
+    """NEWTON on rows of more than 512 points: k_tb2 up to 1024, column-block pairs beyond (r03), against the
+    CPU oracle (pinned to src/cpu); 1e-10 on newtonV (ocml vs glibc exp), 1e-9 on the history."""
+    import oracle as O
+    from conftest import rel
+    og = O.Grid(dims, mode=2, maxiter=2, omega=0.8, gamma=1.0, pre=2, post=2)
+    oh = og.solve()
+    ref = og.field(0, "newtonV").copy()
+    p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=gsv.GS_NEWTON, preSmoothing=2, postSmoothing=2)
+    with gsv.HipGridData(p) as g:
+        hist = gsv.NewtonSolver.solve(g)
+        got = g.field(0, "newtonV")
+    assert len(hist) == len(oh)
+    scale = max(np.abs(ref).max(), 1e-300)
+    assert np.abs(got - ref).max() <= 1e-10 * scale
+    for a, b in zip(hist, oh):
+        assert rel(a, b) < 1e-9, (a, b)

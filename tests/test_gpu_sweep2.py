@@ -56,15 +56,14 @@ def two_sweeps(v0, f0, w0, mode, h):
 
 SHAPES = [(1, 1, 1), (2, 5, 3), (5, 4, 33), (127, 9, 17), (128, 8, 8), (129, 13, 40), (257, 6, 10), (500, 7, 9),
           (512, 4, 5), (513, 5, 6), (1024, 3, 4), (64, 64, 64), (200, 33, 70),
-          # rows > 512 points: column blocks (k_tb2y XH) in LINEAR / NONLINEAR mode, k_tb2 in NEWTON mode
+          # rows > 512 points: column blocks (k_tb2y XH) in LINEAR / NONLINEAR mode, k_tb2 in NEWTON mode up to
+          # 1024 points and NEWTON column blocks beyond (r03)
           (700, 9, 11), (1024, 16, 12), (1025, 7, 9), (1536, 5, 6), (2000, 3, 5)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_sweep2_equals_two_sweeps(shape, mode):
-    if shape[0] > 1024 and mode == 2:
-        pytest.skip("NEWTON pairs stop at 1024-point rows")
     rng = np.random.default_rng(abs(hash((shape, mode))) % 2**32)
     nx, ny, nz = shape
     h = 1.0 / (ny + 1)
@@ -82,8 +81,6 @@ def test_sweep2_equals_two_sweeps(shape, mode):
 @pytest.mark.parametrize("lo,hi", [(1, 9), (5, 14), (12, 22), (3, 3), (10, 11)])
 @pytest.mark.parametrize("mode", [0, 2])
 def test_sweep2_on_slab_with_two_ghost_planes(lo, hi, mode, nx):
-    if nx > 1024 and mode == 2:
-        pytest.skip("NEWTON pairs stop at 1024-point rows")
     rng = np.random.default_rng(lo * 100 + hi)
     ny, NZ = 11, 22
     h = 1.0 / (ny + 1)
@@ -112,13 +109,17 @@ def test_sweep2_on_slab_with_two_ghost_planes(lo, hi, mode, nx):
 def test_sweep2_rejects_unsupported():
     v = DevField(1030, 3, 4)
     L = v.level(0.25)
-    # rows > 1024 points: column blocks in LINEAR / NONLINEAR mode, nothing in NEWTON mode
-    assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(L)) == 0
-    assert k().gs_jacobi_sweep2_supported_mode(C.byref(stencil()), C.byref(L), 0) >= 1
-    assert k().gs_jacobi_sweep2_supported_mode(C.byref(stencil()), C.byref(L), 2) == 0
+    # rows > 1024 points: column blocks in every mode (NEWTON since r03)
+    assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(L)) >= 1
+    for mode in (0, 1, 2):
+        assert k().gs_jacobi_sweep2_supported_mode(C.byref(stencil()), C.byref(L), mode) >= 1
+        assert "XH" in k().gs_jacobi_sweep2_kernel(C.byref(stencil()), C.byref(L), mode).decode()
+    # NEWTON needs newtonV; a non-canonical stencil order has no pair at all
     rc = k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 2, 0.8, 1.0, v.ptr, DevField(1030, 3, 4).ptr, v.ptr,
-                              v.ptr, 0, 0, st())
+                              None, 0, 0, st())
     assert rc == gsv._abi.GS_EINVAL
+    perm = gsv.Stencil([6, -1, -1, -1, -1, -1, -1], [gsv.CANONICAL_OFFSETS[i] for i in (0, 2, 1, 3, 4, 5, 6)]).to_abi()
+    assert k().gs_jacobi_sweep2_supported(C.byref(perm), C.byref(L)) == 0
     big = DevField(512, 512, 64)
     assert k().gs_jacobi_sweep2_supported(C.byref(stencil()), C.byref(big.level(1 / 513))) == 2
 
@@ -128,8 +129,6 @@ def test_sweep2_rejects_unsupported():
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_sweep2_norm_partials(shape, mode):
     """gs_jacobi_sweep2_norm: same output as the plain pair, and its partials sum to ||f - A v_in||^2."""
-    if shape[0] > 1024 and mode == 2:
-        pytest.skip("NEWTON pairs stop at 1024-point rows")
     rng = np.random.default_rng(sum(shape) * 7 + mode)
     nx, ny, nz = shape
     h = 1.0 / (ny + 1)
@@ -153,7 +152,7 @@ def test_sweep2_norm_partials(shape, mode):
     assert abs(got - want) <= 1e-12 * abs(want)
 
 
-@pytest.mark.parametrize("shape", [(5, 4, 33), (129, 13, 40), (512, 6, 5), (64, 64, 64), (1024, 6, 5)])
+@pytest.mark.parametrize("shape", [(5, 4, 33), (129, 13, 40), (512, 6, 5), (64, 64, 64), (1024, 6, 5), (1100, 7, 6)])
 @pytest.mark.parametrize("mode", [0, 2])
 def test_zero_iterate_sweeps(shape, mode):
     """v_in = NULL (the coarse levels' v = 0 after restriction) is bit-identical to a zeroed v_in,
