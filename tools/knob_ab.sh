@@ -7,6 +7,6 @@ for r in $(seq 1 $R); do
   for v in "$@"; do
     env $VAR=$v timeout -k 10 200 python bench.py --steps 20 --warmup 5 --vcycles 10 --cpu-sweeps 0 --newton-iters 0 \
       --config5 0 > $O/b_${v}_r$r.json 2> $O/b_${v}_r$r.err || { tail $O/b_${v}_r$r.err; exit 1; }
-    python -c "import json; d=json.load(open('$O/b_${v}_r$r.json')); print('$VAR=$v r$r', 'GLUPS', round(d['value']/1e3,1), 'pair_ms', d['roofline']['kernel_ms'], 'frac', d['roofline']['frac'], 'vcycle', d['vcycle']['ms'])"
+    python -c "import json; d=json.load(open('$O/b_${v}_r$r.json')); k=d['vcycle']['level0_kernels']; print('$VAR=$v r$r', 'GLUPS', round(d['value']/1e3,1), 'pair_ms', d['roofline']['kernel_ms'], 'frac', d['roofline']['frac'], 'vcycle', d['vcycle']['ms'], 'rr2', k['residual_restrict']['ms'], 'pro', k['prolong_pair']['ms'])"
   done
 done
