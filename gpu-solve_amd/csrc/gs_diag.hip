@@ -460,7 +460,9 @@ const PairVariant kPairVariants[] = {GS_PVF(2, 4),
                                      GS_PVY(3, false, true, " f-cached spec"),
                                      GS_PVY(3, true, false, " f-nt"),
                                      {"tb2y ry2 wx4 wy2 f-cached spec pfd2", 2, 4, 2,
-                                      k_tb2y<GS_LINEAR, 2, 4, true, false, false, true, 0, 2>}};
+                                      k_tb2y<GS_LINEAR, 2, 4, true, false, false, true, 0, 2>},
+                                     {"tb2y ry2 wx4 wy2 f-nt spec pfd2", 2, 4, 2,
+                                      k_tb2y<GS_LINEAR, 2, 4, true, true, false, true, 0, 2>}};
 #undef GS_PVY
 #undef GS_PVF
 #undef GS_PV
