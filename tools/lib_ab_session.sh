@@ -1,15 +1,15 @@
 #!/bin/bash
 # Interleaved A/B of two builds of the kernel library on the headline bench (and optionally Newton): the
 # alternative libgpusolve_hip.so is built here into gpu-solve_amd/lib_alt/ and swapped in between runs.
-#   tools/lib_ab_session.sh <tag> [rounds] [newton-iters]        (through gpurun, from the repo root)
+#   tools/lib_ab_session.sh <tag> [rounds] [newton-iters] [alt .so]   (through gpurun, from the repo root)
 set -o pipefail
-O=gpurun_out/${1:-libab}; R=${2:-3}; NI=${3:-0}; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/${1:-libab}; R=${2:-3}; NI=${3:-0}; ALT=${4:-gpu-solve_amd/lib_alt/libgpusolve_hip.so}; mkdir -p $O; export TMPDIR=/tmp
 L=gpu-solve_amd/lib
 cp $L/libgpusolve_hip.so $O/new.so
 restore() { cp $O/new.so $L/libgpusolve_hip.so; }
 for r in $(seq 1 $R); do
   for v in new alt; do
-    if [ $v = new ]; then cp $O/new.so $L/libgpusolve_hip.so; else cp gpu-solve_amd/lib_alt/libgpusolve_hip.so $L/libgpusolve_hip.so; fi
+    if [ $v = new ]; then cp $O/new.so $L/libgpusolve_hip.so; else cp $ALT $L/libgpusolve_hip.so; fi
     timeout -k 10 300 python bench.py --steps 20 --warmup 5 --vcycles 10 --cpu-sweeps 0 --newton-iters $NI --config5 0 \
       > $O/b_${v}_r$r.json 2> $O/b_${v}_r$r.err || { restore; tail $O/b_${v}_r$r.err; exit 1; }
     python -c "
