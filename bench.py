@@ -412,6 +412,18 @@ def main():
 
     n = a.size
     dims = global_dims(n, world)
+    # N=8 on config #5's grid: rank 0 first times the same 1024^3 grid on its own GPU, in this job and on
+    # this node, before any rank builds its slab (the other ranks wait): the same-job denominator of
+    # speedup_vs_1gpu_same_grid, beside the committed driver record's
+    c5_same_job = None
+    if world > 1 and tuple(dims) == (1024, 1024, 1024) and a.config5:
+        if rank == 0:
+            try:
+                c5_same_job = config5_single_gpu(a.steps, 0)
+            except Exception as e:  # noqa: BLE001 (reported, never required)
+                c5_same_job = {"error": f"{type(e).__name__}: {e}"}
+            torch.cuda.synchronize()
+        barrier()
     params = gsv.GridParams(maxiter=1, tol=0.0, gridDim=dims, mode=gsv.GS_LINEAR, preSmoothing=2,
                             postSmoothing=2)
     grid = make_grid(params, rank, world)
@@ -468,11 +480,12 @@ def main():
         except Exception:  # noqa: BLE001 (diagnostic only)
             local = float("nan")
         import ctypes as C
-        hms, hcalls = C.c_double(), C.c_int64()
+        hms, hcalls, hmax = C.c_double(), C.c_int64(), C.c_double()
         drv.gs_grid_comm_stats(grid.handle, C.byref(hms), C.byref(hcalls))
+        drv.gs_grid_comm_stats_max(grid.handle, C.byref(hmax))
         halo_us = hms.value / max(1, hcalls.value) * 1e3
-        per = torch.tensor([own_elapsed / a.steps * 1e3, kernel_ms, local, halo_us], dtype=torch.float64,
-                           device="cuda")
+        per = torch.tensor([own_elapsed / a.steps * 1e3, kernel_ms, local, halo_us, hmax.value * 1e3],
+                           dtype=torch.float64, device="cuda")
         allp = [torch.zeros_like(per) for _ in range(world)]
         dist.all_gather(allp, per)
         rows = [x.tolist() for x in allp]
@@ -483,11 +496,15 @@ def main():
                  "rank_pair_ms_no_exchange": [fin(r[2]) for r in rows],
                  "exchange_ms_per_pair_max": fin(max(gaps)) if gaps else None,
                  "rank_halo_host_us_per_call": [fin(r[3]) for r in rows],
+                 "rank_halo_host_us_max": [fin(r[4]) for r in rows],
+                 "rccl_ctas": int(os.environ.get("GS_RCCL_CTAS", "0") or 0) or "default (gs_comm.cpp)",
                  "note": "rank_pair_ms: the overlapped pair (boundary planes, RCCL ghost exchange, interior) "
                          "per launch on each rank's compute stream; _no_exchange: the same pair on the same "
-                         "slab run locally, no exchange; rank_halo_host_us_per_call: host wall time inside one "
-                         "ghost exchange call (RCCL group issue + settle), averaged over every call so far; the "
-                         "interior launch is enqueued before it"}
+                         "slab run locally, no exchange; rank_halo_host_us_per_call / _max: host wall time of "
+                         "one ghost exchange (RCCL group issue, polls and settle), mean and maximum over every "
+                         "exchange so far; in a sequence of sweeps an exchange is settled only before the next "
+                         "boundary planes, after the next interior is already enqueued when it is still in "
+                         "flight"}
 
     single = ceiling = None
     if world == 1:
@@ -546,15 +563,31 @@ def main():
             c5 = {"error": f"{type(e).__name__}: {e}"}
     speedup = None
     if world > 1 and tuple(dims) == (1024, 1024, 1024):
+        # strong scaling on 1024^3 (north_star's >= 6x): this line's MLUPS over one GPU's on the same grid.
+        # "value" divides by rank 0's same-job measurement (same node, same run) when it exists, else by
+        # the driver's committed N=1 record; both ratios are reported
+        speedup = {"scaling": "strong", "note": "this line's MLUPS / one GPU's MLUPS on the same 1024^3 grid "
+                                                "(bench.py config5_single_gpu)"}
         try:
             with open(CONFIG5_FILE) as f:
                 ref1 = json.load(f)
-            speedup = {"value": round(value / float(ref1["mlups"]), 3), "one_gpu_mlups": ref1["mlups"],
-                       "one_gpu_source": os.path.relpath(CONFIG5_FILE, REPO) + " (" + ref1.get("source", "?") + ")",
-                       "note": "strong scaling on 1024^3: this line's MLUPS / one GPU's MLUPS on the same grid "
-                               "(bench.py N=1 config5_single_gpu)"}
+            speedup["vs_driver_record"] = round(value / float(ref1["mlups"]), 3)
+            speedup["driver_record_mlups"] = ref1["mlups"]
+            speedup["driver_record_source"] = (os.path.relpath(CONFIG5_FILE, REPO) + " (" + ref1.get("source", "?")
+                                               + ")")
         except (OSError, ValueError, KeyError) as e:
-            speedup = {"error": str(e)}
+            speedup["driver_record_error"] = str(e)
+        if c5_same_job and "mlups" in c5_same_job:
+            speedup["value"] = round(value / float(c5_same_job["mlups"]), 3)
+            speedup["one_gpu_mlups"] = c5_same_job["mlups"]
+            speedup["one_gpu_source"] = "same job: rank 0's GPU, before the slabs were built"
+            speedup["one_gpu_pair_kernel_ms"] = c5_same_job.get("pair_kernel_ms")
+        elif "vs_driver_record" in speedup:
+            speedup["value"] = speedup["vs_driver_record"]
+            speedup["one_gpu_mlups"] = speedup["driver_record_mlups"]
+            speedup["one_gpu_source"] = speedup["driver_record_source"]
+            if c5_same_job:
+                speedup["same_job_error"] = c5_same_job.get("error")
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sweeps > 0:

@@ -319,6 +319,13 @@ int gs_grid_comm_stats(void* grid, double* halo_host_ms, int64_t* halo_calls)
     });
 }
 
+int gs_grid_comm_stats_max(void* grid, double* halo_host_max_ms)
+{
+    return guarded([&] {
+        if (halo_host_max_ms) *halo_host_max_ms = G(grid).haloHostMaxMs;
+    });
+}
+
 int gs_grid_time_jacobi(void* grid, int level, int warmup, int sweeps, float* ms)
 {
     return guarded([&] {

@@ -1,6 +1,7 @@
 // gs_comm.cpp — Z-slab plan, RCCL communicator, single-device loopback communicator.
 #include "gs_comm.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +18,11 @@
 namespace gs {
 
 namespace {
+// RCCL's workgroups per exchange group (ncclConfig_t::minCTAs = maxCTAs; GS_RCCL_CTAS overrides): the
+// stand-in exchange at RCCL's kernel footprint finishes the overlapped config #5 slab step sooner with more
+// workgroups (tools/exchange_probe.py)
+constexpr int kRcclCtasDefault = 32;
+
 void hipOk(hipError_t e, const char* what)
 {
     if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e));
@@ -46,6 +52,10 @@ public:
         std::memcpy(&id, uid, sizeof(id));
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.blocking = 0;
+        if (const int ctas = rcclCtas(); ctas > 0) {
+            cfg.minCTAs = ctas;
+            cfg.maxCTAs = ctas;
+        }
         const ncclResult_t e = ncclCommInitRankConfig(&c_, nranks, id, rank, &cfg);
         if (e != ncclSuccess && e != ncclInProgress) {
             if (c_) (void)ncclCommAbort(c_);
@@ -63,6 +73,13 @@ public:
 
     void halo(double* field, int64_t ldz, int64_t nzl, int depth, hipStream_t s) override
     {
+        haloIssue(field, ldz, nzl, depth, s);
+        haloSettle();
+    }
+
+    void haloIssue(double* field, int64_t ldz, int64_t nzl, int depth, hipStream_t s) override
+    {
+        haloSettle(); // (one exchange in flight at a time)
         if (n_ == 1) return;
         const size_t cnt = (size_t)(depth * ldz);
         call(ncclGroupStart(), "ncclGroupStart");
@@ -75,11 +92,28 @@ public:
             call(ncclRecv(field + (nzl + 1) * ldz, cnt, ncclDouble, r_ + 1, c_, s), "ncclRecv");
         }
         call(ncclGroupEnd(), "ncclGroupEnd");
+        pending_ = true;
+    }
+
+    bool haloReady() override
+    {
+        if (!pending_) return true;
+        const int a = asyncState(false);
+        if (a > 1) abortAndThrow(std::string("halo exchange: ") + ncclGetErrorString((ncclResult_t)(a - 2)));
+        if (a == 0) pending_ = false;
+        return !pending_;
+    }
+
+    void haloSettle() override
+    {
+        if (!pending_) return;
+        pending_ = false;
         settle("halo exchange", timeout_);
     }
 
     void allgather1(const double* in, double* out, hipStream_t s) override
     {
+        haloSettle();
         call(ncclAllGather(in, out, 1, ncclDouble, c_, s), "ncclAllGather");
         settle("ncclAllGather", timeout_);
     }
@@ -87,6 +121,7 @@ public:
     void gatherPlanes(double* field, int64_t ldz, const std::vector<int64_t>& lo, const std::vector<int64_t>& hi,
                       hipStream_t s) override
     {
+        haloSettle();
         call(ncclGroupStart(), "ncclGroupStart");
         for (int q = 0; q < n_; q++) {
             if (hi[q] < lo[q]) continue;
@@ -99,10 +134,12 @@ public:
 
     void sync(hipStream_t s) override
     {
+        haloSettle();
         wait([&] { return hipStreamQuery(s); }, "stream sync");
     }
     void syncEvent(hipEvent_t e) override
     {
+        haloSettle();
         wait([&] { return hipEventQuery(e); }, "event sync");
     }
 
@@ -168,7 +205,17 @@ private:
     ncclComm_t c_ = nullptr;
     long injectAt_ = 0, calls_ = 0;
     double timeout_ = 120.0;
+    bool pending_ = false; // an issued halo exchange not yet settled
 };
+
+int rcclCtas()
+{
+    static const int n = [] {
+        const char* e = std::getenv("GS_RCCL_CTAS");
+        return e && *e ? std::max(0, std::atoi(e)) : kRcclCtasDefault;
+    }();
+    return n;
+}
 
 std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid)
 {

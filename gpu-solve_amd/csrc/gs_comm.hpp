@@ -32,6 +32,17 @@ public:
     // plane 0 and rank+1's bottom plane into plane nzl+1. depth 2 (nzl >= 2): the two outermost
     // planes each way, into planes -1..0 and nzl+1..nzl+2. Asynchronous on s.
     virtual void halo(double* field, int64_t ldz, int64_t nzl, int depth, hipStream_t s) = 0;
+    // halo() in two halves, for RCCL's non-blocking group: haloIssue() starts the exchange and returns;
+    // its kernels are on s once haloSettle() has returned (the communicator settles a pending exchange
+    // itself before any other call). haloReady(): one poll, true once it has settled. Work that must
+    // follow the exchange on s (an event record) is enqueued only after haloSettle(). The default
+    // (loopback, trace) settles inside haloIssue().
+    virtual void haloIssue(double* field, int64_t ldz, int64_t nzl, int depth, hipStream_t s)
+    {
+        halo(field, ldz, nzl, depth, s);
+    }
+    virtual bool haloReady() { return true; }
+    virtual void haloSettle() {}
     // out[r] <- rank r's *in, on every rank (out holds size() doubles). Asynchronous on s.
     virtual void allgather1(const double* in, double* out, hipStream_t s) = 0;
     // field: a full-size level on every rank; rank r has computed planes [lo[r], hi[r]]; afterwards
@@ -52,8 +63,12 @@ public:
 // call are settled by polling ncclCommGetAsyncError under a deadline (GS_COMM_INIT_TIMEOUT_S, default
 // 300 s; GS_COMM_TIMEOUT_S, default 120 s, also for sync()). On an error or a timeout the communicator
 // is aborted (ncclCommAbort) and gs::Error("RCCL ... (rank r of n)") is thrown. GS_COMM_INJECT_ERROR=k
-// (tests) makes the k-th settle or sync of the communicator see ncclInternalError.
+// (tests) makes the k-th settle or sync of the communicator see ncclInternalError. GS_RCCL_CTAS=n (read once,
+// at creation) sets ncclConfig_t::minCTAs = maxCTAs = n: the workgroups RCCL's kernels take for a
+// send/recv group, which share the CUs with the interior sweep they overlap (0: RCCL's own choice).
 std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid);
+// the CTA budget makeRcclComm gives a communicator (GS_RCCL_CTAS, else the default below; 0: RCCL's)
+int rcclCtas();
 void rcclUniqueId(void* uid);
 
 // The rank-0 id file hand-off (publishUid / awaitUid / uidPath), the bounded wait and the loopback

@@ -143,6 +143,8 @@ LevelClock::~LevelClock()
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
 }
 
+int64_t proWsElems(const HipGridData& g, std::size_t l); // below
+
 // ---------------------------------------------------------------------------------------------
 // Level hierarchy: L = floor(log2(min dim)) + 1, dims halve per level, h_l = 1/(ny_l+1)
 // (src/cpu/CpuGridData.cpp:19-41). Fields a mode never touches are not allocated.
@@ -175,6 +177,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         sw.newtonFusedUpdate = !on("GS_NO_NEWTON_FUSED_UPDATE");
         if (const char* e = std::getenv("GS_NEWTON_PRO_POINTS")) sw.newtonProPoints = std::strtoll(e, nullptr, 10);
         if (const char* e = std::getenv("GS_TILE_POINTS")) sw.tilePoints = std::strtoll(e, nullptr, 10);
+        if (const char* e = std::getenv("GS_HALO_ORDER")) sw.haloOrder = std::atoi(e);
     }
     std::vector<int64_t> nzs, pts;
     for (int l = 0; l < nlev; l++) {
@@ -275,6 +278,14 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
     check(gs_rhs_init(&levels_[0].geom, levels_[0].f.data(), (int)mode, 1.0 / (gridDim[1] + 1), gamma, s),
           "gs_rhs_init");
     halo(levels_[0], levels_[0].f, s); // the fused pair's first sweep reads f on a ghost plane
+    // the fused prolongation pair's edge-column workspaces (column-block rows), one per stream, at their
+    // largest size now: proPlanes never reallocates them
+    for (int l = 0; l + 1 < nlev; l++) {
+        const int64_t need = proWsElems(*this, (std::size_t)l);
+        if (need <= 0) continue;
+        levels_[l].proWs[0].get(need);
+        if (bndStream_.s) levels_[l].proWs[1].get(need);
+    }
     check((int)hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
@@ -362,10 +373,50 @@ void HipGridData::halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth)
         rec("halo", {{"L", (long long)levelIndex(L)}, {"depth", depth}}, fieldName(L, fld));
         return;
     }
+    haloSettle(); // (an exchange of the pipelined sequence is settled before anything else is issued)
     // host cost of issuing + settling the exchange (RCCL: group start/end and the async-error poll)
     const auto t0 = std::chrono::steady_clock::now();
     comm_->halo(fld.data(), fld.ldz(), L.geom.nz, depth, s);
-    haloHostMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    haloHostMs += ms;
+    haloHostMaxMs = std::max(haloHostMaxMs, ms);
+    haloCalls++;
+}
+
+void HipGridData::haloIssue(LevelData& L, DeviceField& fld, hipStream_t s, int depth)
+{
+    if (!(L.distributed && nranks() > 1)) return;
+    if (trace) {
+        rec("halo", {{"L", (long long)levelIndex(L)}, {"depth", depth}}, fieldName(L, fld));
+        return;
+    }
+    haloSettle();
+    const auto t0 = std::chrono::steady_clock::now();
+    comm_->haloIssue(fld.data(), fld.ldz(), L.geom.nz, depth, s);
+    haloCurMs_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    haloPending_ = true;
+}
+
+bool HipGridData::haloReady()
+{
+    if (trace) return sw.haloOrder != 1;
+    if (!haloPending_) return sw.haloOrder != 1;
+    const auto t0 = std::chrono::steady_clock::now();
+    const bool ok = comm_->haloReady();
+    haloCurMs_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (sw.haloOrder == 1) return false;
+    return sw.haloOrder == 2 || ok;
+}
+
+void HipGridData::haloSettle()
+{
+    if (!haloPending_) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    comm_->haloSettle();
+    haloCurMs_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    haloPending_ = false;
+    haloHostMs += haloCurMs_;
+    haloHostMaxMs = std::max(haloHostMaxMs, haloCurMs_);
     haloCalls++;
 }
 
@@ -465,16 +516,38 @@ void proPlanes(HipGridData& g, HipGridData::LevelData& F, HipGridData::LevelData
     // rows > 512 points (column blocks): the corrected edge columns go through a workspace, one per
     // stream (the boundary planes' launch runs beside the interior's)
     const int64_t wsn = gs_jacobi_sweep2_prolong_ws_elems(&g.stencilAbi, &sub, (int)g.mode);
-    // (sized for the whole level once: a plane range needs less, and no buffer is ever reallocated
-    // while a launch may still read it)
-    double* ws = wsn > 0 ? F.proWs[s == g.stream() ? 0 : 1].get(std::max(
-                                wsn, gs_jacobi_sweep2_prolong_ws_elems(&g.stencilAbi, &F.geom, (int)g.mode)))
-                         : nullptr;
+    // (allocated once, at grid creation, for the largest plane range upLeg requests: never reallocated —
+    // a hipFree / hipMalloc here would synchronise the device inside the overlapped sequence)
+    DeviceBuf& wb = F.proWs[s == g.stream() ? 0 : 1];
+    if (wsn > wb.size()) throw Error("gs_jacobi_sweep2_prolong: workspace not sized at grid creation");
+    double* ws = wsn > 0 ? wb.get(wsn) : nullptr;
     check(gs_jacobi_sweep2_prolong_ws(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, F.v.data() + off,
                                       C.v.data(), nullptr, &C.geom, F.vAlt.data() + off, F.f.data() + off,
                                       F.newtonV ? F.newtonV.data() + off : nullptr, zlo, zhi, ws, wsn, s),
           "gs_jacobi_sweep2_prolong");
 }
+
+} // namespace
+
+// Workspace elements of the largest plane range upLeg's fused prolongation pair requests on level l
+// (the whole level, or the boundary / interior ranges of the overlapped Z-slab sequence).
+int64_t proWsElems(const HipGridData& g, std::size_t l)
+{
+    const gs_level& G = g.getLevel(l).geom;
+    const int64_t nz = G.nz, zt = nz % 2 == 0 ? nz - 1 : nz - 2;
+    const int64_t ranges[4][2] = {{1, nz}, {1, 2}, {zt, nz}, {3, zt - 1}};
+    int64_t need = 0;
+    for (const auto& r : ranges) {
+        if (r[1] < r[0] || r[0] < 1) continue;
+        gs_level sub = G;
+        sub.nz = r[1] - r[0] + 1;
+        sub.z0 += r[0] - 1;
+        need = std::max(need, gs_jacobi_sweep2_prolong_ws_elems(&g.stencilAbi, &sub, (int)g.mode));
+    }
+    return need;
+}
+
+namespace {
 
 bool transitionLevel(HipGridData& g, std::size_t l)
 {
@@ -533,6 +606,14 @@ void HipSolver::joinComm(HipGridData& grid, bool wait)
     if (grid.trace) return;
     if (!wait) check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
     else check((int)hipStreamWaitEvent(grid.stream(), grid.evB_, 0), "hipStreamWaitEvent");
+}
+
+// the pipelined sequence's pending exchange settled on the host (its kernels are on the comm stream),
+// then the event the next boundary planes and the final join wait on
+void HipSolver::settleExchange(HipGridData& grid)
+{
+    grid.haloSettle();
+    if (!grid.trace) check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
 }
 
 bool HipSolver::speculationEnabled(const HipGridData& grid)
@@ -676,11 +757,26 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
             run(1, nz, s);
         } else if (grid.overlapHalo && nz >= 2 * b + 1) {
             hipStream_t bs = s;
+            // interior k reads boundary k-1's planes (boundary k's event slot is recorded below, k-1's still
+            // holds) and interior k-1's, but no ghost plane: it may go before exchange k-1 has settled. When
+            // that exchange is still being settled on the host (RCCL's non-blocking group), interior k is
+            // enqueued first, so the GPU never idles behind the host; otherwise boundary k goes first, so its
+            // exchange starts as early as possible (GS_HALO_ORDER forces either order)
+            const bool interiorFirst = step > 0 && !grid.haloReady();
             if (!grid.trace) {
                 bs = grid.bndStream_.s;
-                // boundary k after interior k-1 (and everything before it on the compute stream) and after
-                // exchange k-1 (the ghost planes it reads; on the comm stream, after every earlier exchange)
-                check((int)hipEventRecord(grid.evA_, s), "hipEventRecord");
+                check((int)hipEventRecord(grid.evA_, s), "hipEventRecord"); // after interior k-1
+            }
+            auto interior = [&] {
+                if (!grid.trace && step > 0)
+                    check((int)hipStreamWaitEvent(s, grid.evBnd_[(step - 1) & 1], 0), "hipStreamWaitEvent");
+                run(b + 1, nz - b, s);
+            };
+            if (interiorFirst) interior();
+            if (step > 0) settleExchange(grid); // exchange k-1's kernels on the comm stream, then evB
+            if (!grid.trace) {
+                // boundary k after interior k-1 (whose input planes it overwrites) and after exchange k-1
+                // (the ghost planes it reads; on the comm stream, after every earlier exchange)
                 check((int)hipStreamWaitEvent(bs, grid.evA_, 0), "hipStreamWaitEvent");
                 if (step > 0) check((int)hipStreamWaitEvent(bs, grid.evB_, 0), "hipStreamWaitEvent");
             }
@@ -690,15 +786,15 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
                 hipEvent_t bnd = grid.evBnd_[step & 1];
                 check((int)hipEventRecord(bnd, bs), "hipEventRecord");
                 check((int)hipStreamWaitEvent(grid.commStream(), bnd, 0), "hipStreamWaitEvent");
-                // interior k reads boundary k-1's planes (boundary k's slot is recorded, k-1's still holds)
-                if (step > 0) check((int)hipStreamWaitEvent(s, grid.evBnd_[(step - 1) & 1], 0), "hipStreamWaitEvent");
             }
-            run(b + 1, nz - b, s);
-            grid.halo(L, L.vAlt, grid.commStream(), depth);
-            if (!grid.trace) check((int)hipEventRecord(grid.evB_, grid.commStream()), "hipEventRecord");
+            if (!interiorFirst) interior();
+            grid.haloIssue(L, L.vAlt, grid.commStream(), depth); // settled at the next step or below
             step++;
         } else {
-            if (step > 0) joinComm(grid, true); // an earlier overlapped step's exchange
+            if (step > 0) {
+                settleExchange(grid);
+                joinComm(grid, true); // an earlier overlapped step's exchange
+            }
             step = 0;
             run(1, nz, s);
             grid.halo(L, L.vAlt, s, depth);
@@ -710,6 +806,7 @@ void HipSolver::jacobi(HipGridData& grid, std::size_t l, std::size_t sweeps)
     }
     if (step > 0) {
         // the last exchange (and through it the last boundary planes) before anything else on the level
+        settleExchange(grid);
         joinComm(grid, true);
         if (!grid.trace) check((int)hipStreamWaitEvent(s, grid.evBnd_[(step - 1) & 1], 0), "hipStreamWaitEvent");
     }
@@ -807,7 +904,10 @@ void HipSolver::upLeg(HipGridData& grid, std::size_t i)
     auto& F = grid.getLevel(i - 1);
     grid.clock.mark(s, (int)(i - 1), true);
     materialize(grid, i); // only if the level had no sweep at all
-    if (i - 1 >= 1 && F.tiled && !C.distributed && grid.postSmoothing >= 2) {
+    // (the tiled step fuses the prolongation with a pair: the GS_NO_FUSED_SWEEPS / GS_NO_FUSED_PROLONG
+    // alternatives take the general path below)
+    if (i - 1 >= 1 && F.tiled && !C.distributed && grid.postSmoothing >= 2 && grid.sw.fusedSweeps &&
+        grid.sw.fusedProlong) {
         // a small level: prolongation, correction and the first two post-smoothing sweeps in one launch
         materialize(grid, i - 1);
         if (grid.trace)
@@ -886,7 +986,10 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
         }
         auto& L = grid.getLevel(i);
         auto& C = grid.getLevel(i + 1);
-        if (i >= 1 && pre == 2 && L.tiled && !C.distributed) {
+        // (the tiled step fuses a pair, the residual and the restriction and leaves v^2h = 0 as a flag: the
+        // GS_NO_FUSED_SWEEPS / GS_NO_FUSED_RR / GS_NO_ZERO_GUESS alternatives take the general path below)
+        if (i >= 1 && pre == 2 && L.tiled && !C.distributed && grid.sw.fusedSweeps && grid.sw.fusedRR &&
+            grid.sw.zeroGuess) {
             // a small level: the pre-smoothing pair, residual and restriction in one tiled launch
             if (grid.trace)
                 grid.rec("tiledpre", {{"L", (long long)i}, {"vzero", L.vZero}});

@@ -151,6 +151,9 @@ public:
                                                // LINEAR) run the tiled one-launch down/up-leg steps; 0 = off
         int64_t newtonProPoints = (int64_t)1 << 26; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
                                                      // prolongation pair from this many points per rank
+        // GS_HALO_ORDER: in a pipelined Z-slab sweep sequence, interior k goes before boundary k when
+        // exchange k-1 has not settled on the host yet (0, adaptive), always (1), or never (2: boundary first)
+        int haloOrder = 0;
     } sw;
     // levels coarseFrom .. numLevels()-1 run as ONE gs_coarse_cycle launch in every V-cycle
     // (numLevels(): none); set from GS_COARSE_POINTS at construction
@@ -176,7 +179,14 @@ public:
     // ghost planes of a distributed level's field (no-op otherwise); depth 2 where possible for
     // iterate fields (the fused pair reads two ghost planes of v)
     void halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth = 1);
-    double haloHostMs = 0.0; // host wall time spent inside halo() (issue + settle), summed
+    // the same in halves (the pipelined sweep sequence, HipSolver::jacobi): haloIssue starts the exchange,
+    // haloSettle() returns once its kernels are on s (only then may an event be recorded after it);
+    // haloReady(): one poll of an issued exchange (trace mode: GS_HALO_ORDER decides, see Switches)
+    void haloIssue(LevelData& L, DeviceField& fld, hipStream_t s, int depth);
+    bool haloReady();
+    void haloSettle();
+    double haloHostMs = 0.0;    // host wall time spent issuing and settling ghost exchanges, summed
+    double haloHostMaxMs = 0.0; // ... the largest for one exchange (issue + polls + settle)
     int64_t haloCalls = 0;
     int vDepth(const LevelData& L) const { return L.minPlanes >= 2 ? 2 : 1; }
     // replicated level fed from a distributed parent: assemble every rank's owned planes
@@ -199,6 +209,8 @@ private:
     hipEvent_t evBnd_[2] = {nullptr, nullptr}; // boundary planes of sweep k (k & 1) in a pipelined sequence
     std::vector<double> dryParts_;
     long traceNorms_ = 0;
+    bool haloPending_ = false; // an exchange issued by haloIssue, not settled
+    double haloCurMs_ = 0.0;   // host ms spent on that exchange so far
     double traceNorm();
     friend class HipSolver;
 };
@@ -243,6 +255,7 @@ public:
     static hipStream_t forkBoundary(HipGridData& grid);
     static void forkComm(HipGridData& grid);
     static void joinComm(HipGridData& grid, bool wait);
+    static void settleExchange(HipGridData& grid);
 
     // solve() records its residual history here when non-null (initial, then one per V-cycle)
     static thread_local std::vector<double>* history;

@@ -125,6 +125,7 @@ DRIVER_API = {
     "gs_grid_upload": (C.c_int, [C.c_void_p, C.c_int, C.c_int, dptr]),
     "gs_grid_sync": (C.c_int, [C.c_void_p]),
     "gs_grid_comm_stats": (C.c_int, [C.c_void_p, dptr, C.POINTER(C.c_int64)]),
+    "gs_grid_comm_stats_max": (C.c_int, [C.c_void_p, dptr]),
     "gs_grid_metrics": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int, dptr, C.c_int]),
     "gs_dump_write": (C.c_int, [dptr, i64, i64, i64, C.c_char_p]),
     "gs_grid_dump": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),

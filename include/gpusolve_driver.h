@@ -66,6 +66,9 @@ int gs_grid_sync(void* grid);
  * the exchange calls (RCCL: group start/end and the settle poll of the non-blocking communicator) and
  * the number of calls. Zero for single-GPU grids. */
 int gs_grid_comm_stats(void* grid, double* halo_host_ms, int64_t* halo_calls);
+/* The largest host cost of ONE exchange so far (issue + polls + settle; the pipelined sweep sequence
+ * settles an exchange only before the next boundary planes, after the next interior is enqueued). */
+int gs_grid_comm_stats_max(void* grid, double* halo_host_max_ms);
 /* With GS_METRICS=1 in the environment when the grid was created: the "[gs] mlups=... gbps=...
  * pct_peak=... vcycle_ms=... cycles=... level_ms=..." line GpuSolve-hip prints after its solve (over
  * the V-cycles run so far), and the device ms per level and V-cycle. Non-zero if metrics are off. */

@@ -206,3 +206,29 @@ def test_gloo_replay_catches_a_broken_schedule(mutation):
     same_field = np.array_equal(got, ref_v)
     same_hist = all(abs(a - b) <= 1e-12 * abs(b) for a, b in zip(hists[0], ref_hist))
     assert not (same_field and same_hist), "a broken schedule went unnoticed"
+
+
+@pytest.mark.parametrize("order", ["1", "2"])
+@pytest.mark.parametrize("dims,world,min_points,pre,post", [((64, 256, 64), 2, -1, 4, 3), ((48, 256, 70), 3, -1, 6, 2)])
+def test_gloo_replay_halo_orders(monkeypatch, order, dims, world, min_points, pre, post):
+    """Multi-step smoothing calls (several overlapped pair steps per HipSolver::jacobi call) with the
+    pipelined sequence's two dispatch orders forced (GS_HALO_ORDER=1: interior k before boundary k, as when
+    exchange k-1 is still settling on the host; 2: boundary first): the recorded schedule replays bit for
+    bit, and order 1 really puts an interior launch ahead of its step's boundary planes."""
+    import zslab_exec as X
+    monkeypatch.setenv("GS_HALO_ORDER", order)
+    params = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=0, preSmoothing=pre, postSmoothing=post)
+    ops = X.schedule(params, world, 0, min_points)
+    # the first launch of a step that follows another in the same call (after the previous step's exchange
+    # and swap): boundary planes (z1 == 1) or the interior range
+    firsts = [ops[i + 2] for i in range(len(ops) - 2)
+              if ops[i][0] == "halo" and ops[i][1].get("field") == "vAlt" and ops[i + 1][0] == "swap"
+              and ops[i + 2][0] == "pair"]
+    interior_first = any(kv["z1"] > 2 for _, kv in firsts)
+    assert firsts and interior_first == (order == "1"), firsts
+    got, ref_v, hists, ref_hist, _ = _replay(dims, world, min_points, pre, post)
+    for hist in hists:
+        assert len(hist) == len(ref_hist)
+        for a, b in zip(hist, ref_hist):
+            assert abs(a - b) <= 1e-12 * abs(b), (a, b)
+    np.testing.assert_array_equal(got, ref_v)

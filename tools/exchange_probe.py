@@ -211,6 +211,60 @@ def main():
         main_s.wait_event(ev_x)
         main_s.wait_event(evb[(nsteps - 1) & 1])
 
+    def pipe_steps_defer(blocks, nsteps):
+        """r04 driver order when exchange k-1 has not settled on the host yet (HipSolver::jacobi): interior k
+        is enqueued BEFORE boundary k (it needs boundary k-1 only), then boundary k (after interior k-1 and
+        exchange k-1), then exchange k. The GPU-side cost of that dispatch order."""
+        evb = [None, None]
+        ev_x = None
+        for k_ in range(nsteps):
+            ev_a = torch.cuda.Event()
+            ev_a.record(main_s)
+            if k_ > 0:
+                main_s.wait_event(evb[(k_ - 1) & 1])
+            pair(3, NZ - 2, main_s)
+            bnd_s.wait_event(ev_a)
+            if ev_x is not None:
+                bnd_s.wait_event(ev_x)
+            pair(1, 2, bnd_s)
+            pair(NZ - 1, NZ, bnd_s)
+            evb[k_ & 1] = torch.cuda.Event()
+            evb[k_ & 1].record(bnd_s)
+            comm_s.wait_event(evb[k_ & 1])
+            if blocks:
+                assert kd.gs_debug_bw(4, 1, 1, blocks, O.data_ptr(), A.data_ptr(), None, m, sink.data_ptr(),
+                                      comm_s.cuda_stream) == 0
+            ev_x = torch.cuda.Event()
+            ev_x.record(comm_s)
+        main_s.wait_event(ev_x)
+        main_s.wait_event(evb[(nsteps - 1) & 1])
+
+    def timed(fn, *args):
+        for _ in range(2):
+            fn(*args)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(main_s)
+        fn(*args)
+        e1.record(main_s)
+        torch.cuda.synchronize()
+        return round(e0.elapsed_time(e1) / reps, 4)
+
+    if os.environ.get("PROBE_WGS"):
+        # r04: the driver's pipelined step against the stand-in exchange's workgroup count (the RCCL CTA
+        # budget GS_RCCL_CTAS sets), in both dispatch orders; interleaved, PROBE_ROUNDS rounds
+        wgs = [int(x) for x in os.environ["PROBE_WGS"].split(",")]
+        res = {}
+        for rnd in range(int(os.environ.get("PROBE_ROUNDS", "2"))):
+            for b in wgs:
+                for name, fn in (("pipelined", pipe_steps), ("pipelined-interior-first", pipe_steps_defer)):
+                    key = f"{name} x{reps} exchange={'fat x%d' % b if b else 'none'}"
+                    res.setdefault(key, []).append(timed(fn, b, reps))
+        print(json.dumps({"slab": [NX, NY, NZ], "cus": cus, "step_ms": res,
+                          "note": "pipelined overlapped pair steps of config #5's slab per stand-in exchange workgroup "
+                                  "count (k_fatcopy at RCCL's kernel footprint, 34 MB); one value per round"}, indent=1))
+        return
+
     res = {}
     # the boundary launches alone (B planes each side)
     for B in (2, 4):
