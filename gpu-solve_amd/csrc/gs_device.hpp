@@ -25,6 +25,23 @@
 
 #include "gpusolve_hip.h"
 
+// Timing-only experiment builds (tools/exp_builds.sh; never the product, results are wrong):
+//   GS_EXP_NOBAR  the pair's and k_rr2's per-plane LDS barriers removed (what the lock-step costs)
+//   GS_EXP_NOEXP  exp(x) replaced by one multiplication (what the exponentials cost)
+//   GS_EXP_NODIV  NEWTON's r / den replaced by a multiplication (what the divisions cost)
+#ifdef GS_EXP_NOEXP
+#define exp(x) ((x) * 1.0000001)
+#endif
+#ifdef GS_EXP_NOBAR
+#define GS_LDS_BARRIER() __builtin_amdgcn_s_waitcnt(0xc07f)
+#else
+#define GS_LDS_BARRIER()                                                                                               \
+    do {                                                                                                               \
+        __builtin_amdgcn_s_waitcnt(0xc07f);                                                                            \
+        __builtin_amdgcn_s_barrier();                                                                                  \
+    } while (0)
+#endif
+
 namespace {
 
 constexpr int WAVE = 64;
@@ -86,9 +103,10 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_RR_LDS            residual + restriction through the LDS kernel (k_resrestrict) only
 //   GS_RR_NR=1|2         coarse rows per k_rr2 block (default: 2 on LINEAR levels of >= 2^26 points)
 //   GS_RR_NTU=0|2        k_rr2 non-temporal loads never / always (default: two-row blocks only)
+//   GS_RR_REVERSE=1      k_rr2 z-chunks in descending order (A/B)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds;
-    int slabZc, pairZc, rrNr, rrNtu;
+    int slabZc, pairZc, rrNr, rrNtu, rrReverse;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
     {
@@ -100,7 +118,8 @@ struct Knobs {
           pairXh(num("GS_PAIR_XH", 1) != 0), fitRounds(num("GS_FIT_ROUNDS", 1) != 0),
           bigChunks(num("GS_PAIR_BIG_CHUNKS", 1) != 0), oneRound(num("GS_PAIR_ONE_ROUND", 1) != 0),
           rrLds(getenv("GS_RR_LDS") != nullptr), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
-          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
+          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 0)),
+          pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
     }
 };
@@ -279,7 +298,11 @@ __device__ __forceinline__ double newton_op(double q, double c, double A, double
 __device__ __forceinline__ double newton_update(const Coef& k, double v, double r, double A, double E)
 {
     const double den = k.preFac + A * E;
+#ifdef GS_EXP_NODIV
+    return v + k.omega * (r * den);
+#else
     return v + k.omega * (r / den);
+#endif
 }
 
 __device__ __forceinline__ double wave_sum(double x)
@@ -944,7 +967,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
                                                          double* __restrict__ ca,
                                                          double* __restrict__ cb, int fnx, int fny, int fnz,
                                                          int64_t fldy, int64_t fldz, int cnx, int cny, int cnz, int64_t cldy,
-                                                         int64_t cldz, int ZC, int zhi)
+                                                         int64_t cldz, int ZC, int zhi, int rev)
 {
     static_assert(MODE != GS_NEWTON || !PF, "NEWTON: newtonV rows exceed the budget of the prefetch ring");
     constexpr int RR = 2 * NR + 1; // computed fine rows; v rows 0 .. RR+1 (0 and RR+1: halo rows)
@@ -960,7 +983,10 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     __syncthreads();
     const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
     const int Y = 1 + NR * (int)(tile % gridDim.x);
-    const int Zb = 1 + (int)(tile / gridDim.x) * ZC, Ze = min(Zb + ZC - 1, cnz);
+    // rev (GS_RR_REVERSE): the z-chunks in descending order, so the first blocks read the planes the
+    // preceding pair launch touched last
+    const int zi = (int)(tile / gridDim.x);
+    const int Zb = 1 + (rev ? (int)gridDim.y - 1 - zi : zi) * ZC, Ze = min(Zb + ZC - 1, cnz);
     const int X = 1 + wx * WAVE + lane;
     const int x = 2 * X - 1, xl = min(x, fnx + 1);
     const bool okx0 = x <= fnx, okx1 = x + 1 <= fnx;
@@ -1002,10 +1028,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
         H1[s][1] = ld2(at(v, RR + 1, p + 1));
     };
     // LDS-only barrier: the outstanding prefetch stays in flight across it
-    auto lds_barrier = [] {
-        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-    };
+    auto lds_barrier = [] { GS_LDS_BARRIER(); }; // lgkmcnt(0), s_barrier
     // the columns left of lane 0 / right of lane 63 on two planes: v(x-1) of lane 0, v(x+2) of lane 63
     auto edges_v = [&](int par, const double2 (&P)[RR], const double2 (&Q)[RR], double (&CLp)[RR], double (&CRp)[RR],
                        double (&CLq)[RR], double (&CRq)[RR]) {
@@ -2196,8 +2219,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             yrow[ph][wy][wx][0][lane] = Vc[RY];
             yrow[ph][wy][wx][1][lane] = V1c[RY];
             // LDS-only barrier: the outstanding prefetch stays in flight across it
-            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
-            __builtin_amdgcn_s_barrier();
+            GS_LDS_BARRIER(); // lgkmcnt(0), s_barrier
             double CL[NE], CR[NE];
 #pragma unroll
             for (int i = 0; i < NE; i++) { // wave-uniform: kept in SGPRs

@@ -1198,11 +1198,15 @@ double NewtonSolver::compF(HipGridData& grid)
 // the sum goes to level 0's vAlt — zero outside the interior like newtonV + v, and dead once the inner
 // solve has returned (its pending speculative sweep is dropped; the next inner solve starts from the
 // zero iterate) — which then becomes newtonV. Bit-identical to gs_axpy + gs_newton_F.
+// On a Z-slab rank the pass reads w and e on the ghost planes 0 and nz+1 (both current: newtonV's from the
+// previous update, v's from the inner solve's last exchange) but stores w' only on the owned planes, so
+// the new newtonV's ghost planes are formed afterwards as k_axpy would leave them (newtonV + 1.0 v, two
+// planes: a copy and an axpy each) — no exchange, bit-identical to the whole-array gs_axpy of the
+// two-pass path.
 bool NewtonSolver::fusedUpdate(const HipGridData& grid)
 {
     const auto& L0 = grid.getLevel(0);
-    return grid.sw.newtonFusedUpdate && !(L0.distributed && grid.nranks() > 1) &&
-           gs_newton_F_update_supported(&grid.stencilAbi, &L0.geom) != 0;
+    return grid.sw.newtonFusedUpdate && gs_newton_F_update_supported(&grid.stencilAbi, &L0.geom) != 0;
 }
 
 double NewtonSolver::compFUpdate(HipGridData& grid)
@@ -1214,6 +1218,18 @@ double NewtonSolver::compFUpdate(HipGridData& grid)
         check(gs_newton_F_update(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
                                  grid.newtonF.data(), L0.vAlt.data(), L0.f.data(), grid.partials(), grid.stream()),
               "gs_newton_F_update");
+    if (L0.distributed && grid.nranks() > 1) {
+        // the ghost planes of w' = newtonV + v (see fusedUpdate)
+        const int64_t ldz = L0.v.ldz();
+        for (const int64_t p : {(int64_t)0, L0.geom.nz + 1}) {
+            if (grid.trace) {
+                grid.rec("ghostsum", {{"L", 0}, {"plane", (long long)p}}, "vAlt=newtonV+v");
+                continue;
+            }
+            check(gs_copy(L0.vAlt.data() + p * ldz, L0.newtonV.data() + p * ldz, ldz, grid.stream()), "gs_copy");
+            check(gs_axpy(L0.vAlt.data() + p * ldz, L0.v.data() + p * ldz, 1.0, ldz, grid.stream()), "gs_axpy");
+        }
+    }
     L0.newtonV.swap(L0.vAlt);
     grid.halo(L0, L0.f, grid.stream());
     return HipSolver::finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L0.geom));

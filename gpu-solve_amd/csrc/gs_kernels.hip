@@ -207,11 +207,15 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
                            dim3(256), 0, st, v_in, coarse_v, nullptr, ws, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy,
                            L->ldz, cl->ldy, cl->ldz, bw, zlo ? 1 : 0, zhi ? 1 : 0);
     }
-#define GS_TBP1(M, P, U, X) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, false, true, P, 1, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
-#define GS_TBP(M, P, X) do { if (k.unit) GS_TBP1(M, P, true, X); else GS_TBP1(M, P, false, X); } while (0)
-    if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1, false);
-    else if (xh) GS_TBP(GS_LINEAR, 1, true);
-    else GS_TBP(GS_LINEAR, 1, false);
+#define GS_TBP1(M, P, U, X, WM) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, 1, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
+#define GS_TBP(M, P, X, WM) do { if (k.unit) GS_TBP1(M, P, true, X, WM); else GS_TBP1(M, P, false, X, WM); } while (0)
+    // NEWTON's variant keeps ~37 KB of state per x-wave in LDS (its RECOMP rows): rows of <= 256 points
+    // (two x-waves) take the instance sized for two, so that two blocks share a CU (8 waves, the VGPR
+    // limit) instead of one block of 4 waves holding the whole LDS of a four-x-wave instance
+    if (mode == GS_NEWTON && b.y <= 2) GS_TBP(GS_NEWTON, 1, false, 2);
+    else if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1, false, TBY_WX);
+    else if (xh) GS_TBP(GS_LINEAR, 1, true, TBY_WX);
+    else GS_TBP(GS_LINEAR, 1, false, TBY_WX);
 #undef GS_TBP
 #undef GS_TBP1
     return launch_status();
@@ -357,7 +361,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         // 512^3, r02 tools/rr_ab_session.sh rrntu); GS_RR_NTU=0 keeps them cached (A/B)
         const int ntu_env = kKnobs.rrNtu;
         const bool ntu = ntu_env == 2 || (ntu_env == 1 && nr == 2);
-#define GS_RR2V(M, N, U, T) hipLaunchKernelGGL((k_rr2<M, false, N, U, T>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0)
+#define GS_RR2V(M, N, U, T) hipLaunchKernelGGL((k_rr2<M, false, N, U, T>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0, kKnobs.rrReverse)
 #define GS_RR2U(M, N, U) do { if (ntu) GS_RR2V(M, N, U, true); else GS_RR2V(M, N, U, false); } while (0)
 #define GS_RR2(M, N) do { if (k.unit) GS_RR2U(M, N, true); else GS_RR2U(M, N, false); } while (0)
         if (mode == GS_LINEAR && nr == 2) GS_RR2(GS_LINEAR, 2);

@@ -156,3 +156,24 @@ def test_zslab_random_vs_single(case):
     for a, b in zip(hn, h1):
         if np.isfinite(a) or np.isfinite(b):
             assert rel(a, b) < 1e-12
+
+
+@pytest.mark.parametrize("dims,nranks", [((512, 128, 128), 2), ((512, 256, 128), 4), ((512, 256, 256), 8)])
+def test_newton_fused_update_on_slabs(monkeypatch, dims, nranks):
+    """findError's newtonV += v fused into the next compF on Z-slab ranks (k_newton_upd on the owned planes,
+    the new newtonV's ghost planes formed as newtonV + 1.0 v): 2-8 loopback slabs, fused (default) and two-pass
+    (GS_NO_NEWTON_FUSED_UPDATE) bit-identical to each other and to one GPU, three Newton iterations."""
+    import zslab_exec as X
+    p = gsv.GridParams(maxiter=3, tol=0.0, gridDim=dims, mode=2)
+    ops = {op for op, _ in X.schedule(p, nranks, 0, -1)}
+    assert {"newtonFupdate", "ghostsum"} <= ops, ops  # the fused path is the one the slabs take
+    ref_h, ref_v = single(p, 0, True)
+    h, v = loopback(p, nranks, -1, 0, True)
+    monkeypatch.setenv("GS_NO_NEWTON_FUSED_UPDATE", "1")
+    h2, v2 = loopback(p, nranks, -1, 0, True)
+    assert all(math.isfinite(a) for a in ref_h), ref_h
+    assert len(h) == len(h2) == len(ref_h)
+    for a, b, c in zip(h, h2, ref_h):
+        assert a == b and rel(a, c) < 1e-12, (a, b, c)
+    np.testing.assert_array_equal(v[:, :, 1:-1], v2[:, :, 1:-1])
+    np.testing.assert_array_equal(v[:, :, 1:-1], ref_v[:, :, 1:-1])

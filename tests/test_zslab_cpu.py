@@ -232,3 +232,19 @@ def test_gloo_replay_halo_orders(monkeypatch, order, dims, world, min_points, pr
         for a, b in zip(hist, ref_hist):
             assert abs(a - b) <= 1e-12 * abs(b), (a, b)
     np.testing.assert_array_equal(got, ref_v)
+
+
+def test_newton_slab_schedule_fuses_the_update(monkeypatch):
+    """NEWTON on Z-slabs (trace mode): findError's newtonV += v is fused into the next compF
+    (newtonFupdate) and the new newtonV's two ghost planes are formed from both operands (ghostsum, planes 0
+    and nz+1) instead of a whole-array axpy; GS_NO_NEWTON_FUSED_UPDATE restores the two passes."""
+    import zslab_exec as X
+    p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=(512, 128, 128), mode=2)
+    ops = X.schedule(p, 2, 0, -1)
+    names = [op for op, _ in ops]
+    assert names.count("newtonFupdate") == 2 and "axpy" not in names
+    ghost = [kv["plane"] for op, kv in ops if op == "ghostsum"]
+    assert ghost == [0, 65, 0, 65], ghost
+    monkeypatch.setenv("GS_NO_NEWTON_FUSED_UPDATE", "1")
+    names = [op for op, _ in X.schedule(p, 2, 0, -1)]
+    assert "newtonFupdate" not in names and names.count("axpy") == 2
