@@ -401,8 +401,20 @@ int gs_zslab_schedule(const gs_params* p, int nranks, int rank, int64_t min_poin
             auto comm = gs::makeTraceComm(rank, nranks);
             gs::HipGridData g(toParams(p), comm.get(), min_points, &ops);
             g.printProgress = false;
-            if (g.mode == gs::GridParams::NEWTON) gs::NewtonSolver::solve(g);
-            else gs::HipSolver::solve(g);
+            // the solve's residuals are read (as GpuSolve-hip prints them): every closing norm is in the schedule
+            std::vector<double> hist;
+            gs::NewtonSolver::history = &hist;
+            gs::HipSolver::history = &hist;
+            try {
+                if (g.mode == gs::GridParams::NEWTON) gs::NewtonSolver::solve(g);
+                else gs::HipSolver::solve(g);
+            } catch (...) {
+                gs::NewtonSolver::history = nullptr;
+                gs::HipSolver::history = nullptr;
+                throw;
+            }
+            gs::NewtonSolver::history = nullptr;
+            gs::HipSolver::history = nullptr;
         }
         std::string text;
         for (const auto& o : ops) text += o + "\n";

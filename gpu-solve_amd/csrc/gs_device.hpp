@@ -16,6 +16,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <cmath>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -67,6 +69,10 @@ struct Coef {
     double preFac; // s0 / (h*h)        (CpuSolver.cpp:144)
     int fastdiv;   // 2^-120 <= hh <= 1: div_hh may take its 3-operation path
     int unit;      // s[1..6] == -1 and |s[0]| >= 1: the unit-neighbour stencil sum applies (stencil_sum<true>)
+    int swz;       // column-block pairs: x-waves of the mirrored row rotated by two (GS_XH_SWIZZLE)
+    int zq;        // every s[i] finite and hh a positive normal number: the stencil sum of an identically zero
+                   // iterate over hh is exactly +0 (each s[i] * 0 is a signed zero, +0 plus a signed zero is
+                   // +0, +0 / hh is +0), so zero-iterate sweeps take q = +0 without evaluating it
     int64_t off[7]; // generic kernel: linear element offsets of the 7 entries
 };
 
@@ -104,8 +110,11 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_RR_NR=1|2         coarse rows per k_rr2 block (default: 2 on LINEAR levels of >= 2^26 points)
 //   GS_RR_NTU=0|2        k_rr2 non-temporal loads never / always (default: two-row blocks only)
 //   GS_RR_REVERSE=1      k_rr2 z-chunks in descending order (A/B)
+//   GS_NO_ZERO_Q         zero-iterate sweeps evaluate the stencil of their zeros instead of taking q = +0
+//   GS_XH_SWIZZLE=0|1    column-block pairs: the mirrored row's x-waves rotated by two (1) or not (0)
 struct Knobs {
-    bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds;
+    bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ;
+    int xhSwizzle;
     int slabZc, pairZc, rrNr, rrNtu, rrReverse;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
@@ -117,7 +126,8 @@ struct Knobs {
         : unitStencil(getenv("GS_NO_UNIT_STENCIL") == nullptr), tbxPfd2(num("GS_TBX_PFD", 2) != 1),
           pairXh(num("GS_PAIR_XH", 1) != 0), fitRounds(num("GS_FIT_ROUNDS", 1) != 0),
           bigChunks(num("GS_PAIR_BIG_CHUNKS", 1) != 0), oneRound(num("GS_PAIR_ONE_ROUND", 1) != 0),
-          rrLds(getenv("GS_RR_LDS") != nullptr), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
+          rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
+          xhSwizzle(num("GS_XH_SWIZZLE", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
           rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 0)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
@@ -140,6 +150,9 @@ Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamm
     k.fastdiv = k.hh >= 0x1p-120 && k.hh <= 1.0;
     k.unit = kKnobs.unitStencil && (S->s[0] >= 1.0 || S->s[0] <= -1.0);
     for (int i = 1; i < 7; i++) k.unit = k.unit && S->s[i] == -1.0;
+    k.swz = kKnobs.xhSwizzle;
+    k.zq = kKnobs.zeroQ && std::isnormal(k.hh) && k.hh > 0.0;
+    for (int i = 0; i < 7; i++) k.zq = k.zq && std::isfinite(S->s[i]);
     return k;
 }
 
@@ -1958,9 +1971,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // y-edge rows: [parity][y-wave][x-wave][v | sweep-1][lane]
     __shared__ double2 yrow[2][2][WXMAX][2][WAVE];
     const int lane = threadIdx.x;
-    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int wy = __builtin_amdgcn_readfirstlane(threadIdx.z);
     const int WX = blockDim.y;
+    // XH (Coef::swz): the mirrored y-wave row runs its x-waves rotated by two, so that the two waves a SIMD
+    // hosts (hardware wave i -> SIMD i mod 4) are never both edge waves (the edge column's extra work)
+    const int wx = __builtin_amdgcn_readfirstlane(XH && k.swz && wy && WX == 4 ? (threadIdx.y + 2) & 3 : threadIdx.y);
     const int tid = threadIdx.x + WAVE * (threadIdx.y + WX * threadIdx.z);
     for (int i = tid; i < 2 * 2 * (WXMAX + 2) * 2 * NE; i += WAVE * WX * 2) (&edge[0][0][0][0][0])[i] = 0.0;
     __syncthreads();
@@ -2259,13 +2274,16 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         const double lm = lane_from_left<true>(EC, 0.0), lp = lane_from_right<true>(EC, 0.0);
                         const double ym = M ? lp : lm, yp = M ? lm : lp;
                         double nv;
+                        // (zero iterate: q = +0 exactly, Coef::zq)
+                        auto qe = [&] {
+                            return (ZV && k.zq) ? 0.0 : div_hh(k, stencil_sum<UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP));
+                        };
                         if constexpr (MODE == GS_NEWTON) { // the interior rows' NEWTON expressions, exp once
                             const double we = EW[cs], A = k.gamma * (1 + we), E = exp(we);
-                            const double a = newton_op(div_hh(k, stencil_sum<UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP)),
-                                                       c, A, E);
+                            const double a = newton_op(qe(), c, A, E);
                             nv = newton_update(k, c, EF[cs] - a, A, E);
                         } else {
-                            const double a = op_value<MODE, UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP, 0.0);
+                            const double a = op_finish<MODE>(k, qe(), c, 0.0);
                             nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
                         }
                         ES1n = (!pz || !erowc) ? c : nv;
@@ -2285,11 +2303,17 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                     const double2 c = Vc[j], zm = Vp[j], zp = VL[cs][j];
                     const double2 lm = j == 0 ? HL[cs] : Vc[j - 1], lp = j == RY ? vY : Vc[j + 1];
                     const double2 ym = M ? lp : lm, yp = M ? lm : lp;
-                    const double xm0 = lane_from_left<true>(c.y, CL[j]);
-                    const double xp1 = lane_from_right<true>(c.x, CR[j]);
-                    double q[2] = {stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x),
-                                   stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
-                    div_hh_row<MODE>(k, q);
+                    double q[2];
+                    if (ZV && k.zq) { // the stencil of the zero iterate over h^2: +0 exactly (Coef::zq)
+                        q[0] = 0.0;
+                        q[1] = 0.0;
+                    } else {
+                        const double xm0 = lane_from_left<true>(c.y, CL[j]);
+                        const double xp1 = lane_from_right<true>(c.x, CR[j]);
+                        q[0] = stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x);
+                        q[1] = stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y);
+                        div_hh_row<MODE>(k, q);
+                    }
                     double a0, a1, n0, n1;
                     if constexpr (MODE == GS_NEWTON) {
                         const double2 wv = WL[cs][j];

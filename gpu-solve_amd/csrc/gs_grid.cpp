@@ -643,12 +643,29 @@ void HipSolver::solve(HipGridData& grid)
         }
         return res <= initialResidual / (1.0 / grid.tol);
     };
+    // The closing norm of the LAST cycle decides nothing (the loop ends at maxiter either way): when nobody
+    // reads it — no print, no history, no per-level clock; NewtonSolver::findError's inner solves — that
+    // cycle ends with its up-leg and the norm's pass (a whole level-0 pair at 512^3) is not run
+    const bool lastNormDead = !print && history == nullptr && !grid.clock.on;
     if (spec) {
-        runCycles(grid, &pending, grid.maxiter, onNorm);
+        runCycles(grid, &pending, grid.maxiter, onNorm, lastNormDead);
     } else {
-        for (std::size_t i = 0; i < grid.maxiter; i++)
+        for (std::size_t i = 0; i < grid.maxiter; i++) {
+            if (lastNormDead && i + 1 == grid.maxiter) {
+                cycleDown(grid, nullptr);
+                cycleUpNoNorm(grid);
+                break;
+            }
             if (onNorm(i, vcycle(grid))) break;
+        }
     }
+}
+
+// level 0's up-leg without the closing norm (the last cycle of a solve whose final norm nobody reads)
+void HipSolver::cycleUpNoNorm(HipGridData& grid)
+{
+    if (std::min(grid.coarseFrom, grid.numLevels() - 1) >= 1) upLeg(grid, 1);
+    if (grid.trace) grid.rec("nonorm", {{"L", 0}});
 }
 
 // Global ||.|| from this rank's per-block partials: fixed-order sums per rank, then over ranks in
@@ -1118,12 +1135,19 @@ bool HipSolver::pipelinable(const HipGridData& grid, int pending)
 }
 
 std::size_t HipSolver::runCycles(HipGridData& grid, int* pending, std::size_t maxCycles,
-                                 const std::function<bool(std::size_t, double)>& onNorm)
+                                 const std::function<bool(std::size_t, double)>& onNorm, bool lastNormDead)
 {
     // (cycle-invariant: every closing speculative step leaves the same number of sweeps pending)
     const bool pipe = pipelinable(grid, *pending);
     bool downDone = false; // this cycle's cycleDown was enqueued during the previous cycle's wait
     for (std::size_t i = 0; i < maxCycles; i++) {
+        if (lastNormDead && i + 1 == maxCycles) {
+            // the last cycle's closing norm decides nothing and nobody reads it: no speculative pass
+            if (!downDone) cycleDown(grid, pending);
+            cycleUpNoNorm(grid);
+            *pending = 0;
+            return maxCycles;
+        }
         if (!pipe) {
             if (onNorm(i, vcycleSpeculative(grid, pending))) return i + 1;
             continue;

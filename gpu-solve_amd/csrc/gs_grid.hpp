@@ -239,8 +239,10 @@ public:
     // to stop — the early-enqueued work then only wrote coarse levels and scratch, and the adoption
     // of the speculative level-0 sweeps is undone, so level 0 holds cycle i's iterate exactly as
     // without the overlap. *pending: the speculative sweeps vAlt holds on entry and on return.
+    // lastNormDead: the last cycle's closing norm is not computed (nobody reads it, see solve())
     static std::size_t runCycles(HipGridData& grid, int* pending, std::size_t maxCycles,
-                                 const std::function<bool(std::size_t, double)>& onNorm);
+                                 const std::function<bool(std::size_t, double)>& onNorm, bool lastNormDead = false);
+    static void cycleUpNoNorm(HipGridData& grid);
     static bool pipelinable(const HipGridData& grid, int pending);
     static void upLeg(HipGridData& grid, std::size_t level); // level-1 -> level-1 up-leg (from `level`)
     // level-0 sweep or pair v -> vAlt (no swap) + norm of f - A v; *sweeps = sweeps run; !wait: the

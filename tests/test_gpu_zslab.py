@@ -158,7 +158,7 @@ def test_zslab_random_vs_single(case):
             assert rel(a, b) < 1e-12
 
 
-@pytest.mark.parametrize("dims,nranks", [((512, 128, 128), 2), ((512, 256, 128), 4), ((512, 256, 256), 8)])
+@pytest.mark.parametrize("dims,nranks", [((511, 127, 127), 2), ((511, 255, 127), 4), ((511, 255, 255), 8)])
 def test_newton_fused_update_on_slabs(monkeypatch, dims, nranks):
     """findError's newtonV += v fused into the next compF on Z-slab ranks (k_newton_upd on the owned planes,
     the new newtonV's ghost planes formed as newtonV + 1.0 v): 2-8 loopback slabs, fused (default) and two-pass
