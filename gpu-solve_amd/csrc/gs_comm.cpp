@@ -19,9 +19,10 @@ namespace gs {
 
 namespace {
 // RCCL's workgroups per exchange group (ncclConfig_t::minCTAs = maxCTAs; GS_RCCL_CTAS overrides): the
-// stand-in exchange at RCCL's kernel footprint finishes the overlapped config #5 slab step sooner with more
-// workgroups (tools/exchange_probe.py)
-constexpr int kRcclCtasDefault = 32;
+// stand-in exchange at RCCL's kernel footprint (34 MB per step) finishes the overlapped config #5 slab step
+// sooner with more workgroups — 0.958 / 0.838 / 0.826 / 0.771-0.789 / 0.752-0.754 ms at 8 / 16 / 32 / 64 / 128
+// against 0.722 ms without an exchange (profiles/r04/r04b_exchange_wgs.json); 64 is NCCL's channel limit
+constexpr int kRcclCtasDefault = 64;
 
 void hipOk(hipError_t e, const char* what)
 {

@@ -318,6 +318,38 @@ __device__ __forceinline__ double newton_update(const Coef& k, double v, double 
 #endif
 }
 
+// NEWTON's update with the quotient r / den formed from den's reciprocal y = hh_recip(den) (sharing y
+// between a pair's two sweeps through LDS or registers measured no better than recomputing it: it spills).
+// The gfx950 IEEE division is div_scale, rcp + two Newton steps, q = N y, e = fma(-D, q, N),
+// div_fmas(e, y, q), div_fixup: with 2^-300 <= |den| < 2^400 and 2^-400 <= |r| < 2^300 neither operand is
+// scaled, VCC stays clear (exponent gap < 768, no denormal reciprocal or quotient, numerator exponent > 53),
+// div_fmas is the plain fma and div_fixup returns q', so the three operations below equal r / den bit for
+// bit. Anything else (zero, NaN, inf, extreme magnitudes) takes the division itself.
+__device__ __forceinline__ bool newton_den_ok(double den)
+{
+    const double a = __builtin_fabs(den);
+    return a >= 0x1p-300 && a < 0x1p400;
+}
+// a row's two points at once: one branch for both (either both quotients fast, or both divided)
+__device__ __forceinline__ double2 newton_update_y2(const Coef& k, double2 v, double2 r, double2 den)
+{
+    const double ax = __builtin_fabs(r.x), ay = __builtin_fabs(r.y);
+    const bool ok = newton_den_ok(den.x) && newton_den_ok(den.y) && ax >= 0x1p-400 && ax < 0x1p300 &&
+                    ay >= 0x1p-400 && ay < 0x1p300;
+    double qx, qy;
+    if (ok) {
+        const double yx = hh_recip(den.x), yy = hh_recip(den.y);
+        qx = r.x * yx;
+        qy = r.y * yy;
+        const double ex = __builtin_fma(-den.x, qx, r.x), ey = __builtin_fma(-den.y, qy, r.y);
+        qx = __builtin_fma(ex, yx, qx);
+        qy = __builtin_fma(ey, yy, qy);
+    } else {
+        qx = r.x / den.x;
+        qy = r.y / den.y;
+    }
+    return make_double2(v.x + k.omega * qx, v.y + k.omega * qy);
+}
 __device__ __forceinline__ double wave_sum(double x)
 {
 #pragma unroll
@@ -2036,6 +2068,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     constexpr int NS = PFD == 2 ? 4 : 2, UNR = PFD == 2 ? 4 : 2;
     double2 Vp[NV], Vc[NV], VL[NS][NV], FL[NS][NV], WL[NS][NV], HL[NS];
     double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
+    // SHY (NEWTON plain pairs on whole rows): the quotient r / den through den's reciprocal (newton_update_y)
+    constexpr bool SHY = MODE == GS_NEWTON && PRO == 0 && !XH;
     // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes A from the
     // newtonV rows at z-1 and reads E = exp(w) from LDS (same expressions, same values)
     constexpr bool RECOMP = MODE == GS_NEWTON && PRO != 0;
@@ -2326,8 +2360,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         if (RECOMP && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
                         a0 = newton_op(q[0], c.x, A.x, E.x);
                         a1 = newton_op(q[1], c.y, A.y, E.y);
-                        n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
-                        n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
+                        if constexpr (SHY) {
+                            const double2 n = newton_update_y2(k, c, make_double2(FL[cs][j].x - a0, FL[cs][j].y - a1),
+                                                               make_double2(k.preFac + A.x * E.x, k.preFac + A.y * E.y));
+                            n0 = n.x;
+                            n1 = n.y;
+                        } else {
+                            n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
+                            n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
+                        }
                     } else {
                         a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                         a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
@@ -2369,8 +2410,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                             const double a0 = newton_op(q[0], c.x, A.x, E.x);
                             const double a1 = newton_op(q[1], c.y, A.y, E.y);
                             const double2 fp = RECOMP ? fprev_l[j - 1][wx + WX * wy][lane] : Fprev[j - 1];
-                            o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
-                            o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
+                            if constexpr (SHY) {
+                                const double2 o = newton_update_y2(k, c, make_double2(fp.x - a0, fp.y - a1),
+                                                                   make_double2(k.preFac + A.x * E.x, k.preFac + A.y * E.y));
+                                o0 = o.x;
+                                o1 = o.y;
+                            } else {
+                                o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
+                                o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
+                            }
                         } else {
                             const double a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                             const double a1 = op_finish<MODE>(k, q[1], c.y, 0.0);

@@ -26,4 +26,11 @@ for r in 1 2; do
 done
 step rr-reverse
 bash tools/knob_ab.sh r04c/rrrev GS_RR_REVERSE 2 0 1 || exit 1
+step kprobe
+timeout -k 10 300 python tools/newton_kprobe.py 3 10 > "$OUT/kprobe.json" 2> "$OUT/kprobe.err" || { tail -20 "$OUT/kprobe.err"; exit 1; }
+cat "$OUT/kprobe.json"
+step ranks8-rocprof
+PROF=1 bash tools/bench_ranks.sh r04c/ranks8 8 256 --vcycles 2 --cpu-sweeps 0 --newton-iters 0 --config5 0 > "$OUT/ranks8.log" 2>&1 || { tail -30 "$OUT/ranks8.log"; exit 1; }
+tail -3 "$OUT/ranks8.log"
+python tools/rccl_grid.py gpurun_out/r04c/ranks8 | head -40
 step done
