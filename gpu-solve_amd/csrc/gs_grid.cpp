@@ -644,9 +644,11 @@ void HipSolver::solve(HipGridData& grid)
         return res <= initialResidual / (1.0 / grid.tol);
     };
     // The closing norm of the LAST cycle decides nothing (the loop ends at maxiter either way): when nobody
-    // reads it — no print, no history, no per-level clock; NewtonSolver::findError's inner solves — that
+    // reads it — no progress print, no history, no per-level clock; NewtonSolver::findError's inner solves — that
     // cycle ends with its up-leg and the norm's pass (a whole level-0 pair at 512^3) is not run
-    const bool lastNormDead = !print && history == nullptr && !grid.clock.on;
+    // (rank-uniform: every rank must run the same exchanges and collectives, so the decision rests on the
+    // grid's printProgress, not on `print`, which only rank 0 has)
+    const bool lastNormDead = !grid.printProgress && history == nullptr && !grid.clock.on;
     if (spec) {
         runCycles(grid, &pending, grid.maxiter, onNorm, lastNormDead);
     } else {

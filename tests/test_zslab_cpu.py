@@ -248,3 +248,18 @@ def test_newton_slab_schedule_fuses_the_update(monkeypatch):
     monkeypatch.setenv("GS_NO_NEWTON_FUSED_UPDATE", "1")
     names = [op for op, _ in X.schedule(p, 2, 0, -1)]
     assert "newtonFupdate" not in names and names.count("axpy") == 2
+
+
+@pytest.mark.parametrize("mode,dims,world", [(0, (64, 256, 64), 2), (0, (48, 256, 70), 3), (2, (255, 511, 63), 2),
+                                             (2, (64, 128, 96), 3)])
+def test_schedules_agree_on_collectives(mode, dims, world):
+    """Every rank's schedule issues the same exchanges, gathers and norm reductions in the same order (a rank
+    that skipped one — a rank-dependent branch in the driver — would deadlock or fail the real RCCL run)."""
+    import zslab_exec as X
+    p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=mode)
+    seqs = []
+    for r in range(world):
+        ops = X.schedule(p, world, r, -1)
+        seqs.append([(op, kv.get("L"), kv.get("field"), kv.get("depth"), kv.get("allgather"))
+                     for op, kv in ops if op in ("halo", "gather", "norm")])
+    assert all(s == seqs[0] for s in seqs[1:])
