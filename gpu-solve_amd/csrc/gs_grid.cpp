@@ -1257,6 +1257,7 @@ double NewtonSolver::compFUpdate(HipGridData& grid)
         }
     }
     L0.newtonV.swap(L0.vAlt);
+    if (grid.trace) grid.rec("swapnewton", {{"L", 0}});
     grid.halo(L0, L0.f, grid.stream());
     return HipSolver::finishNorm(grid, gs_residual_num_partials(&grid.stencilAbi, &L0.geom));
 }

@@ -91,7 +91,9 @@ void solveDistributed(const gs::GridParams& gridParams, int rank, int world)
         comm = gs::makeRcclComm(rank, world, uid);
     }
     gs::HipGridData grid(gridParams, comm.get());
-    grid.printProgress = rank == 0;
+    // (the solvers print on rank 0 only; printProgress itself must be the same on every rank: it decides
+    // whether the last closing norm, a collective, is computed)
+    grid.printProgress = true;
     if (gridParams.mode == gs::GridParams::NEWTON) gs::NewtonSolver::solve(grid);
     else gs::HipSolver::solve(grid);
     if (grid.clock.on && rank == 0) std::cout << gs::metricsLine(grid) << '\n';

@@ -38,6 +38,8 @@ struct GridParams {
     Stencil stencil{};
     Mode mode = LINEAR;
 
+    // rank 0 prints the solve's progress; on a Z-slab grid the flag must be the same on every rank (it also
+    // decides whether a solve's last, otherwise unread closing norm — a collective — is computed)
     bool printProgress = true;
 };
 

@@ -263,3 +263,58 @@ def test_schedules_agree_on_collectives(mode, dims, world):
         seqs.append([(op, kv.get("L"), kv.get("field"), kv.get("depth"), kv.get("allgather"))
                      for op, kv in ops if op in ("halo", "gather", "norm")])
     assert all(s == seqs[0] for s in seqs[1:])
+
+
+def _replay_newton_worker(rank, world, port, params, min_points, q, env):
+    import zslab_exec as X
+    os.environ.update(env)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ops = X.schedule(params, world, rank, min_points)
+        R = X.Rank(params, rank, world, min_points)
+        R.run(ops)
+        lo, hi, v = R.owned_v("v")
+        _, _, w = R.owned_v("newtonV")
+        q.put((rank, lo, hi, v, w, R.newton_history, sorted({op for op, _ in ops})))
+    except Exception:
+        import traceback
+        q.put((rank, None, None, None, None, traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fused", [True])  # (False, the two-pass axpy path, replays too: ~2 min more)
+def test_gloo_replay_newton_schedule(fused):
+    """NEWTON's Z-slab schedule (NewtonSolver: newtonF, the inner solves, findError's newtonV += v — fused into
+    the next compF with the new newtonV's ghost planes formed from both operands, or the two-pass axpy with
+    GS_NO_NEWTON_FUSED_UPDATE — and the per-level newtonV restriction) replayed on two gloo ranks with the
+    oracle's point expressions: Newton history, newtonV and v against the single-domain oracle solve. numpy's
+    exp stands in for libm's, so the comparison is to 1e-10, not bit for bit. A power-of-two grid: its inner
+    solves never meet their tol-0.1 exit, so the traced schedule — whose placeholder norms
+    never stop a loop — runs the ten inner V-cycles the oracle runs."""
+    dims, world = (256, 512, 64), 2
+    params = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=2)
+    env = {} if fused else {"GS_NO_NEWTON_FUSED_UPDATE": "1"}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replay_newton_worker, args=(r, world, port, params, -1, q, env)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=900) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] is not None, r[5]
+    og = O.Grid(dims, mode=O.NEWTON, maxiter=2)
+    ref_hist = og.solve()
+    ref_v, ref_w = og.field(0, "v").copy(), og.field(0, "newtonV").copy()
+    for rank, lo, hi, v, w, hist, ops in res:
+        assert ("newtonFupdate" in ops and "ghostsum" in ops) == fused and ("axpy" in ops) != fused, ops
+        assert len(hist) == len(ref_hist)
+        for a, b in zip(hist, ref_hist):
+            assert abs(a - b) <= 1e-10 * abs(b), (a, b)
+        np.testing.assert_allclose(w, ref_w[:, :, lo: hi + 1], rtol=0, atol=1e-10 * np.abs(ref_w).max())
+        np.testing.assert_allclose(v, ref_v[:, :, lo: hi + 1], rtol=0, atol=1e-9 * np.abs(ref_v).max())

@@ -7,7 +7,9 @@ reference's point expressions evaluated in the reference's order (src/cpu/CpuSol
 :211-290) on numpy float64 — so a correct schedule reproduces the single-domain oracle bit for bit, and
 a wrong one (a missing or misplaced exchange, a wrong plane range, a wrong ghost depth) does not.
 Ghost planes hold NaN until an exchange fills them, so any read of a stale ghost plane poisons the
-result. LINEAR mode (the schedule BASELINE config #5 runs).
+result. LINEAR mode (the schedule BASELINE config #5 runs) bit for bit; NEWTON mode (NewtonSolver.cpp:10-108:
+newtonF, the fused newtonV update with its ghost planes, the per-level newtonV restriction, the inner solves)
+with numpy's exp in place of libm's, so to ~1e-10 instead of bit for bit.
 
 Arrays use the reference layout (x, y, z), z last; a level's array covers global planes
 [base, base + NP) with base = lo - 2 on a Z-slab level (two ghost planes each side) and -1 on a
@@ -23,6 +25,7 @@ import gpusolve as gsv
 import oracle as O
 
 STENCIL = (6.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0)
+LINEAR, NEWTON = 0, 2
 
 
 def schedule(params, nranks, rank, min_points):
@@ -94,7 +97,8 @@ class Level:
             npl = self.nz + 4
         shape = (self.nx + 2, self.ny + 2, npl)
         nan = np.full(shape, np.nan)
-        self.fields = {"v": np.zeros(shape), "vAlt": np.zeros(shape), "f": np.zeros(shape), "r": np.zeros(shape)}
+        self.fields = {"v": np.zeros(shape), "vAlt": np.zeros(shape), "f": np.zeros(shape), "r": np.zeros(shape),
+                       "newtonV": np.zeros(shape), "newtonF": np.zeros(shape)}
         # ghost planes of f / r are unknown until exchanged (NaN: any read before poisons the result);
         # v and vAlt start as the zero iterate everywhere, ghost planes included, as on the device
         if dist_:
@@ -126,16 +130,32 @@ def stencil_div(A, zi, hh):
     return s / hh
 
 
-def sweep_planes(V, F, gplanes, L, omega, keep=None):
-    """One Jacobi sweep (CpuSolver.cpp:144-171, LINEAR) of array V at global planes gplanes: returns the
+def operator(V, zi, L, mode, W, gamma):
+    """A(V) at the interior x / y points of array planes zi: the stencil over h^2, plus NEWTON's
+    gamma (1 + w) v exp(w) with w = W (CpuSolver.cpp:56-66, reference order); also A = gamma (1 + w),
+    E = exp(w) for the update's denominator."""
+    s = stencil_div(V, zi, L.h * L.h)
+    if mode == NEWTON:
+        w = W[1:-1, 1:-1, zi]
+        A, E = gamma * (1 + w), np.exp(w)
+        return s + A * V[1:-1, 1:-1, zi] * E, A, E
+    return s, None, None
+
+
+def sweep_planes(V, F, gplanes, L, omega, keep=None, mode=LINEAR, W=None, gamma=1.0):
+    """One Jacobi sweep (CpuSolver.cpp:144-171) of array V at global planes gplanes: returns the
     new values of those planes (whole padded cross-sections; boundary rows / columns keep V) and the
     residual r = f - A V there."""
     zi = np.array([L.idx(g) for g in gplanes])
     hh = L.h * L.h
     alpha = hh / STENCIL[0]
-    r = F[1:-1, 1:-1, zi] - stencil_div(V, zi, hh)
+    a, A, E = operator(V, zi, L, mode, W, gamma)
+    r = F[1:-1, 1:-1, zi] - a
     out = V[:, :, zi].copy()
-    out[1:-1, 1:-1, :] = V[1:-1, 1:-1, zi] + omega * (alpha * r)
+    if mode == NEWTON:
+        out[1:-1, 1:-1, :] = V[1:-1, 1:-1, zi] + omega * (r / (STENCIL[0] / hh + A * E))
+    else:
+        out[1:-1, 1:-1, :] = V[1:-1, 1:-1, zi] + omega * (alpha * r)
     if keep is not None:
         for j, g in enumerate(gplanes):
             if keep(g):
@@ -193,6 +213,8 @@ class Rank:
         self.levels = [Level(dims[l], *pl[l], rank) for l in range(len(pl))]
         self.partial = 0.0
         self.history = []
+        self.mode, self.gamma = params.mode, params.gamma
+        self.newton_history, self._newton_norm = [], False
 
     # ---- communication (gloo) ----
     def halo(self, L, name, depth):
@@ -236,6 +258,9 @@ class Rank:
             total = self.partial
         self.partial = 0.0
         self.history.append(float(np.sqrt(total)))
+        if self._newton_norm:  # the norm of a newtonF pass: NewtonSolver's own residual
+            self.newton_history.append(self.history[-1])
+            self._newton_norm = False
 
     def fields(self, L, name):
         return L.fields[name]
@@ -243,6 +268,9 @@ class Rank:
     # ---- ops ----
     def v_in(self, L, vzero):
         return np.zeros_like(L.fields["v"]) if vzero else L.fields["v"]
+
+    def sw(self, L):
+        return dict(mode=self.mode, W=L.fields["newtonV"], gamma=self.gamma)
 
     def op_pair(self, L, z1, z2, zlo, zhi, vzero, norm, V=None):
         g1, g2 = L.local_to_global(z1), L.local_to_global(z2)
@@ -252,19 +280,20 @@ class Rank:
         # sweep 1 on g1-1 .. g2+1: planes outside the range are computed only on an internal side
         gp = list(range(g1 - 1, g2 + 2))
         keep = lambda g: (g == g1 - 1 and not zlo) or (g == g2 + 1 and not zhi)  # noqa: E731
-        S1, r = sweep_planes(V, F, gp, L, om, keep)
+        S1, r = sweep_planes(V, F, gp, L, om, keep, **self.sw(L))
         if norm:
             self.partial += float(np.sum(r[:, :, 1:-1] ** 2))
         W = V.copy()
         for j, g in enumerate(gp):
             W[:, :, L.idx(g)] = S1[:, :, j]
-        S2, _ = sweep_planes(W, F, list(range(g1, g2 + 1)), L, om)
+        S2, _ = sweep_planes(W, F, list(range(g1, g2 + 1)), L, om, **self.sw(L))
         out = L.fields["vAlt"]
         out[1:-1, 1:-1, L.idx(g1): L.idx(g2) + 1] = S2[1:-1, 1:-1, :]
 
     def op_sweep(self, L, z1, z2, vzero, norm):
         g1, g2 = L.local_to_global(z1), L.local_to_global(z2)
-        S, r = sweep_planes(self.v_in(L, vzero), L.fields["f"], list(range(g1, g2 + 1)), L, self.p.omega)
+        S, r = sweep_planes(self.v_in(L, vzero), L.fields["f"], list(range(g1, g2 + 1)), L, self.p.omega,
+                            **self.sw(L))
         if norm:
             self.partial += float(np.sum(r ** 2))
         L.fields["vAlt"][1:-1, 1:-1, L.idx(g1): L.idx(g2) + 1] = S[1:-1, 1:-1, :]
@@ -306,7 +335,8 @@ class Rank:
         inner = [j for j, g in enumerate(gplanes) if 1 <= g <= L.nz]
         if inner:
             zi = np.array([L.idx(gplanes[j]) for j in inner])
-            R[1:-1, 1:-1, inner] = L.fields["f"][1:-1, 1:-1, zi] - stencil_div(L.fields["v"], zi, hh)
+            a, _, _ = operator(L.fields["v"], zi, L, self.mode, L.fields["newtonV"], self.gamma)
+            R[1:-1, 1:-1, inner] = L.fields["f"][1:-1, 1:-1, zi] - a
         return R
 
     def op_resrestrict(self, L, Lc, c1, c2):
@@ -344,19 +374,22 @@ class Rank:
 
         vs = {}
 
+        m, g = self.mode, self.gamma
+
         def vc(l, v):
             L = self.levels[l]
             f = arr(L, "f")
+            w = arr(L, "newtonV") if m == NEWTON else None
             if l == nl - 1:
-                return O.jacobi(v, f, L.h, O.LINEAR, p.omega, 1.0, p.preSmoothing + p.postSmoothing)
-            v = O.jacobi(v, f, L.h, O.LINEAR, p.omega, 1.0, p.preSmoothing) if p.preSmoothing else v
-            r, _ = O.residual(v, f, L.h, O.LINEAR)
+                return O.jacobi(v, f, L.h, m, p.omega, g, p.preSmoothing + p.postSmoothing, w=w)
+            v = O.jacobi(v, f, L.h, m, p.omega, g, p.preSmoothing, w=w) if p.preSmoothing else v
+            r, _ = O.residual(v, f, L.h, m, g, w=w)
             C_ = self.levels[l + 1]
             put(C_, "f", O.restrict(r, (C_.nx, C_.ny, C_.nz)))
             vc_ = vc(l + 1, O.zeros(C_.nx, C_.ny, C_.nz))
             vs[l + 1] = vc_
             v = v + O.interpolate(vc_, (L.nx, L.ny, L.nz))
-            return O.jacobi(v, f, L.h, O.LINEAR, p.omega, 1.0, p.postSmoothing) if p.postSmoothing else v
+            return O.jacobi(v, f, L.h, m, p.omega, g, p.postSmoothing, w=w) if p.postSmoothing else v
 
         L0 = self.levels[frm]
         v0 = np.zeros((L0.nx + 2, L0.ny + 2, L0.nz + 2)) if vzero else arr(L0, "v")
@@ -365,13 +398,55 @@ class Rank:
         for l, v in vs.items():
             put(self.levels[l], "vAlt" if odd else "v", v)
 
+    # ---- Newton (NewtonSolver.cpp:48-81, 105-107) ----
+    def newton_f(self, L, W, gplanes):
+        """f = newtonF - N(W) on planes gplanes (N: the NONLINEAR operator, reference order), + partials."""
+        zi = np.array([L.idx(g) for g in gplanes])
+        s = stencil_div(W, zi, L.h * L.h)
+        w = W[1:-1, 1:-1, zi]
+        s = s + self.gamma * w * np.exp(w)
+        r = L.fields["newtonF"][1:-1, 1:-1, zi] - s
+        L.fields["f"][1:-1, 1:-1, zi] = r
+        self.partial += float(np.sum(r ** 2))
+        self._newton_norm = True
+
+    def op_newton_update(self, L):
+        """gs_newton_F_update: w' = newtonV + v formed wherever compF reads it (owned planes and the ghost
+        planes next to them), stored on the owned planes' interior into vAlt; f from w'."""
+        g1, g2 = L.lo - 1, L.hi + 1
+        W = np.full_like(L.fields["v"], np.nan)
+        sl = slice(L.idx(g1), L.idx(g2) + 1)
+        W[:, :, sl] = L.fields["newtonV"][:, :, sl] + L.fields["v"][:, :, sl]
+        own = slice(L.idx(L.lo), L.idx(L.hi) + 1)
+        L.fields["vAlt"][1:-1, 1:-1, own] = W[1:-1, 1:-1, own]
+        self.newton_f(L, W, list(range(L.lo, L.hi + 1)))
+
     def run(self, ops):
         Ls = self.levels
         for op, kv in ops:
             L = Ls[kv["L"]] if "L" in kv else None
             if op == "rhs":
-                f = O.rhs(L.nx, L.ny, L.nz, O.LINEAR)
+                f = O.rhs(L.nx, L.ny, L.nz, self.mode, self.gamma)
                 L.fields["f"][:, :, L.idx(L.lo): L.idx(L.hi) + 1] = f[:, :, L.lo: L.hi + 1]
+            elif op == "copy":  # f > newtonF (NewtonSolver.cpp:12), the whole local array
+                L.fields["newtonF"][:] = L.fields["f"]
+            elif op == "newtonF":
+                self.newton_f(L, L.fields["newtonV"], list(range(L.lo, L.hi + 1)))
+            elif op == "newtonFupdate":
+                self.op_newton_update(L)
+            elif op == "ghostsum":  # a ghost plane of the new newtonV: newtonV + 1.0 v (the axpy's value)
+                g = L.local_to_global(kv["plane"])
+                L.fields["vAlt"][:, :, L.idx(g)] = L.fields["newtonV"][:, :, L.idx(g)] + 1.0 * L.fields["v"][:, :, L.idx(g)]
+            elif op == "swapnewton":
+                L.fields["newtonV"], L.fields["vAlt"] = L.fields["vAlt"], L.fields["newtonV"]
+                # the second ghost layer came over from the iterate's buffer: never read as newtonV
+                for g in (L.lo - 2, L.hi + 2):
+                    L.fields["newtonV"][:, :, L.idx(g)] = np.nan
+            elif op == "axpy":  # newtonV += v over planes 0 .. nz+1 of the local array
+                sl = slice(L.idx(L.lo - 1), L.idx(L.hi + 1) + 1)
+                L.fields["newtonV"][:, :, sl] = L.fields["newtonV"][:, :, sl] + 1.0 * L.fields["v"][:, :, sl]
+            elif op == "nonorm":  # the last inner cycle's unread closing norm, not computed
+                pass
             elif op == "halo":
                 self.halo(L, kv["field"], kv["depth"])
             elif op == "gather":
@@ -414,6 +489,6 @@ class Rank:
             else:
                 raise NotImplementedError(op)
 
-    def owned_v(self):
+    def owned_v(self, name="v"):
         L = self.levels[0]
-        return L.lo, L.hi, L.fields["v"][:, :, L.idx(L.lo): L.idx(L.hi) + 1].copy()
+        return L.lo, L.hi, L.fields[name][:, :, L.idx(L.lo): L.idx(L.hi) + 1].copy()
