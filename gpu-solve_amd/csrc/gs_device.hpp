@@ -112,9 +112,11 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_RR_REVERSE=1      k_rr2 z-chunks in descending order (A/B)
 //   GS_NO_ZERO_Q         zero-iterate sweeps evaluate the stencil of their zeros instead of taking q = +0
 //   GS_XH_SWIZZLE=0|1    column-block pairs: the mirrored row's x-waves rotated by two (1) or not (0)
+//   GS_MID_ZC=n          z-chunk of pair launches over whole levels of < 2^26 points (A/B)
+//   GS_RR_ZC=n           z-chunk (coarse planes) of k_rr2 launches from fine levels of < 2^26 points (A/B)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ;
-    int xhSwizzle;
+    int xhSwizzle, midZc, rrZc;
     int slabZc, pairZc, rrNr, rrNtu, rrReverse;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
@@ -127,7 +129,7 @@ struct Knobs {
           pairXh(num("GS_PAIR_XH", 1) != 0), fitRounds(num("GS_FIT_ROUNDS", 1) != 0),
           bigChunks(num("GS_PAIR_BIG_CHUNKS", 1) != 0), oneRound(num("GS_PAIR_ONE_ROUND", 1) != 0),
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
-          xhSwizzle(num("GS_XH_SWIZZLE", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
+          xhSwizzle(num("GS_XH_SWIZZLE", 0)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
           rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 0)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
@@ -318,38 +320,6 @@ __device__ __forceinline__ double newton_update(const Coef& k, double v, double 
 #endif
 }
 
-// NEWTON's update with the quotient r / den formed from den's reciprocal y = hh_recip(den) (sharing y
-// between a pair's two sweeps through LDS or registers measured no better than recomputing it: it spills).
-// The gfx950 IEEE division is div_scale, rcp + two Newton steps, q = N y, e = fma(-D, q, N),
-// div_fmas(e, y, q), div_fixup: with 2^-300 <= |den| < 2^400 and 2^-400 <= |r| < 2^300 neither operand is
-// scaled, VCC stays clear (exponent gap < 768, no denormal reciprocal or quotient, numerator exponent > 53),
-// div_fmas is the plain fma and div_fixup returns q', so the three operations below equal r / den bit for
-// bit. Anything else (zero, NaN, inf, extreme magnitudes) takes the division itself.
-__device__ __forceinline__ bool newton_den_ok(double den)
-{
-    const double a = __builtin_fabs(den);
-    return a >= 0x1p-300 && a < 0x1p400;
-}
-// a row's two points at once: one branch for both (either both quotients fast, or both divided)
-__device__ __forceinline__ double2 newton_update_y2(const Coef& k, double2 v, double2 r, double2 den)
-{
-    const double ax = __builtin_fabs(r.x), ay = __builtin_fabs(r.y);
-    const bool ok = newton_den_ok(den.x) && newton_den_ok(den.y) && ax >= 0x1p-400 && ax < 0x1p300 &&
-                    ay >= 0x1p-400 && ay < 0x1p300;
-    double qx, qy;
-    if (ok) {
-        const double yx = hh_recip(den.x), yy = hh_recip(den.y);
-        qx = r.x * yx;
-        qy = r.y * yy;
-        const double ex = __builtin_fma(-den.x, qx, r.x), ey = __builtin_fma(-den.y, qy, r.y);
-        qx = __builtin_fma(ex, yx, qx);
-        qy = __builtin_fma(ey, yy, qy);
-    } else {
-        qx = r.x / den.x;
-        qy = r.y / den.y;
-    }
-    return make_double2(v.x + k.omega * qx, v.y + k.omega * qy);
-}
 __device__ __forceinline__ double wave_sum(double x)
 {
 #pragma unroll
@@ -616,13 +586,22 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
 // Same shape, grid, term order and partial-sum order as k_rb<NONLINEAR, 1> under pass_plan, so f, the
 // partials and the norm are bit-identical to the two launches; the caller guarantees that wout's
 // non-interior cells already hold what k_axpy would leave there (zeros on a whole level).
-template <int RY, int W, bool UN>
-__global__ __launch_bounds__(WAVE* W) void k_newton_upd(Coef k, const double* __restrict__ w,
+// RS: findError's restriction of the new newtonV onto level 1 (NewtonSolver.cpp:88-92, CpuSolver.cpp:211-238) in
+// the same pass: a wave's two rows are the fine rows 2Y-1, 2Y of coarse row Y (its upper halo row is 2Y+1), a
+// lane's pair the fine columns 2X-1, 2X (2X+1 from the next lane), and coarse plane Z is summed at step 2Z+1 from
+// the register window of planes 2Z-1 .. 2Z+1 (never from the slot in flight), in the reference's term order:
+// bit-identical to gs_restrict of the stored newtonV, whose 1.1 GB re-read at 512^3 it saves. The chunk of
+// planes is even; the last chunk runs one step past the level when nz is even (coarse plane nz / 2).
+// (three waves per SIMD, as the plain pass has: <= 168 VGPRs for the restriction's rings)
+template <int RY, int W, bool UN, bool RS = false>
+__global__ __launch_bounds__(WAVE* W, 3) void k_newton_upd(Coef k, const double* __restrict__ w,
                                                          const double* __restrict__ e, const double* __restrict__ F,
                                                          double* __restrict__ wout, double* __restrict__ fout,
                                                          double* __restrict__ partials, int nx, int ny, int nz,
-                                                         int64_t ldy, int64_t ldz, int ZC)
+                                                         int64_t ldy, int64_t ldz, int ZC, double* __restrict__ cw,
+                                                         int cnx, int cny, int cnz, int64_t cldy, int64_t cldz)
 {
+    static_assert(!RS || RY == 2, "the restriction takes two fine rows per wave");
     __shared__ double red[W];
     const int lane = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.y);
@@ -633,6 +612,7 @@ __global__ __launch_bounds__(WAVE* W) void k_newton_upd(Coef k, const double* __
     const int y0 = 1 + (blockIdx.y * W + wv) * RY;
     const int zb = 1 + blockIdx.z * ZC;
     const int ze = min(zb + ZC - 1, nz);
+    const int zlast = (RS && ze == nz) ? nz + 1 : ze;
     const int xle = x0 - 1;
     const int xre = min(x0 + 2 * WAVE, nx + 1);
     const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
@@ -647,6 +627,10 @@ __global__ __launch_bounds__(WAVE* W) void k_newton_upd(Coef k, const double* __
     // the ring of k_rb: plane z+1's halo rows, F, edges and plane z+2's rows in slot ph
     double2 P[RY], C[RY], NL[2][RY], FL[2][RY], HL[2][2];
     double EL[2][RY], ER[2][RY];
+    // RS: own rows at plane z-2, the upper halo row at planes z-1 / z-2, and the right-edge column (rows 2Y-1,
+    // 2Y, 2Y+1) at planes z-1 / z-2; EH: the halo row's right edge in the slot
+    double2 PP[RS ? RY : 1], Hh1, Hh2;
+    double EH[2], E1[3], E2[3];
     double sumsq = 0.0;
     auto load_slot = [&](const int s, const int64_t z1, const int64_t z2) {
 #pragma unroll
@@ -658,6 +642,7 @@ __global__ __launch_bounds__(WAVE* W) void k_newton_upd(Coef k, const double* __
         }
         HL[s][0] = lw2(xl + roff[0] + z1);
         HL[s][1] = lw2(xl + roff[RY + 1] + z1);
+        if constexpr (RS) EH[s] = lw1(xre + roff[RY + 1] + z1);
     };
     if (zb <= ze) {
         const int64_t zo = (int64_t)zb * ldz;
@@ -666,9 +651,22 @@ __global__ __launch_bounds__(WAVE* W) void k_newton_upd(Coef k, const double* __
             P[r] = lw2(xl + roff[r + 1] + zo - ldz);
             C[r] = lw2(xl + roff[r + 1] + zo);
         }
+        if constexpr (RS) {
+#pragma unroll
+            for (int r = 0; r < RY; r++) {
+                PP[r] = lw2(xl + roff[r + 1] + zo - 2 * ldz);
+                E1[r] = lw1(xre + roff[r + 1] + zo - ldz);
+                E2[r] = lw1(xre + roff[r + 1] + zo - 2 * ldz);
+            }
+            Hh1 = lw2(xl + roff[RY + 1] + zo - ldz);
+            Hh2 = lw2(xl + roff[RY + 1] + zo - 2 * ldz);
+            E1[2] = lw1(xre + roff[RY + 1] + zo - ldz);
+            E2[2] = lw1(xre + roff[RY + 1] + zo - 2 * ldz);
+        }
         load_slot(1, zo, zo + ldz);
     }
-    for (int z0 = zb; z0 <= ze; z0 += 2) {
+    const int X = 1 + (int)blockIdx.x * WAVE + lane, Yc = (y0 + 1) / 2;
+    for (int z0 = zb; z0 <= zlast; z0 += 2) {
 #pragma unroll
         for (int ph = 0; ph < 2; ph++) {
             const int z = z0 + ph;
@@ -698,6 +696,42 @@ __global__ __launch_bounds__(WAVE* W) void k_newton_upd(Coef k, const double* __
                         wout[q] = c.x;
                     }
                 }
+            }
+            if constexpr (RS) {
+                // coarse plane Z = (z - 1) / 2 from planes z-2 (PP), z-1 (P), z (C): fine (2X+ii, 2Y+jj, 2Z+kk)
+                const int Zc = (z - 1) >> 1;
+                const bool odd = z & 1;
+                // the fine column 2X+1 of each (row, plane): the next lane's 2X-1, the edge column for lane 63
+                const double2 rows[3][3] = {{PP[0], PP[1], Hh2}, {P[0], P[1], Hh1}, {C[0], C[1], HL[cs][1]}};
+                const double eg[3][3] = {{E2[0], E2[1], E2[2]}, {E1[0], E1[1], E1[2]}, {ER[cs][0], ER[cs][1], EH[cs]}};
+                if (odd && Zc >= 1 && Zc <= cnz) { // (wave-uniform; the DPP shifts need every lane)
+                    double acc = 0.0;
+#pragma unroll
+                    for (int ii = -1; ii <= 1; ii++)
+#pragma unroll
+                        for (int jj = -1; jj <= 1; jj++)
+#pragma unroll
+                            for (int kk = -1; kk <= 1; kk++) {
+                                const double fac = 0.125 * ((2.0 - (ii < 0 ? -ii : ii)) / 2.0) *
+                                                   ((2.0 - (jj < 0 ? -jj : jj)) / 2.0) *
+                                                   ((2.0 - (kk < 0 ? -kk : kk)) / 2.0);
+                                const double2 v2 = rows[kk + 1][jj + 1];
+                                const double t = ii < 0 ? v2.x
+                                                        : (ii == 0 ? v2.y
+                                                                   : lane_from_right<true>(v2.x, eg[kk + 1][jj + 1]));
+                                acc += fac * t;
+                            }
+                    if (X <= cnx && Yc <= cny) cw[X + (int64_t)Yc * cldy + (int64_t)Zc * cldz] = acc;
+                }
+                Hh2 = Hh1;
+                Hh1 = HL[cs][1];
+#pragma unroll
+                for (int i = 0; i < 3; i++) E2[i] = E1[i];
+                E1[0] = ER[cs][0];
+                E1[1] = ER[cs][1];
+                E1[2] = EH[cs];
+#pragma unroll
+                for (int r = 0; r < RY; r++) PP[r] = P[r];
             }
 #pragma unroll
             for (int r = 0; r < RY; r++) {
@@ -2068,8 +2102,6 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     constexpr int NS = PFD == 2 ? 4 : 2, UNR = PFD == 2 ? 4 : 2;
     double2 Vp[NV], Vc[NV], VL[NS][NV], FL[NS][NV], WL[NS][NV], HL[NS];
     double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
-    // SHY (NEWTON plain pairs on whole rows): the quotient r / den through den's reciprocal (newton_update_y)
-    constexpr bool SHY = MODE == GS_NEWTON && PRO == 0 && !XH;
     // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes A from the
     // newtonV rows at z-1 and reads E = exp(w) from LDS (same expressions, same values)
     constexpr bool RECOMP = MODE == GS_NEWTON && PRO != 0;
@@ -2360,15 +2392,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         if (RECOMP && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
                         a0 = newton_op(q[0], c.x, A.x, E.x);
                         a1 = newton_op(q[1], c.y, A.y, E.y);
-                        if constexpr (SHY) {
-                            const double2 n = newton_update_y2(k, c, make_double2(FL[cs][j].x - a0, FL[cs][j].y - a1),
-                                                               make_double2(k.preFac + A.x * E.x, k.preFac + A.y * E.y));
-                            n0 = n.x;
-                            n1 = n.y;
-                        } else {
-                            n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
-                            n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
-                        }
+                        n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
+                        n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
                     } else {
                         a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                         a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
@@ -2410,15 +2435,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                             const double a0 = newton_op(q[0], c.x, A.x, E.x);
                             const double a1 = newton_op(q[1], c.y, A.y, E.y);
                             const double2 fp = RECOMP ? fprev_l[j - 1][wx + WX * wy][lane] : Fprev[j - 1];
-                            if constexpr (SHY) {
-                                const double2 o = newton_update_y2(k, c, make_double2(fp.x - a0, fp.y - a1),
-                                                                   make_double2(k.preFac + A.x * E.x, k.preFac + A.y * E.y));
-                                o0 = o.x;
-                                o1 = o.y;
-                            } else {
-                                o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
-                                o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
-                            }
+                            o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
+                            o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
                         } else {
                             const double a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                             const double a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
@@ -2664,6 +2682,7 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
             if (wz > 0) c = std::max(2, wz);
         }
     }
+    if (kKnobs.midZc > 0 && L->z0 == 0 && L->nx * L->ny * L->nz < ((int64_t)1 << 26)) c = std::max(2, kKnobs.midZc);
     c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)
     *zc = (int)c;
     *grid = dim3((unsigned)tiles, (unsigned)((L->nz + c - 1) / c));

@@ -357,23 +357,6 @@ __global__ __launch_bounds__(256) void k_div_check(const double* __restrict__ a,
     ref[i] = a[i] / k.hh;
 }
 
-// newton_update_y2 (NEWTON pairs: r / den through den's reciprocal) against the plain division, bitwise:
-// element pairs (r[2i], r[2i+1]) with (den[2i], den[2i+1]) form one row's two points; omega = 1, v = 0, so the
-// result is +0 + q — compared with +0 + r / den
-__global__ __launch_bounds__(256) void k_ndiv_check(const double* __restrict__ r, const double* __restrict__ den,
-                                                    int64_t n2, Coef k, double* __restrict__ fast,
-                                                    double* __restrict__ ref)
-{
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n2) return;
-    const double2 rr = make_double2(r[2 * i], r[2 * i + 1]), dd = make_double2(den[2 * i], den[2 * i + 1]);
-    const double2 q = newton_update_y2(k, make_double2(0.0, 0.0), rr, dd);
-    fast[2 * i] = q.x;
-    fast[2 * i + 1] = q.y;
-    ref[2 * i] = 0.0 + k.omega * (rr.x / dd.x);
-    ref[2 * i + 1] = 0.0 + k.omega * (rr.y / dd.y);
-}
-
 __global__ __launch_bounds__(256) void k_triad(double* __restrict__ out, const double* __restrict__ a,
                                                const double* __restrict__ b, int64_t n2)
 {
@@ -606,18 +589,6 @@ int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, doub
     k.hh = hh;
     k.fastdiv = hh >= 0x1p-120 && hh <= 1.0;
     hipLaunchKernelGGL(k_div_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, n, k, fast, ref);
-    return launch_status();
-}
-
-int gs_debug_newton_div_check(const double* r, const double* den, int64_t n, double omega, double* fast, double* ref,
-                              hipStream_t st)
-{
-    if (!r || !den || !fast || !ref || n < 0 || (n & 1)) return GS_EINVAL;
-    if (n == 0) return 0;
-    Coef k{};
-    k.omega = omega;
-    const int64_t n2 = n / 2;
-    hipLaunchKernelGGL(k_ndiv_check, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, r, den, n2, k, fast, ref);
     return launch_status();
 }
 

@@ -1186,6 +1186,7 @@ void NewtonSolver::solve(HipGridData& grid)
     else
         check(gs_copy(grid.newtonF.data(), L0.f.data(), L0.f.span(), s), "gs_copy");
     const double initialResidual = compF(grid);
+    grid.newtonR1_ = false; // (the first findError restricts level 1 itself: fields may have been set since)
     if (history) history->push_back(initialResidual);
     if (print) std::cout << "Inital newton residual: " << initialResidual << '\n';
 
@@ -1238,12 +1239,22 @@ bool NewtonSolver::fusedUpdate(const HipGridData& grid)
 double NewtonSolver::compFUpdate(HipGridData& grid)
 {
     auto& L0 = grid.getLevel(0);
+    // single GPU: the next findError's restriction of newtonV onto level 1 (NewtonSolver.cpp:88-92) comes out of
+    // the same pass (gs_newton_F_update_restrict), so findError skips that 1.1 GB re-read at 512^3
+    const bool r1 = grid.numLevels() >= 3 && !(L0.distributed && grid.nranks() > 1) &&
+                    gs_newton_F_update_restrict_supported(&grid.stencilAbi, &L0.geom, &grid.getLevel(1).geom) != 0;
     if (grid.trace)
-        grid.rec("newtonFupdate", {{"L", 0}});
+        grid.rec("newtonFupdate", {{"L", 0}, {"restrict", r1}});
+    else if (r1)
+        check(gs_newton_F_update_restrict(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
+                                          grid.newtonF.data(), L0.vAlt.data(), L0.f.data(), grid.partials(),
+                                          grid.getLevel(1).newtonV.data(), &grid.getLevel(1).geom, grid.stream()),
+              "gs_newton_F_update_restrict");
     else
         check(gs_newton_F_update(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
                                  grid.newtonF.data(), L0.vAlt.data(), L0.f.data(), grid.partials(), grid.stream()),
               "gs_newton_F_update");
+    grid.newtonR1_ = r1;
     if (L0.distributed && grid.nranks() > 1) {
         // the ghost planes of w' = newtonV + v (see fusedUpdate)
         const int64_t ldz = L0.v.ldz();
@@ -1265,8 +1276,10 @@ double NewtonSolver::compFUpdate(HipGridData& grid)
 // NewtonSolver.cpp:83-108
 bool NewtonSolver::findError(HipGridData& grid)
 {
-    for (std::size_t i = 1; i + 1 < grid.numLevels(); i++)
+    for (std::size_t i = 1; i + 1 < grid.numLevels(); i++) {
+        if (i == 1 && grid.newtonR1_) continue; // restricted by the last compFUpdate, newtonV unchanged since
         HipSolver::restrict(grid, grid.getLevel(i - 1).newtonV, i - 1, grid.getLevel(i).newtonV);
+    }
 
     const bool keepPrint = grid.printProgress;
     grid.printProgress = false;
@@ -1287,6 +1300,7 @@ bool NewtonSolver::findError(HipGridData& grid)
     // whole local array, ghost planes included: both operands' ghosts are current, so the sum's are
     if (grid.trace) grid.rec("axpy", {{"L", 0}}, "newtonV+=v");
     else check(gs_axpy(L0.newtonV.data(), L0.v.data(), 1.0, L0.v.span(), grid.stream()), "gs_axpy");
+    grid.newtonR1_ = false;
     return false;
 }
 

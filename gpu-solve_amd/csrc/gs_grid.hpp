@@ -210,6 +210,8 @@ private:
     std::vector<double> dryParts_;
     long traceNorms_ = 0;
     bool haloPending_ = false; // an exchange issued by haloIssue, not settled
+    friend class NewtonSolver;
+    bool newtonR1_ = false;    // level 1's newtonV holds R(level 0's newtonV) (gs_newton_F_update_restrict)
     double haloCurMs_ = 0.0;   // host ms spent on that exchange so far
     double traceNorm();
     friend class HipSolver;

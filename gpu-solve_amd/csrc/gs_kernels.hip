@@ -354,6 +354,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         const int64_t chunks = (2048 + rows - 1) / rows;
         int64_t zc = (cl->nz + chunks - 1) / chunks;
         zc = zc < 1 ? 1 : (zc > 32 ? 32 : zc);
+        if (kKnobs.rrZc > 0 && !big) zc = kKnobs.rrZc; // (A/B: fine levels of < 2^26 points)
         const dim3 g((unsigned)rows, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
@@ -461,10 +462,37 @@ int gs_newton_F_update(const gs_stencil* S, const gs_level* L, double gamma, con
     const dim3 b(WAVE, RB_W);
     if (k.unit)
         hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, true>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials,
-                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc);
+                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, nullptr, 0, 0, 0, 0, 0);
     else
         hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, false>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials,
-                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc);
+                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, nullptr, 0, 0, 0, 0, 0);
+    return launch_status();
+}
+
+int gs_newton_F_update_restrict_supported(const gs_stencil* S, const gs_level* L, const gs_level* cl)
+{
+    // a whole level (z0 = 0) and its coarse level (n/2 per axis, the hierarchy's), RB_RY = 2 rows per wave
+    return (gs_newton_F_update_supported(S, L) && cl && !bad_level(cl) && L->z0 == 0 && cl->z0 == 0 &&
+            cl->nx == L->nx / 2 && cl->ny == L->ny / 2 && cl->nz == L->nz / 2 && cl->nx > 0 && cl->ny > 0 && cl->nz > 0)
+               ? 1
+               : 0;
+}
+
+int gs_newton_F_update_restrict(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* e,
+                                const double* F, double* w_out, double* f, double* partials, double* coarse_w,
+                                const gs_level* cl, hipStream_t st)
+{
+    if (!w || !e || !F || !w_out || !f || !coarse_w || w_out == w || w_out == e ||
+        !gs_newton_F_update_restrict_supported(S, L, cl))
+        return GS_EINVAL;
+    static_assert(RB_RY == 2, "the fused restriction takes two fine rows per wave");
+    const Coef k = make_coef(S, L, 0.0, gamma);
+    const PassPlan plan = pass_plan(S, L); // the same grid / partials as gs_newton_F_update
+    const dim3 b(WAVE, RB_W);
+#define GS_NUR(U) hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, U, true>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, coarse_w, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz)
+    if (k.unit) GS_NUR(true);
+    else GS_NUR(false);
+#undef GS_NUR
     return launch_status();
 }
 

@@ -97,6 +97,10 @@ KERNEL_API = {
     "gs_newton_F": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
                               C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_newton_F_update_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level)]),
+    "gs_newton_F_update_restrict_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.POINTER(gs_level)]),
+    "gs_newton_F_update_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.POINTER(gs_level), C.c_void_p]),
     "gs_newton_F_update": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_copy": (C.c_int, [C.c_void_p, C.c_void_p, i64, C.c_void_p]),
@@ -159,8 +163,6 @@ DIAG_API = {
     "gs_debug_sweep_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double,
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_debug_div_check": (C.c_int, [C.c_void_p, i64, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
-    "gs_debug_newton_div_check": (C.c_int, [C.c_void_p, C.c_void_p, i64, C.c_double, C.c_void_p, C.c_void_p,
-                                            C.c_void_p]),
     "gs_debug_num_pair_variants": (C.c_int, []),
     "gs_debug_pair_variant_name": (C.c_char_p, [C.c_int]),
     "gs_debug_pair_timestamps": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,

@@ -216,6 +216,13 @@ int gs_newton_F(const gs_stencil* S, const gs_level* L, double gamma, const doub
 int gs_newton_F_update_supported(const gs_stencil* S, const gs_level* L);
 int gs_newton_F_update(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* e,
                        const double* F, double* w_out, double* f, double* partials, hipStream_t stream);
+/* The same pass plus findError's restriction of the new newtonV onto the next level (NewtonSolver.cpp:88-92):
+ * coarse_w (the coarse level's newtonV, interior written) = R(w_out), bit-identical to gs_restrict(w_out, ...)
+ * after gs_newton_F_update; whole levels (z0 = 0) whose coarse level has n/2 points per axis. */
+int gs_newton_F_update_restrict_supported(const gs_stencil* S, const gs_level* L, const gs_level* coarse);
+int gs_newton_F_update_restrict(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* e,
+                                const double* F, double* w_out, double* f, double* partials, double* coarse_w,
+                                const gs_level* coarse, hipStream_t stream);
 
 /* dst[i] = src[i] for i < n (Vector3 copy-assignment: NewtonSolver.cpp:12 newtonF = f), non-temporal
  * streams; the buffers must not overlap unless dst == src. */

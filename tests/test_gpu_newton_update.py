@@ -72,6 +72,43 @@ def test_fused_update_equals_axpy_then_compF(dims, values):
     np.testing.assert_array_equal(e.to_xyz(), e0)
 
 
+@pytest.mark.parametrize("dims,values", [
+    ((512, 128, 64), (6, -1, -1, -1, -1, -1, -1)),   # even extents: the last chunk runs one step past the level
+    ((300, 150, 71), (6, -1, -1, -1, -1, -1, -1)),   # ragged x-blocks and rows, odd plane count
+    ((301, 151, 129), (6, -1, -1, -1, -1, -1, -1)),  # odd everywhere: coarse n/2 leaves the last fine line unread
+    ((260, 130, 130), (6.5, -1.25, -0.75, -1, -1, -1.5, -0.5)),  # non-unit stencil
+])
+def test_fused_update_restrict_equals_update_then_restrict(dims, values):
+    """gs_newton_F_update_restrict = gs_newton_F_update followed by gs_restrict of the new newtonV onto the next
+    level (NewtonSolver.cpp:88-92), bit for bit: w_out, f, the partials and every coarse point."""
+    S = gsv.Stencil(list(values), list(gsv.CANONICAL_OFFSETS)).to_abi()
+    rng = np.random.default_rng(sum(dims) + 1)
+    w0, e0 = interior_random(rng, dims, 0.7), interior_random(rng, dims, 0.3)
+    F0 = rng.uniform(-2, 2, tuple(d + 2 for d in dims))
+    h = 1.0 / (dims[1] + 1)
+    cd = tuple(d // 2 for d in dims)
+    w, e, F = DevField(*dims).from_xyz(w0), DevField(*dims).from_xyz(e0), DevField(*dims).from_xyz(F0)
+    L = w.level(h)
+    Lc = DevField(*cd).level(1.0 / (cd[1] + 1))
+    assert k().gs_newton_F_update_restrict_supported(C.byref(S), C.byref(L), C.byref(Lc)) == 1
+    n = k().gs_residual_num_partials(C.byref(S), C.byref(L))
+    w_ref, f_ref = DevField(*dims), DevField(*dims, fill=np.nan)
+    c_ref = DevField(*cd)
+    p_ref = torch.zeros(n, dtype=torch.float64, device="cuda")
+    ok(k().gs_newton_F_update(C.byref(S), C.byref(L), 1.0, w.ptr, e.ptr, F.ptr, w_ref.ptr, f_ref.ptr,
+                              p_ref.data_ptr(), stream()))
+    ok(k().gs_restrict(w_ref.ptr, C.byref(L), c_ref.ptr, C.byref(c_ref.level(Lc.h)), stream()))
+    w_got, f_got = DevField(*dims), DevField(*dims, fill=np.nan)
+    c_got = DevField(*cd)  # (the pass writes the coarse interior only, as gs_restrict does)
+    p_got = torch.full((n,), np.nan, dtype=torch.float64, device="cuda")
+    ok(k().gs_newton_F_update_restrict(C.byref(S), C.byref(L), 1.0, w.ptr, e.ptr, F.ptr, w_got.ptr, f_got.ptr,
+                                       p_got.data_ptr(), c_got.ptr, C.byref(c_got.level(Lc.h)), stream()))
+    np.testing.assert_array_equal(w_got.to_xyz(), w_ref.to_xyz())
+    np.testing.assert_array_equal(f_got.to_xyz()[1:-1, 1:-1, 1:-1], f_ref.to_xyz()[1:-1, 1:-1, 1:-1])
+    np.testing.assert_array_equal(p_got.cpu().numpy(), p_ref.cpu().numpy())
+    np.testing.assert_array_equal(c_got.to_xyz(), c_ref.to_xyz())
+
+
 def test_fused_update_refuses_what_it_cannot_run():
     S = gsv.Stencil([6, -1, -1, -1, -1, -1, -1], list(gsv.CANONICAL_OFFSETS)).to_abi()
     w = DevField(8, 8, 8)

@@ -420,6 +420,11 @@ class Rank:
         own = slice(L.idx(L.lo), L.idx(L.hi) + 1)
         L.fields["vAlt"][1:-1, 1:-1, own] = W[1:-1, 1:-1, own]
         self.newton_f(L, W, list(range(L.lo, L.hi + 1)))
+        return W
+
+    def op_newton_update_restrict(self, L, Lc, W):
+        """gs_newton_F_update_restrict (single domain): level 1's newtonV = R(w') in the same pass."""
+        Lc.fields["newtonV"][1:-1, 1:-1, Lc.idx(1): Lc.idx(Lc.nz) + 1] = restrict_planes(W, L, Lc, 1, Lc.nz)
 
     def run(self, ops):
         Ls = self.levels
@@ -433,7 +438,9 @@ class Rank:
             elif op == "newtonF":
                 self.newton_f(L, L.fields["newtonV"], list(range(L.lo, L.hi + 1)))
             elif op == "newtonFupdate":
-                self.op_newton_update(L)
+                W = self.op_newton_update(L)
+                if kv.get("restrict"):
+                    self.op_newton_update_restrict(L, Ls[kv["L"] + 1], W)
             elif op == "ghostsum":  # a ghost plane of the new newtonV: newtonV + 1.0 v (the axpy's value)
                 g = L.local_to_global(kv["plane"])
                 L.fields["vAlt"][:, :, L.idx(g)] = L.fields["newtonV"][:, :, L.idx(g)] + 1.0 * L.fields["v"][:, :, L.idx(g)]

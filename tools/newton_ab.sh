@@ -14,5 +14,5 @@ done
 for v in "$@"; do
   env $VAR=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$v -o run --output-format csv -- \
       python tools/newton_prof.py > $O/prof_$v.log 2>&1 || { tail -20 $O/prof_$v.log; exit 1; }
-  echo "== $VAR=$v"; python tools/kernel_agg.py "$(find $O/prof_$v -name '*kernel_trace.csv' -print -quit)" | head -14
+  echo "== $VAR=$v"; python tools/kernel_agg.py "$(find $O/prof_$v -name '*kernel_trace.csv' -print -quit)" | head -14 || true
 done
