@@ -217,6 +217,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         if (l + 1 < nlev) L.r = DeviceField(nx, ny, nz, s, dry); // restriction source
         if (mode == NONLINEAR && l > 0) L.restV = DeviceField(nx, ny, nz, s, dry);
         if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s, dry);
+        if (mode == NEWTON && l == 1 && nlev >= 3 && !L.distributed) L.newtonVNext = DeviceField(nx, ny, nz, s, dry);
         L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), L.lo - 1, L.h};
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
         maxParts = std::max(maxParts, gs_jacobi_sweep2_num_partials(&stencilAbi, &L.geom, (int)mode));
@@ -1242,13 +1243,14 @@ double NewtonSolver::compFUpdate(HipGridData& grid)
     // single GPU: the next findError's restriction of newtonV onto level 1 (NewtonSolver.cpp:88-92) comes out of
     // the same pass (gs_newton_F_update_restrict), so findError skips that 1.1 GB re-read at 512^3
     const bool r1 = grid.numLevels() >= 3 && !(L0.distributed && grid.nranks() > 1) &&
+                    (grid.trace || grid.getLevel(1).newtonVNext.data() != nullptr) &&
                     gs_newton_F_update_restrict_supported(&grid.stencilAbi, &L0.geom, &grid.getLevel(1).geom) != 0;
     if (grid.trace)
         grid.rec("newtonFupdate", {{"L", 0}, {"restrict", r1}});
     else if (r1)
         check(gs_newton_F_update_restrict(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
                                           grid.newtonF.data(), L0.vAlt.data(), L0.f.data(), grid.partials(),
-                                          grid.getLevel(1).newtonV.data(), &grid.getLevel(1).geom, grid.stream()),
+                                          grid.getLevel(1).newtonVNext.data(), &grid.getLevel(1).geom, grid.stream()),
               "gs_newton_F_update_restrict");
     else
         check(gs_newton_F_update(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
@@ -1277,7 +1279,12 @@ double NewtonSolver::compFUpdate(HipGridData& grid)
 bool NewtonSolver::findError(HipGridData& grid)
 {
     for (std::size_t i = 1; i + 1 < grid.numLevels(); i++) {
-        if (i == 1 && grid.newtonR1_) continue; // restricted by the last compFUpdate, newtonV unchanged since
+        if (i == 1 && grid.newtonR1_) { // restricted by the last compFUpdate; level 0's newtonV unchanged since
+            grid.getLevel(1).newtonV.swap(grid.getLevel(1).newtonVNext);
+            if (grid.trace) grid.rec("swapnewton", {{"L", 1}});
+            grid.newtonR1_ = false;
+            continue;
+        }
         HipSolver::restrict(grid, grid.getLevel(i - 1).newtonV, i - 1, grid.getLevel(i).newtonV);
     }
 

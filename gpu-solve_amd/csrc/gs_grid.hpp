@@ -99,6 +99,8 @@ public:
         DeviceField vAlt;    // Jacobi ping-pong partner (the fused sweep reads v, writes vAlt)
         DeviceField restV;   // restricted v (FAS)
         DeviceField newtonV; // Newton linearisation point
+        DeviceField newtonVNext; // (level 1, single GPU) R(level 0's newtonV) from the last compF update, swapped
+                                 // in by the next findError — until then newtonV keeps the reference's value
         DeviceField f;       // right-hand side
         DeviceField r;       // residual (restriction source)
         std::array<std::size_t, 3> levelDim{}; // global interior extents
@@ -211,7 +213,7 @@ private:
     long traceNorms_ = 0;
     bool haloPending_ = false; // an exchange issued by haloIssue, not settled
     friend class NewtonSolver;
-    bool newtonR1_ = false;    // level 1's newtonV holds R(level 0's newtonV) (gs_newton_F_update_restrict)
+    bool newtonR1_ = false;    // level 1's newtonVNext holds R(level 0's newtonV) (gs_newton_F_update_restrict)
     double haloCurMs_ = 0.0;   // host ms spent on that exchange so far
     double traceNorm();
     friend class HipSolver;

@@ -424,7 +424,8 @@ class Rank:
 
     def op_newton_update_restrict(self, L, Lc, W):
         """gs_newton_F_update_restrict (single domain): level 1's newtonV = R(w') in the same pass."""
-        Lc.fields["newtonV"][1:-1, 1:-1, Lc.idx(1): Lc.idx(Lc.nz) + 1] = restrict_planes(W, L, Lc, 1, Lc.nz)
+        Lc.fields["vAlt_newton"] = Lc.fields.get("vAlt_newton", np.zeros_like(Lc.fields["newtonV"]))
+        Lc.fields["vAlt_newton"][1:-1, 1:-1, Lc.idx(1): Lc.idx(Lc.nz) + 1] = restrict_planes(W, L, Lc, 1, Lc.nz)
 
     def run(self, ops):
         Ls = self.levels
@@ -444,6 +445,8 @@ class Rank:
             elif op == "ghostsum":  # a ghost plane of the new newtonV: newtonV + 1.0 v (the axpy's value)
                 g = L.local_to_global(kv["plane"])
                 L.fields["vAlt"][:, :, L.idx(g)] = L.fields["newtonV"][:, :, L.idx(g)] + 1.0 * L.fields["v"][:, :, L.idx(g)]
+            elif op == "swapnewton" and kv["L"] > 0:  # findError takes the fused update's restriction
+                L.fields["newtonV"], L.fields["vAlt_newton"] = L.fields["vAlt_newton"], L.fields["newtonV"]
             elif op == "swapnewton":
                 L.fields["newtonV"], L.fields["vAlt"] = L.fields["vAlt"], L.fields["newtonV"]
                 # the second ghost layer came over from the iterate's buffer: never read as newtonV
