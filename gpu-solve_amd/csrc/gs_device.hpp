@@ -31,6 +31,8 @@
 //   GS_EXP_NOBAR  the pair's and k_rr2's per-plane LDS barriers removed (what the lock-step costs)
 //   GS_EXP_NOEXP  exp(x) replaced by one multiplication (what the exponentials cost)
 //   GS_EXP_NODIV  NEWTON's r / den replaced by a multiplication (what the divisions cost)
+//   GS_EXP_EFIELD k_tb2y's NEWTON sweep-1 rows load E = exp(w) from a second field instead of evaluating it
+//                 (the field lies GS_EXP_EFOFF elements past newtonV; tools/newton_kprobe.py sets both)
 #ifdef GS_EXP_NOEXP
 #define exp(x) ((x) * 1.0000001)
 #endif
@@ -74,6 +76,9 @@ struct Coef {
                    // iterate over hh is exactly +0 (each s[i] * 0 is a signed zero, +0 plus a signed zero is
                    // +0, +0 / hh is +0), so zero-iterate sweeps take q = +0 without evaluating it
     int64_t off[7]; // generic kernel: linear element offsets of the 7 entries
+#ifdef GS_EXP_EFIELD
+    int64_t efoff;
+#endif
 };
 
 bool canonical_order(const gs_stencil* S)
@@ -109,9 +114,9 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_RR_LDS            residual + restriction through the LDS kernel (k_resrestrict) only
 //   GS_RR_NR=1|2         coarse rows per k_rr2 block (default: 2 on LINEAR levels of >= 2^26 points)
 //   GS_RR_NTU=0|2        k_rr2 non-temporal loads never / always (default: two-row blocks only)
-//   GS_RR_REVERSE=1      k_rr2 z-chunks in descending order (A/B)
+//   GS_RR_REVERSE=0|1    k_rr2 z-chunks in ascending (0) or descending (1, default: r04e, -1% on 512^3) order
 //   GS_NO_ZERO_Q         zero-iterate sweeps evaluate the stencil of their zeros instead of taking q = +0
-//   GS_XH_SWIZZLE=0|1    column-block pairs: the mirrored row's x-waves rotated by two (1) or not (0)
+//   GS_XH_SWIZZLE=0|1    column-block pairs: the mirrored row's x-waves rotated by two (1, default) or not (0)
 //   GS_MID_ZC=n          z-chunk of pair launches over whole levels of < 2^26 points (A/B)
 //   GS_RR_ZC=n           z-chunk (coarse planes) of k_rr2 launches from fine levels of < 2^26 points (A/B)
 struct Knobs {
@@ -129,8 +134,8 @@ struct Knobs {
           pairXh(num("GS_PAIR_XH", 1) != 0), fitRounds(num("GS_FIT_ROUNDS", 1) != 0),
           bigChunks(num("GS_PAIR_BIG_CHUNKS", 1) != 0), oneRound(num("GS_PAIR_ONE_ROUND", 1) != 0),
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
-          xhSwizzle(num("GS_XH_SWIZZLE", 0)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
-          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 0)),
+          xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
+          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 1)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
     }
@@ -155,6 +160,9 @@ Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamm
     k.swz = kKnobs.xhSwizzle;
     k.zq = kKnobs.zeroQ && std::isnormal(k.hh) && k.hh > 0.0;
     for (int i = 0; i < 7; i++) k.zq = k.zq && std::isfinite(S->s[i]);
+#ifdef GS_EXP_EFIELD
+    k.efoff = getenv("GS_EXP_EFOFF") ? strtoll(getenv("GS_EXP_EFOFF"), nullptr, 10) : 0;
+#endif
     return k;
 }
 
@@ -2102,6 +2110,9 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     constexpr int NS = PFD == 2 ? 4 : 2, UNR = PFD == 2 ? 4 : 2;
     double2 Vp[NV], Vc[NV], VL[NS][NV], FL[NS][NV], WL[NS][NV], HL[NS];
     double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
+#ifdef GS_EXP_EFIELD
+    double2 XL[NS][NV];
+#endif
     // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes A from the
     // newtonV rows at z-1 and reads E = exp(w) from LDS (same expressions, same values)
     constexpr bool RECOMP = MODE == GS_NEWTON && PRO != 0;
@@ -2125,6 +2136,9 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             VL[s][j] = ldv2<ZV>(at(v, j, zv));
             FL[s][j] = ld2s<NTF>(at(f, j, z));
             if (MODE == GS_NEWTON) WL[s][j] = ld2(at(w, j, z));
+#ifdef GS_EXP_EFIELD
+            if (MODE == GS_NEWTON) XL[s][j] = ld2(at(w, j, z) + k.efoff);
+#endif
         }
         HL[s] = ldv2<ZV>(at(v, -1, z));
         if constexpr (XH) {
@@ -2384,7 +2398,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                     if constexpr (MODE == GS_NEWTON) {
                         const double2 wv = WL[cs][j];
                         const double2 A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
+#ifdef GS_EXP_EFIELD
+                        const double2 E = XL[cs][j];
+#else
                         const double2 E = make_double2(exp(wv.x), exp(wv.y));
+#endif
                         if (!RECOMP && j >= 1) {
                             Acur[j - 1] = A;
                             Ecur[j - 1] = E;

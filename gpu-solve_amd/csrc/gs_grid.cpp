@@ -730,9 +730,13 @@ static bool proSlabOk(HipGridData& grid, std::size_t l)
 
 // NEWTON's fused prolongation pair keeps part of its state in LDS and recomputes exp(newtonV) for
 // its second sweep: on 512^3 it saves 0.14 ms per V-cycle against gs_prolong_add + the plain pair, on
-// 256^3 / 128^3 it costs 0.065 / 0.05 ms more (profiles/r01l_summary.md), so NEWTON levels take it
-// from GS_NEWTON_PRO_POINTS (default 2^26) points per rank on (judged on the thinnest slab: rank-
-// uniform). LINEAR levels always do.
+// 256^3 / 128^3 it cost 0.065 / 0.05 ms more (profiles/r01l_summary.md). Since r04 levels of at most
+// two 256-point y-blocks launch a two-x-wave instance (74 KB of LDS, two blocks per CU), which wins on
+// 512^3's level 1 and 256^3's level 0 too (Newton iteration 36.5-36.6 against 36.7-36.75 ms at 512^3,
+// 6.32-6.36 against 6.58-6.62 ms at 256^3: profiles/r04/r04e_newton_ab_swizzle_rrreverse.txt,
+// r04f_newton_pro_threshold.txt),
+// so NEWTON levels take it from GS_NEWTON_PRO_POINTS (default 2^24) points per rank on (judged on the
+// thinnest slab: rank-uniform). LINEAR levels always do.
 static bool proWorthIt(HipGridData& grid, std::size_t l)
 {
     if (grid.mode != GridParams::NEWTON) return true;

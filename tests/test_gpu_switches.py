@@ -31,13 +31,13 @@ CASES = {
                                           ("GS_COARSE_POINTS", "4096"), ("GS_NO_ZERO_Q", "1"),
                                           ("GS_MID_ZC", "32"), ("GS_RR_ZC", "5")]),
     "linear2e26": ((0, 512, 512, 256, 2), [("GS_RR_NR", "1"), ("GS_PAIR_BIG_CHUNKS", "0"), ("GS_RR_NTU", "0")]),
-    "linear512": ((0, 512, 512, 512, 2), [("GS_PAIR_ONE_ROUND", "0"), ("GS_PAIR_ZC", "96"), ("GS_RR_REVERSE", "1")]),
-    "linear_rows700": ((0, 700, 64, 64, 3), [("GS_PAIR_XH", "0"), ("GS_TBX_PFD", "1"), ("GS_XH_SWIZZLE", "1")]),
+    "linear512": ((0, 512, 512, 512, 2), [("GS_PAIR_ONE_ROUND", "0"), ("GS_PAIR_ZC", "96"), ("GS_RR_REVERSE", "0")]),
+    "linear_rows700": ((0, 700, 64, 64, 3), [("GS_PAIR_XH", "0"), ("GS_TBX_PFD", "1"), ("GS_XH_SWIZZLE", "0")]),
     # two loopback slabs of 512^3: the interior launches of the overlapped sweeps (z0 != 0)
     "slabs512": ((0, 512, 512, 1024, 2, 2, 2, 2), [("GS_SLAB_ZC", "16"), ("GS_HALO_ORDER", "1")]),
     "newton127": ((2, 127, 127, 127, 2), [("GS_NEWTON_PRO_POINTS", "0"), ("GS_NO_FUSED_PROLONG", "1"),
                                           ("GS_NO_PIPELINE", "1"), ("GS_NO_NEWTON_FUSED_UPDATE", "1"),
-                                          ("GS_RR_REVERSE", "1"), ("GS_NO_ZERO_Q", "1")]),
+                                          ("GS_RR_REVERSE", "0"), ("GS_NO_ZERO_Q", "1")]),
 }
 PARAMS = [(case, sw, val) for case, (_, sws) in CASES.items() for sw, val in sws]
 _default = {}
