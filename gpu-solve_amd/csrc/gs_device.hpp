@@ -32,7 +32,7 @@
 //   GS_EXP_NOEXP  exp(x) replaced by one multiplication (what the exponentials cost)
 //   GS_EXP_NODIV  NEWTON's r / den replaced by a multiplication (what the divisions cost)
 //   GS_EXP_EFIELD k_tb2y's NEWTON sweep-1 rows load E = exp(w) from a second field instead of evaluating it
-//                 (the field lies GS_EXP_EFOFF elements past newtonV; tools/newton_kprobe.py sets both)
+//                 (the field lies gs_exp_set_efoff(n) elements past newtonV; tools/newton_kprobe.py sets it)
 #ifdef GS_EXP_NOEXP
 #define exp(x) ((x) * 1.0000001)
 #endif
@@ -142,6 +142,10 @@ struct Knobs {
 };
 const Knobs kKnobs;
 
+#ifdef GS_EXP_EFIELD
+int64_t gs_exp_efoff = 0; // set by gs_exp_set_efoff (gs_kernels.hip, this build only)
+#endif
+
 Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamma)
 {
     Coef k;
@@ -161,7 +165,7 @@ Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamm
     k.zq = kKnobs.zeroQ && std::isnormal(k.hh) && k.hh > 0.0;
     for (int i = 0; i < 7; i++) k.zq = k.zq && std::isfinite(S->s[i]);
 #ifdef GS_EXP_EFIELD
-    k.efoff = getenv("GS_EXP_EFOFF") ? strtoll(getenv("GS_EXP_EFOFF"), nullptr, 10) : 0;
+    k.efoff = gs_exp_efoff;
 #endif
     return k;
 }
@@ -2034,8 +2038,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     static_assert(PRO == 0 || (SPEC && !ZV && RY % 2 == 0), "fused prolongation: per-wave code, even RY");
     static_assert(!TS || (PRO == 0 && !XH), "timestamps: plain pairs (es carries the buffer)");
     const uint64_t tstart = TS ? wall_clock64() : 0;
-    static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR) && RY + 2 <= WAVE),
-                  "column blocks: LINEAR / NONLINEAR pairs, LINEAR prolongation pairs");
+    static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR || MODE == GS_NEWTON) && RY + 2 <= WAVE),
+                  "column blocks: every pair, LINEAR / NEWTON prolongation pairs");
     constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
     constexpr int NE = NV + RY; // x-edge values per wave side: v rows 0..RY, sweep-1 rows 1..RY
     __shared__ double red[2 * WXMAX];
@@ -2636,14 +2640,15 @@ int slab_zc() { return kKnobs.slabZc; }
 int whole_zc() { return kKnobs.pairZc; }
 
 int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* block, bool* y2 = nullptr,
-             int mode = GS_LINEAR, bool* xh = nullptr)
+             int mode = GS_LINEAR, bool* xh = nullptr, bool pro = false)
 {
     if (!S || !L || !canonical_order(S) || L->nx < 1 || L->ny < 1 || L->nz < 1) return 0;
     const bool two = L->nx <= 2 * WAVE * TBY_WX;
-    // NEWTON: column blocks only where k_tb2 has no shape (rows > 1024 points): the NEWTON column-block pair
-    // carries the edge column's newtonV too and spills (~45 VGPRs), k_tb2 does not
+    // NEWTON plain pairs: column blocks only where k_tb2 has no shape (rows > 1024 points): the NEWTON
+    // column-block pair carries the edge column's newtonV too and spills (~45 VGPRs), k_tb2 does not.
+    // NEWTON prolongation pairs (pro) have no k_tb2 form: column blocks from 513 points
     const bool colb = !two && xh_enabled() && L->nx <= (int64_t)1 << 20 &&
-                      (mode != GS_NEWTON || L->nx > 2 * WAVE * TB_WX_B);
+                      (mode != GS_NEWTON || pro || L->nx > 2 * WAVE * TB_WX_B);
     if (!two && !colb && L->nx > 2 * WAVE * TB_WX_B) return 0;
     const int64_t nh = colb ? (L->nx + 2 * WAVE * TBY_WX - 1) / (2 * WAVE * TBY_WX) : 1;
     const int rows = (two || colb) ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block

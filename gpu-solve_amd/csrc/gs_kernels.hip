@@ -154,11 +154,12 @@ int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, i
     int zc;
     dim3 g, b;
     bool y2 = false, xh = false;
-    // LINEAR and NEWTON (NONLINEAR carries restV too). Rows of more than 512 points (column blocks, XH):
-    // LINEAR, with the workspace of gs_jacobi_sweep2_prolong_ws_elems (the corrected edge columns).
-    // The fine planes' parities must be the global ones (even z0): they select each plane's combination
+    // LINEAR and NEWTON (NONLINEAR carries restV too). Rows of more than 512 points (column blocks, XH,
+    // NEWTON too since r04) with the workspace of gs_jacobi_sweep2_prolong_ws_elems (the corrected edge
+    // columns). The fine planes' parities must be the global ones (even z0): they select each plane's
+    // combination
     return !bad_level(L) && valid_stencil(S) && (mode == GS_LINEAR || mode == GS_NEWTON) && L->z0 % 2 == 0 &&
-           tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh) && (y2 || (xh && mode == GS_LINEAR));
+           tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh, true) && (y2 || xh);
 }
 
 int64_t gs_jacobi_sweep2_prolong_ws_elems(const gs_stencil* S, const gs_level* L, int mode)
@@ -166,7 +167,7 @@ int64_t gs_jacobi_sweep2_prolong_ws_elems(const gs_stencil* S, const gs_level* L
     int zc;
     dim3 g, b;
     bool y2 = false, xh = false;
-    if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh) || !xh)
+    if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh, true) || !xh)
         return 0;
     const int64_t bw = 2 * WAVE * TBY_WX, nb = (L->nx + bw - 1) / bw - 1; // interior block boundaries
     return nb * (L->nz + 4) * 4 * (L->ny + 2);
@@ -193,7 +194,7 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || bad_level(cl) || czoff < 0 || !v_in || !coarse_v ||
         !v_out || !f || v_in == v_out || (mode == GS_NONLINEAR) != (coarse_sub != nullptr) || (mode == GS_NEWTON && !w) ||
         (L->nx + 1) / 2 > cl->nx + 1 || (L->ny + 1) / 2 > cl->ny + 1 || (L->nz + 1) / 2 + czoff > cl->nz + 1 ||
-        !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh))
+        !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh, true))
         return GS_EINVAL;
     const int64_t need = gs_jacobi_sweep2_prolong_ws_elems(S, L, mode);
     if (need > 0 && (!ws || ws_elems < need)) return GS_EINVAL;
@@ -212,7 +213,9 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     // NEWTON's variant keeps ~37 KB of state per x-wave in LDS (its RECOMP rows): rows of <= 256 points
     // (two x-waves) take the instance sized for two, so that two blocks share a CU (8 waves, the VGPR
     // limit) instead of one block of 4 waves holding the whole LDS of a four-x-wave instance
-    if (mode == GS_NEWTON && b.y <= 2) GS_TBP(GS_NEWTON, 1, false, 2);
+    // (NEWTON column blocks: the RECOMP LDS state and the edge columns together, 144 B per lane spilled)
+    if (mode == GS_NEWTON && xh) GS_TBP(GS_NEWTON, 1, true, TBY_WX);
+    else if (mode == GS_NEWTON && b.y <= 2) GS_TBP(GS_NEWTON, 1, false, 2);
     else if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1, false, TBY_WX);
     else if (xh) GS_TBP(GS_LINEAR, 1, true, TBY_WX);
     else GS_TBP(GS_LINEAR, 1, false, TBY_WX);
@@ -579,3 +582,8 @@ const char* gs_build_info(void)
 }
 
 } // extern "C"
+
+#ifdef GS_EXP_EFIELD
+// timing-only build (gs_device.hpp): the E field's element distance from newtonV
+extern "C" void gs_exp_set_efoff(int64_t n) { gs_exp_efoff = n; }
+#endif

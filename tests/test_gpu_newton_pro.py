@@ -39,13 +39,16 @@ def solve(params):
 
 
 @pytest.mark.parametrize("dims,pre,post", [((64, 64, 64), 2, 2), ((33, 31, 29), 3, 3), ((40, 24, 48), 1, 2),
-                                           ((130, 66, 34), 2, 3)])
+                                           ((130, 66, 34), 2, 3),
+                                           # rows > 512 points: the column-block NEWTON prolongation pair (r04)
+                                           ((1400, 12, 10), 2, 2), ((1100, 20, 18), 2, 2), ((1024, 16, 16), 2, 3)])
 def test_newton_fused_prolong_bit_identical(dims, pre, post):
     p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=gsv.GS_NEWTON, preSmoothing=pre, postSmoothing=post)
     with env(GS_NEWTON_PRO_POINTS=1 << 62):
         h_ref, f_ref = solve(p)
     with env(GS_NEWTON_PRO_POINTS=0):
         h_got, f_got = solve(p)
+    assert np.all(np.isfinite(h_ref)), h_ref
     assert h_got == h_ref
     for key, a in f_ref.items():
         np.testing.assert_array_equal(f_got[key], a, err_msg=str(key))

@@ -224,11 +224,9 @@ def test_prolong_fused_pair_bit_identical(shape, mode):
     w0 = rand_full(rng, *shape, 0.5)
     L = DevField(nx, ny, nz).level(h)
     supported = k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), mode)
-    # the fused prolongation pair exists for every LINEAR shape and for NEWTON rows of <= 512 points; NEWTON's
-    # longer rows are refused (the driver then runs gs_prolong_add + the plain pair, tests below)
-    assert supported == (1 if mode == 0 or nx <= 512 else 0), (shape, mode, supported)
-    if not supported:
-        return
+    # the fused prolongation pair exists for every LINEAR and NEWTON shape (NEWTON rows > 512 points: column
+    # blocks since r04, against k_tb2's plain pair as the reference here)
+    assert supported == 1, (shape, mode, supported)
     # reference: prolongation + correction stored, then the plain fused pair
     v, f, c, out_ref = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
                         DevField(*cd).from_xyz(c0), DevField(nx, ny, nz))
@@ -261,14 +259,16 @@ PRO_SPLITS = [((64, 64, 64), [(1, 2), (63, 64), (3, 62)]),
               ((1100, 5, 20), [(1, 6), (7, 12), (13, 20)])]
 
 
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("coarse_view", [False, True])
 @pytest.mark.parametrize("shape,ranges", PRO_SPLITS)
-def test_prolong_fused_pair_plane_ranges(shape, ranges, coarse_view):
+def test_prolong_fused_pair_plane_ranges(shape, ranges, coarse_view, mode):
     """gs_jacobi_sweep2_prolong on plane ranges (z0 > 0, internal sides flagged zlo / zhi, whose
     planes the kernel corrects as it reads them) assembles the whole-level result bit for bit. With
     coarse_view the coarse level is passed as the plane range under the fine one (a Z-slab coarse
-    level: coarse z0 = fine z0 / 2, its ghost plane -1 read), else whole (a replicated coarse level)."""
-    rng = np.random.default_rng(sum(shape) * 7 + coarse_view)
+    level: coarse z0 = fine z0 / 2, its ghost plane -1 read), else whole (a replicated coarse level).
+    LINEAR and NEWTON (newtonV offset with the range like f)."""
+    rng = np.random.default_rng(sum(shape) * 7 + coarse_view + 100 * mode)
     nx, ny, nz = shape
     cd = [x // 2 for x in shape]
     h = 1.0 / (ny + 1)
@@ -276,8 +276,9 @@ def test_prolong_fused_pair_plane_ranges(shape, ranges, coarse_view):
     L = DevField(nx, ny, nz).level(h)
     v, f, c, out_ref = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
                         DevField(*cd).from_xyz(c0), DevField(nx, ny, nz))
+    w = DevField(nx, ny, nz).from_xyz(rand_full(rng, *shape, 0.5)) if mode == 2 else None
     Lc = c.level(2 * h)
-    ok(prolong_ws(stencil(), L, 0, v.ptr, c.ptr, None, Lc, out_ref.ptr, f.ptr, None, 0, 0))
+    ok(prolong_ws(stencil(), L, mode, v.ptr, c.ptr, None, Lc, out_ref.ptr, f.ptr, w.ptr if w else None, 0, 0))
     out = DevField(nx, ny, nz)
     for z1, z2 in ranges:
         off = 8 * (z1 - 1) * L.ldz
@@ -287,8 +288,8 @@ def test_prolong_fused_pair_plane_ranges(shape, ranges, coarse_view):
             z0c = (z1 - 1) // 2
             cptr = c.ptr + 8 * z0c * Lc.ldz
             cl = gsv._abi.gs_level(Lc.nx, Lc.ny, min((z2 - z1 + 2) // 2, cd[2] - z0c), Lc.ldy, Lc.ldz, z0c, 2 * h)
-        rc = prolong_ws(stencil(), sub, 0, v.ptr + off, cptr, None, cl, out.ptr + off, f.ptr + off, None,
-                        int(z1 > 1), int(z2 < nz))
+        rc = prolong_ws(stencil(), sub, mode, v.ptr + off, cptr, None, cl, out.ptr + off, f.ptr + off,
+                        w.ptr + off if w else None, int(z1 > 1), int(z2 < nz))
         if z1 % 2 == 0:
             assert rc == gsv._abi.GS_EINVAL  # plane parities must be the global ones
         else:
@@ -307,15 +308,18 @@ def test_prolong_fused_pair_rejects():
     L2 = DevField(600, 4, 4).level(0.2)
     assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 0) == 1  # rows > 512: LINEAR
     assert k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(stencil()), C.byref(L2), 0) == 1 * (4 + 4) * 4 * (4 + 2)
-    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 2) == 0  # NEWTON: k_tb2 rows
+    assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 2) == 1  # NEWTON: column blocks
+    assert k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(stencil()), C.byref(L2), 2) == 1 * (4 + 4) * 4 * (4 + 2)
+    assert b"XH" not in k().gs_jacobi_sweep2_kernel(C.byref(stencil()), C.byref(L2), 2)  # the plain pair: k_tb2
     L3 = DevField(512, 4, 4).level(0.2)
     assert k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(stencil()), C.byref(L3), 0) == 0
 
 
-def test_prolong_fused_pair_full_1024_plane_set():
+@pytest.mark.parametrize("mode", [0, 2])
+def test_prolong_fused_pair_full_1024_plane_set(mode):
     """Config #5's row length on a full 1024 x 1024 plane set (8 planes): the column-block prolongation pair
-    against gs_prolong_add + the plain pair, bit for bit."""
-    rng = np.random.default_rng(10241)
+    against gs_prolong_add + the plain pair, bit for bit (LINEAR; NEWTON with a newtonV field)."""
+    rng = np.random.default_rng(10241 + mode)
     shape = (1024, 1024, 8)
     nx, ny, nz = shape
     cd = [x // 2 for x in shape]
@@ -324,11 +328,13 @@ def test_prolong_fused_pair_full_1024_plane_set():
     L = DevField(*shape).level(h)
     v, f, c, out_ref = (DevField(*shape).from_xyz(v0), DevField(*shape).from_xyz(f0), DevField(*cd).from_xyz(c0),
                         DevField(*shape))
+    w = DevField(*shape).from_xyz(rand_full(rng, *shape, 0.5)) if mode == 2 else None
+    wp = w.ptr if w else None
     Lc = c.level(2 * h)
     ok(k().gs_prolong_add(c.ptr, None, C.byref(Lc), v.ptr, C.byref(L), st()))
-    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, out_ref.ptr, f.ptr, None, 0, 0, st()))
+    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), mode, 0.8, 1.0, v.ptr, out_ref.ptr, f.ptr, wp, 0, 0, st()))
     v2, out = DevField(*shape).from_xyz(v0), DevField(*shape)
-    ok(prolong_ws(stencil(), L, 0, v2.ptr, c.ptr, None, Lc, out.ptr, f.ptr, None, 0, 0))
+    ok(prolong_ws(stencil(), L, mode, v2.ptr, c.ptr, None, Lc, out.ptr, f.ptr, wp, 0, 0))
     np.testing.assert_array_equal(out.to_xyz(), out_ref.to_xyz())
 
 

@@ -8,7 +8,7 @@ Inputs: smooth fields (v = 0.25 sin, f = 1, newtonV = 0.1 sin, coarse v = 0.05),
 arithmetic of a sane iterate. Prints one JSON line: ms per launch (min over rounds) and GB/s algorithmic.
 GS_KPROBE_LIB=<path to an alternative libgpusolve_hip.so> loads that build instead (A/B of kernel
 variants: the same script against two builds). GS_KPROBE_EFIELD=1 (with a -DGS_EXP_EFIELD build) gives
-the pairs a second field E = exp(newtonV) of newtonV's shape and passes its distance as GS_EXP_EFOFF."""
+the pairs a second field E = exp(newtonV) of newtonV's shape and passes its distance (gs_exp_set_efoff)."""
 import ctypes as C
 import json
 import os
@@ -47,7 +47,9 @@ def main():
         e = DevField(*dims)
         e.zyx_ext.copy_(torch.exp(w.zyx_ext))
         assert (e.ptr - w.ptr) % 8 == 0
-        os.environ["GS_EXP_EFOFF"] = str((e.ptr - w.ptr) // 8)
+        fn = getattr(kl, "gs_exp_set_efoff")  # only a -DGS_EXP_EFIELD build exports it
+        fn.argtypes, fn.restype = [C.c_int64], None
+        fn((e.ptr - w.ptr) // 8)
     f = DevField(*dims, fill=1.0)
     out = DevField(*dims)
     cv = DevField(*cd, fill=0.05)
