@@ -119,8 +119,9 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_XH_SWIZZLE=0|1    column-block pairs: the mirrored row's x-waves rotated by two (1, default) or not (0)
 //   GS_MID_ZC=n          z-chunk of pair launches over whole levels of < 2^26 points (A/B)
 //   GS_RR_ZC=n           z-chunk (coarse planes) of k_rr2 launches from fine levels of < 2^26 points (A/B)
+//   GS_NEWTON_XH=1       NEWTON plain pairs on rows of 513-1024 points as column blocks instead of k_tb2 (A/B)
 struct Knobs {
-    bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ;
+    bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh;
     int xhSwizzle, midZc, rrZc;
     int slabZc, pairZc, rrNr, rrNtu, rrReverse;
     int64_t pairMinBlocks;
@@ -134,6 +135,7 @@ struct Knobs {
           pairXh(num("GS_PAIR_XH", 1) != 0), fitRounds(num("GS_FIT_ROUNDS", 1) != 0),
           bigChunks(num("GS_PAIR_BIG_CHUNKS", 1) != 0), oneRound(num("GS_PAIR_ONE_ROUND", 1) != 0),
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
+          newtonXh(num("GS_NEWTON_XH", 0) != 0),
           xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
           rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 1)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
@@ -2648,7 +2650,7 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
     // column-block pair carries the edge column's newtonV too and spills (~45 VGPRs), k_tb2 does not.
     // NEWTON prolongation pairs (pro) have no k_tb2 form: column blocks from 513 points
     const bool colb = !two && xh_enabled() && L->nx <= (int64_t)1 << 20 &&
-                      (mode != GS_NEWTON || pro || L->nx > 2 * WAVE * TB_WX_B);
+                      (mode != GS_NEWTON || pro || kKnobs.newtonXh || L->nx > 2 * WAVE * TB_WX_B);
     if (!two && !colb && L->nx > 2 * WAVE * TB_WX_B) return 0;
     const int64_t nh = colb ? (L->nx + 2 * WAVE * TBY_WX - 1) / (2 * WAVE * TBY_WX) : 1;
     const int rows = (two || colb) ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block
