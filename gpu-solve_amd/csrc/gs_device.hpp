@@ -2121,7 +2121,9 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 #endif
     // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes A from the
     // newtonV rows at z-1 and reads E = exp(w) from LDS (same expressions, same values)
-    constexpr bool RECOMP = MODE == GS_NEWTON && PRO != 0;
+    // NEWTON column blocks (XH) likewise: their edge-column state leaves no room for Aprev / Eprev / Fprev
+    constexpr bool RECOMP = MODE == GS_NEWTON && (PRO != 0 || XH);
+    constexpr bool WLDS = RECOMP && PRO != 0; // the coarse X-pass rows in LDS (prolongation pairs)
     // (Wprev, Fprev: sweep 2's newtonV / f rows at z-1, in LDS like the coarse rows below)
     __shared__ double2 wprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
     __shared__ double2 fprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
@@ -2184,17 +2186,17 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // (0.5 * fine(y-1) + 0.5 * fine(y+1) with fine(y+-1) an X-pass value; 0.5 * fine(z) + 0.5 * fine(z+2)
     // with fine(z), fine(z+2) X-pass values on even rows): formed once per coarse row instead of at every
     // fine point that reads it — the same products, so the same bits
-    constexpr bool HALF = !RECOMP;
+    constexpr bool HALF = !WLDS;
     double2 H0[HALF ? NCR : 1], H1[HALF ? NCR : 1], Hm[HALF ? NCR : 1];
     // NEWTON (RECOMP): the X-pass rows of planes K, K+1 live in LDS, slot wsl / wsl^1 — each lane
     // reads back only what it wrote, so no barrier; this keeps the variant inside 256 VGPRs
-    __shared__ double2 wlds[RECOMP ? 2 : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? NCR : 1][RECOMP ? WAVE : 1];
+    __shared__ double2 wlds[WLDS ? 2 : 1][WLDS ? 2 * WXMAX : 1][WLDS ? NCR : 1][WLDS ? WAVE : 1];
     int wsl = 0;
-    const int wid_l = RECOMP ? wx + WX * wy : 0;
+    const int wid_l = WLDS ? wx + WX * wy : 0;
     // coarse X-pass row r of plane slot s (0: K, 1: K+1, 2: K-1 on the first step)
     auto wget = [&](int s, int r) -> double2 {
         if (s == 2) return Wm[r];
-        if constexpr (RECOMP) return wlds[s ^ wsl][wid_l][r][lane];
+        if constexpr (WLDS) return wlds[s ^ wsl][wid_l][r][lane];
         else return s == 0 ? W0[r] : W1[r];
     };
     auto hget = [&](int s, int r) -> double2 { return s == 2 ? Hm[HALF ? r : 0] : (s == 0 ? H0[HALF ? r : 0] : H1[HALF ? r : 0]); };
@@ -2225,7 +2227,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                 else H1[r] = Hh;
             }
             if (s == 2) Wm[r] = X;
-            else if constexpr (RECOMP) wlds[s ^ wsl][wid_l][r][lane] = X;
+            else if constexpr (WLDS) wlds[s ^ wsl][wid_l][r][lane] = X;
             else if (s == 0) W0[r] = X;
             else W1[r] = X;
         }
@@ -2506,7 +2508,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                 ES1c = ES1n;
             }
             if (PRO && ph == 1) { // next step: coarse planes K+1, K+2
-                if constexpr (RECOMP) {
+                if constexpr (WLDS) {
                     wsl ^= 1;
                 } else {
 #pragma unroll

@@ -116,7 +116,7 @@ int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L, in
  * gs_jacobi_sweep2, with the corrected iterate never stored. Replaces CpuSolver.cpp:127-135
  * (interpolate, v += e, jacobi(post)) for the first two post-smoothing sweeps. Supported
  * (gs_jacobi_sweep2_prolong_supported != 0) for LINEAR and NEWTON levels of rows <= 512 points, and
- * LINEAR levels of longer rows (with a workspace, gs_jacobi_sweep2_prolong_ws), whose z0 is even (a level, a Z-slab of one, or a plane range of either); coarse_sub must then be NULL. Fine local
+ * LINEAR and NEWTON levels of longer rows (with a workspace, gs_jacobi_sweep2_prolong_ws), whose z0 is even (a level, a Z-slab of one, or a plane range of either); coarse_sub must then be NULL. Fine local
  * plane z interpolates from coarse planes (z + z0) / 2 - coarse->z0 (+1); zlo / zhi as for
  * gs_jacobi_sweep2 — the ghost planes of an internal side are corrected too, from the coarse field's
  * planes under them (coarse ghost planes -1 / nz+1 must then be current). w: the level's newtonV

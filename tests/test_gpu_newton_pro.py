@@ -54,10 +54,10 @@ def test_newton_fused_prolong_bit_identical(dims, pre, post):
         np.testing.assert_array_equal(f_got[key], a, err_msg=str(key))
 
 
-def test_newton_fused_prolong_slabs():
+@pytest.mark.parametrize("dims", [(64, 128, 128), (1030, 18, 16)])  # (1030: column-block prolongation pairs)
+def test_newton_fused_prolong_slabs(dims):
     """Z-slab loopback (2 ranks) with the fused NEWTON pair on every slab level == without it."""
     d = gsv.driver()
-    dims = (64, 128, 128)
     p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=gsv.GS_NEWTON).to_abi()
     out = []
     for thr in (1 << 62, 0):
@@ -69,5 +69,6 @@ def test_newton_fused_prolong_slabs():
                                          v.ctypes.data_as(gsv._abi.dptr))
         assert rc == 0, d.gs_last_error().decode()
         out.append((list(hist[: cnt.value]), v))
+    assert np.all(np.isfinite(out[0][0])), out[0][0]
     assert out[0][0] == out[1][0]
     np.testing.assert_array_equal(out[0][1], out[1][1])

@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
 step pytest-switch
-timeout -k 10 600 python -u -m pytest tests/test_gpu_switches.py -m gpu -x -q -k "newton_rows700 or list_matches" \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_switches.py tests/test_gpu_newton_pro.py -m gpu -x -q -k "newton_rows700 or list_matches or newton_fused_prolong" \
   --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 for v in 0 1; do
