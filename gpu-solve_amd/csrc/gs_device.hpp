@@ -2136,8 +2136,26 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     for (int j = 0; j < RY; j++) V1p[j] = make_double2(0.0, 0.0);
     // XH edge column: v at plane z+1 (EA), its x-neighbours (EXm, EXp) and f at plane z, per slot;
     // EP / EC: v at planes z-1 / z; ES1c: sweep 1 at plane z-1
-    double EA[XH ? NS : 1], EXm[XH ? NS : 1], EXp[XH ? NS : 1], EF[XH ? NS : 1], EP = 0.0, EC = 0.0, ES1c = 0.0;
-    double EW[(XH && MODE == GS_NEWTON) ? NS : 1]; // NEWTON: newtonV at the edge column, plane z
+    // NEWTON (ELATE): no slots for them — a step loads its own edge values at its top, before the publish
+    // and the barrier (the strip / edge column is L2-resident), so they are not live across a whole step of
+    // the NEWTON arithmetic: 30 fewer live VGPRs, where the slots made the NEWTON column-block pairs spill
+    constexpr bool ELATE = XH && MODE == GS_NEWTON;
+    constexpr int NES = (XH && !ELATE) ? NS : 1;
+    double EA[NES], EXm[NES], EXp[NES], EF[NES], EP = 0.0, EC = 0.0, ES1c = 0.0;
+    double EW[1]; // NEWTON: newtonV at the edge column, plane z (ELATE: loaded per step)
+    auto load_edge = [&](const int s, const int z, const int zv) {
+        if constexpr (PRO != 0) {
+            EA[s] = *sat(0, zv);
+            EXm[s] = *sat(-1, z);
+            EXp[s] = *sat(1, z);
+        } else {
+            EA[s] = ldv1<ZV>(eat(v, 0, zv));
+            EXm[s] = ldv1<ZV>(eat(v, -1, z));
+            EXp[s] = ldv1<ZV>(eat(v, 1, z));
+        }
+        EF[s] = *eat(f, 0, z);
+        if constexpr (MODE == GS_NEWTON) EW[0] = *eat(w, 0, z);
+    };
     auto load_slot = [&](const int s, const int z, const int zv) {
 #pragma unroll
         for (int j = 0; j < NV; j++) {
@@ -2149,20 +2167,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 #endif
         }
         HL[s] = ldv2<ZV>(at(v, -1, z));
-        if constexpr (XH) {
-            if (edg) {
-                if constexpr (PRO != 0) {
-                    EA[s] = *sat(0, zv);
-                    EXm[s] = *sat(-1, z);
-                    EXp[s] = *sat(1, z);
-                } else {
-                    EA[s] = ldv1<ZV>(eat(v, 0, zv));
-                    EXm[s] = ldv1<ZV>(eat(v, -1, z));
-                    EXp[s] = ldv1<ZV>(eat(v, 1, z));
-                }
-                EF[s] = *eat(f, 0, z);
-                if constexpr (MODE == GS_NEWTON) EW[s] = *eat(w, 0, z);
-            }
+        if constexpr (XH && !ELATE) {
+            if (edg) load_edge(s, z, zv);
         }
     };
 #pragma unroll
@@ -2306,6 +2312,10 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             if (PFD == 1) load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
             else load_slot((ph4 + 2) & 3, min(z + 2, nz + 1), min(z + 3, nz + 2));
             if (PRO && ph == 0) craw((z >> 1) + 2); // consumed at the end of the next step
+            if constexpr (ELATE) {
+                if (edg) load_edge(0, min(z, nz + 1), min(z + 1, nz + 2)); // this step's edge values
+            }
+            const int ce = ELATE ? 0 : cs; // slot of this step's edge values
             // ---- publish: x-edge columns (v(z) rows 0..RY, sweep-1(z-1) rows 1..RY) and the y-edge row
             if (lane == 0) {
 #pragma unroll
@@ -2364,15 +2374,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         double nv;
                         // (zero iterate: q = +0 exactly, Coef::zq)
                         auto qe = [&] {
-                            return (ZV && k.zq) ? 0.0 : div_hh(k, stencil_sum<UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP));
+                            return (ZV && k.zq) ? 0.0 : div_hh(k, stencil_sum<UN>(k, c, EXp[ce], EXm[ce], yp, ym, EA[ce], EP));
                         };
                         if constexpr (MODE == GS_NEWTON) { // the interior rows' NEWTON expressions, exp once
-                            const double we = EW[cs], A = k.gamma * (1 + we), E = exp(we);
+                            const double we = EW[0], A = k.gamma * (1 + we), E = exp(we);
                             const double a = newton_op(qe(), c, A, E);
-                            nv = newton_update(k, c, EF[cs] - a, A, E);
+                            nv = newton_update(k, c, EF[ce] - a, A, E);
                         } else {
                             const double a = op_finish<MODE>(k, qe(), c, 0.0);
-                            nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
+                            nv = jacobi_update<MODE>(k, c, EF[ce] - a, 0.0);
                         }
                         ES1n = (!pz || !erowc) ? c : nv;
                     }
@@ -2504,7 +2514,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             }
             if constexpr (XH) {
                 EP = EC;
-                EC = EA[cs];
+                EC = EA[ce];
                 ES1c = ES1n;
             }
             if (PRO && ph == 1) { // next step: coarse planes K+1, K+2
