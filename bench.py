@@ -404,6 +404,12 @@ def main():
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # RCCL's p2p channels per peer fill the halo communicator's CTA budget (GS_RCCL_CTAS, default 64: four
+        # send/recv per rank, so budget / 4 per peer; gs_comm.cpp). RCCL reads it once per process: before torch's
+        # communicator. An explicit value in the environment wins.
+        ctas = int(os.environ.get("GS_RCCL_CTAS") or 64)
+        if ctas > 0:
+            os.environ.setdefault("NCCL_NCHANNELS_PER_PEER", str(max(1, ctas // 4)))
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local % max(1, torch.cuda.device_count())))
 
     def barrier():
@@ -497,7 +503,8 @@ def main():
                  "exchange_ms_per_pair_max": fin(max(gaps)) if gaps else None,
                  "rank_halo_host_us_per_call": [fin(r[3]) for r in rows],
                  "rank_halo_host_us_max": [fin(r[4]) for r in rows],
-                 "rccl_ctas": int(os.environ.get("GS_RCCL_CTAS", "0") or 0) or "default (gs_comm.cpp)",
+                 "rccl_ctas": int(os.environ.get("GS_RCCL_CTAS", "0") or 0) or "default (gs_comm.cpp: 64)",
+                 "rccl_channels_per_peer": os.environ.get("NCCL_NCHANNELS_PER_PEER"),
                  "note": "rank_pair_ms: the overlapped pair (boundary planes, RCCL ghost exchange, interior) "
                          "per launch on each rank's compute stream; _no_exchange: the same pair on the same "
                          "slab run locally, no exchange; rank_halo_host_us_per_call / _max: host wall time of "

@@ -56,6 +56,12 @@ public:
         if (const int ctas = rcclCtas(); ctas > 0) {
             cfg.minCTAs = ctas;
             cfg.maxCTAs = ctas;
+            // the CTA budget caps RCCL's send/recv grid, the p2p channels per peer fill it: a rank's grouped
+            // exchange is four send/recv operations, so ctas / 4 channels per peer give it the whole budget
+            // (the 8-rank rehearsal's bulk launches: 4 workgroups by default, 16 at 16 channels per peer,
+            // profiles/r04/r04i_rccl_grid_cpp16.txt). A value in the environment wins; RCCL reads it once
+            // per process, so bench.py sets it before torch's own communicator exists
+            setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(std::max(1, ctas / 4)).c_str(), 0);
         }
         const ncclResult_t e = ncclCommInitRankConfig(&c_, nranks, id, rank, &cfg);
         if (e != ncclSuccess && e != ncclInProgress) {

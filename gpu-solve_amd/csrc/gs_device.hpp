@@ -119,7 +119,7 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_XH_SWIZZLE=0|1    column-block pairs: the mirrored row's x-waves rotated by two (1, default) or not (0)
 //   GS_MID_ZC=n          z-chunk of pair launches over whole levels of < 2^26 points (A/B)
 //   GS_RR_ZC=n           z-chunk (coarse planes) of k_rr2 launches from fine levels of < 2^26 points (A/B)
-//   GS_NEWTON_XH=1       NEWTON plain pairs on rows of 513-1024 points as column blocks instead of k_tb2 (A/B)
+//   GS_NEWTON_XH=0       NEWTON plain pairs on rows of 513-1024 points through k_tb2 instead of column blocks (A/B)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh;
     int xhSwizzle, midZc, rrZc;
@@ -135,7 +135,7 @@ struct Knobs {
           pairXh(num("GS_PAIR_XH", 1) != 0), fitRounds(num("GS_FIT_ROUNDS", 1) != 0),
           bigChunks(num("GS_PAIR_BIG_CHUNKS", 1) != 0), oneRound(num("GS_PAIR_ONE_ROUND", 1) != 0),
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
-          newtonXh(num("GS_NEWTON_XH", 0) != 0),
+          newtonXh(num("GS_NEWTON_XH", 1) != 0),
           xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
           rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 1)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
@@ -2658,9 +2658,10 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
 {
     if (!S || !L || !canonical_order(S) || L->nx < 1 || L->ny < 1 || L->nz < 1) return 0;
     const bool two = L->nx <= 2 * WAVE * TBY_WX;
-    // NEWTON plain pairs: column blocks only where k_tb2 has no shape (rows > 1024 points): the NEWTON
-    // column-block pair carries the edge column's newtonV too and spills (~45 VGPRs), k_tb2 does not.
-    // NEWTON prolongation pairs (pro) have no k_tb2 form: column blocks from 513 points
+    // NEWTON: column blocks from 513 points too since r04 (sweep 2's rows in LDS, edge values loaded per
+    // step: 255 VGPRs, no spill): 1023^3 pair 8.83 vs 29.9 ms for k_tb2, Newton iteration 109-110 vs
+    // 166-167 ms (profiles/r04/r04i_newton_1023.txt); GS_NEWTON_XH=0 keeps k_tb2 for the plain pairs (A/B).
+    // NEWTON prolongation pairs (pro) have no k_tb2 form
     const bool colb = !two && xh_enabled() && L->nx <= (int64_t)1 << 20 &&
                       (mode != GS_NEWTON || pro || kKnobs.newtonXh || L->nx > 2 * WAVE * TB_WX_B);
     if (!two && !colb && L->nx > 2 * WAVE * TB_WX_B) return 0;

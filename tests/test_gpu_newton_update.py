@@ -178,7 +178,7 @@ def test_copy(n, doff, soff):
 
 @pytest.mark.parametrize("dims", [(1100, 20, 18), (700, 12, 10)])
 def test_newton_long_rows_vs_oracle(dims):
-    """NEWTON on rows of more than 512 points: k_tb2 up to 1024, column-block pairs beyond (r03), against the
+    """NEWTON on rows of more than 512 points: column-block pairs (k_tb2 up to 1024 points before r04), against the
     CPU oracle (pinned to src/cpu); 1e-10 on newtonV (ocml vs glibc exp), 1e-9 on the history."""
     import oracle as O
     from conftest import rel

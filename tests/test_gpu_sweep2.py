@@ -56,8 +56,8 @@ def two_sweeps(v0, f0, w0, mode, h):
 
 SHAPES = [(1, 1, 1), (2, 5, 3), (5, 4, 33), (127, 9, 17), (128, 8, 8), (129, 13, 40), (257, 6, 10), (500, 7, 9),
           (512, 4, 5), (513, 5, 6), (1024, 3, 4), (64, 64, 64), (200, 33, 70),
-          # rows > 512 points: column blocks (k_tb2y XH) in LINEAR / NONLINEAR mode, k_tb2 in NEWTON mode up to
-          # 1024 points and NEWTON column blocks beyond (r03)
+          # rows > 512 points: column blocks (k_tb2y XH) in every mode (NEWTON rows of 513-1024 points since r04;
+          # GS_NEWTON_XH=0 keeps k_tb2 for them, tests/test_gpu_switches.py)
           (700, 9, 11), (1024, 16, 12), (1025, 7, 9), (1536, 5, 6), (2000, 3, 5)]
 
 
@@ -225,7 +225,7 @@ def test_prolong_fused_pair_bit_identical(shape, mode):
     L = DevField(nx, ny, nz).level(h)
     supported = k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L), mode)
     # the fused prolongation pair exists for every LINEAR and NEWTON shape (NEWTON rows > 512 points: column
-    # blocks since r04, against k_tb2's plain pair as the reference here)
+    # blocks since r04)
     assert supported == 1, (shape, mode, supported)
     # reference: prolongation + correction stored, then the plain fused pair
     v, f, c, out_ref = (DevField(nx, ny, nz).from_xyz(v0), DevField(nx, ny, nz).from_xyz(f0),
@@ -310,7 +310,7 @@ def test_prolong_fused_pair_rejects():
     assert k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(stencil()), C.byref(L2), 0) == 1 * (4 + 4) * 4 * (4 + 2)
     assert k().gs_jacobi_sweep2_prolong_supported(C.byref(stencil()), C.byref(L2), 2) == 1  # NEWTON: column blocks
     assert k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(stencil()), C.byref(L2), 2) == 1 * (4 + 4) * 4 * (4 + 2)
-    assert b"XH" not in k().gs_jacobi_sweep2_kernel(C.byref(stencil()), C.byref(L2), 2)  # the plain pair: k_tb2
+    assert b"XH" in k().gs_jacobi_sweep2_kernel(C.byref(stencil()), C.byref(L2), 2)  # the plain pair too (r04)
     L3 = DevField(512, 4, 4).level(0.2)
     assert k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(stencil()), C.byref(L3), 0) == 0
 

@@ -38,7 +38,7 @@ CASES = {
     "newton127": ((2, 127, 127, 127, 2), [("GS_NEWTON_PRO_POINTS", "0"), ("GS_NO_FUSED_PROLONG", "1"),
                                           ("GS_NO_PIPELINE", "1"), ("GS_NO_NEWTON_FUSED_UPDATE", "1"),
                                           ("GS_RR_REVERSE", "0"), ("GS_NO_ZERO_Q", "1")]),
-    "newton_rows700": ((2, 700, 12, 10, 2), [("GS_NEWTON_XH", "1")]),
+    "newton_rows700": ((2, 700, 12, 10, 2), [("GS_NEWTON_XH", "0")]),
 }
 PARAMS = [(case, sw, val) for case, (_, sws) in CASES.items() for sw, val in sws]
 _default = {}
