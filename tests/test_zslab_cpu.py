@@ -296,7 +296,8 @@ def test_gloo_replay_newton_schedule(fused):
     never stop a loop — runs the ten inner V-cycles the oracle runs."""
     dims, world = (256, 512, 64), 2
     params = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=2)
-    env = {} if fused else {"GS_NO_NEWTON_FUSED_UPDATE": "1"}
+    # (the fused run also takes the NEWTON prolongation pair on every slab level: GS_NEWTON_PRO_POINTS=0)
+    env = {"GS_NEWTON_PRO_POINTS": "0"} if fused else {"GS_NO_NEWTON_FUSED_UPDATE": "1"}
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -313,6 +314,7 @@ def test_gloo_replay_newton_schedule(fused):
     ref_v, ref_w = og.field(0, "v").copy(), og.field(0, "newtonV").copy()
     for rank, lo, hi, v, w, hist, ops in res:
         assert ("newtonFupdate" in ops and "ghostsum" in ops) == fused and ("axpy" in ops) != fused, ops
+        assert ("pro" in ops) == fused, ops
         assert len(hist) == len(ref_hist)
         for a, b in zip(hist, ref_hist):
             assert abs(a - b) <= 1e-10 * abs(b), (a, b)
