@@ -2055,7 +2055,10 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     const int WX = blockDim.y;
     // XH (Coef::swz): the mirrored y-wave row runs its x-waves rotated by two, so that the two waves a SIMD
     // hosts (hardware wave i -> SIMD i mod 4) are never both edge waves (the edge column's extra work)
-    const int wx = __builtin_amdgcn_readfirstlane(XH && k.swz && wy && WX == 4 ? (threadIdx.y + 2) & 3 : threadIdx.y);
+    // (not in the prolongation pairs: there the rotation costs the LINEAR column-block form 3 VGPRs, 8-12 B
+    // spilled per lane, where it fits 253 without)
+    const int wx = __builtin_amdgcn_readfirstlane(XH && PRO == 0 && k.swz && wy && WX == 4 ? (threadIdx.y + 2) & 3
+                                                                                            : threadIdx.y);
     const int tid = threadIdx.x + WAVE * (threadIdx.y + WX * threadIdx.z);
     for (int i = tid; i < 2 * 2 * (WXMAX + 2) * 2 * NE; i += WAVE * WX * 2) (&edge[0][0][0][0][0])[i] = 0.0;
     __syncthreads();
