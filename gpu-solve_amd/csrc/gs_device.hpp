@@ -2139,13 +2139,14 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     for (int j = 0; j < RY; j++) V1p[j] = make_double2(0.0, 0.0);
     // XH edge column: v at plane z+1 (EA), its x-neighbours (EXm, EXp) and f at plane z, per slot;
     // EP / EC: v at planes z-1 / z; ES1c: sweep 1 at plane z-1
-    // NEWTON (ELATE): no slots for them — a step loads its own edge values at its top, before the publish
-    // and the barrier (the strip / edge column is L2-resident), so they are not live across a whole step of
-    // the NEWTON arithmetic: 30 fewer live VGPRs, where the slots made the NEWTON column-block pairs spill
-    constexpr bool ELATE = XH && MODE == GS_NEWTON;
-    constexpr int NES = (XH && !ELATE) ? NS : 1;
+    // NEWTON (EPK): the five edge values of a step share ONE register per slot: lane 8 f + r holds field f
+    // (0 v or the corrected v at plane z+1, 1 / 2 its x-neighbours at plane z, 3 f, 4 newtonV) of local row r,
+    // and the edge computation takes them with lane permutes. The prefetch distance stays one step, at 2
+    // VGPRs per slot instead of 10 (the NEWTON column-block pairs spilled with five slot arrays)
+    constexpr bool EPK = XH && MODE == GS_NEWTON;
+    constexpr int NES = (XH && !EPK) ? NS : 1;
     double EA[NES], EXm[NES], EXp[NES], EF[NES], EP = 0.0, EC = 0.0, ES1c = 0.0;
-    double EW[1]; // NEWTON: newtonV at the edge column, plane z (ELATE: loaded per step)
+    double EPS[EPK ? NS : 1]; // EPK: the packed slots
     auto load_edge = [&](const int s, const int z, const int zv) {
         if constexpr (PRO != 0) {
             EA[s] = *sat(0, zv);
@@ -2157,8 +2158,33 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             EXp[s] = ldv1<ZV>(eat(v, 1, z));
         }
         EF[s] = *eat(f, 0, z);
-        if constexpr (MODE == GS_NEWTON) EW[0] = *eat(w, 0, z);
     };
+    // EPK: lane 8 f + r's row offset (row r = 0..7 clamped to the edge rows 0..RY+1) and field f
+    const int pfld = EPK ? lane >> 3 : 0;
+    int64_t proff = 0;
+    const double* psr = es;
+    if constexpr (EPK) {
+        const int y = yof(min(lane & 7, RY + 1));
+        proff = (int64_t)min(max(y, 0), ny + 1) * ldy;
+        if (PRO != 0 && edg) {
+            const int hb = eL ? hx - 1 : hx;
+            psr = es + (int64_t)hb * (nz + 4) * 4 * (ny + 2) + (eL ? 1 : 2) * (ny + 2) + min(max(y, 0), ny + 1);
+        }
+    }
+    auto load_packed = [&](const int s, const int z, const int zv) {
+        const int dx = pfld == 1 ? -1 : (pfld == 2 ? 1 : 0);
+        const int zz = pfld == 0 ? zv : z;
+        double val = 0.0;
+        if (pfld <= 2) {
+            if constexpr (PRO != 0) val = psr[((int64_t)(zz + 1) * 4 + dx) * (ny + 2)];
+            else if constexpr (!ZV) val = v[(xe + dx) + proff + (int64_t)zz * ldz];
+        } else if (pfld <= 4) {
+            val = (pfld == 3 ? f : w)[xe + proff + (int64_t)z * ldz];
+        }
+        EPS[s] = val;
+    };
+    // field fl of this lane's edge row from packed slot s (a lane permute; every lane of the wave active)
+    auto efld = [&](const int s, const int fl) { return __shfl(EPS[s], fl * 8 + (lane & 7), WAVE); };
     auto load_slot = [&](const int s, const int z, const int zv) {
 #pragma unroll
         for (int j = 0; j < NV; j++) {
@@ -2170,8 +2196,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 #endif
         }
         HL[s] = ldv2<ZV>(at(v, -1, z));
-        if constexpr (XH && !ELATE) {
+        if constexpr (XH && !EPK) {
             if (edg) load_edge(s, z, zv);
+        }
+        if constexpr (EPK) {
+            if (edg) load_packed(s, z, zv);
         }
     };
 #pragma unroll
@@ -2315,10 +2344,6 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             if (PFD == 1) load_slot(ph, min(z + 1, nz + 1), min(z + 2, nz + 2));
             else load_slot((ph4 + 2) & 3, min(z + 2, nz + 1), min(z + 3, nz + 2));
             if (PRO && ph == 0) craw((z >> 1) + 2); // consumed at the end of the next step
-            if constexpr (ELATE) {
-                if (edg) load_edge(0, min(z, nz + 1), min(z + 1, nz + 2)); // this step's edge values
-            }
-            const int ce = ELATE ? 0 : cs; // slot of this step's edge values
             // ---- publish: x-edge columns (v(z) rows 0..RY, sweep-1(z-1) rows 1..RY) and the y-edge row
             if (lane == 0) {
 #pragma unroll
@@ -2377,15 +2402,20 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         double nv;
                         // (zero iterate: q = +0 exactly, Coef::zq)
                         auto qe = [&] {
-                            return (ZV && k.zq) ? 0.0 : div_hh(k, stencil_sum<UN>(k, c, EXp[ce], EXm[ce], yp, ym, EA[ce], EP));
+                            if constexpr (EPK) {
+                                const double exm = efld(cs, 1), exq = efld(cs, 2), ea = efld(cs, 0);
+                                return (ZV && k.zq) ? 0.0 : div_hh(k, stencil_sum<UN>(k, c, exq, exm, yp, ym, ea, EP));
+                            } else {
+                                return (ZV && k.zq) ? 0.0 : div_hh(k, stencil_sum<UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP));
+                            }
                         };
                         if constexpr (MODE == GS_NEWTON) { // the interior rows' NEWTON expressions, exp once
-                            const double we = EW[0], A = k.gamma * (1 + we), E = exp(we);
+                            const double we = efld(cs, 4), A = k.gamma * (1 + we), E = exp(we);
                             const double a = newton_op(qe(), c, A, E);
-                            nv = newton_update(k, c, EF[ce] - a, A, E);
+                            nv = newton_update(k, c, efld(cs, 3) - a, A, E);
                         } else {
                             const double a = op_finish<MODE>(k, qe(), c, 0.0);
-                            nv = jacobi_update<MODE>(k, c, EF[ce] - a, 0.0);
+                            nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
                         }
                         ES1n = (!pz || !erowc) ? c : nv;
                     }
@@ -2517,7 +2547,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
             }
             if constexpr (XH) {
                 EP = EC;
-                EC = EA[ce];
+                if constexpr (EPK) {
+                    if (edg) EC = efld(cs, 0);
+                } else {
+                    EC = EA[cs];
+                }
                 ES1c = ES1n;
             }
             if (PRO && ph == 1) { // next step: coarse planes K+1, K+2
