@@ -109,9 +109,13 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     // 71 us; the same rule measured no better for the other pairs, worse for k_rr2 and for NEWTON's
     // zero-iterate pair at two blocks per CU: 133 vs 120 us, r02 tools/fit_session.sh)
     const bool refit = !v_in && !partials && (int64_t)L->nx * L->ny * L->nz < ((int64_t)1 << 26);
+    // GS_SPEC_CACHED=1: pairs with norm partials (the V-cycle's speculative pre-smoothing pair, which k_rr2 reads
+    // next, last planes first) store through the caches instead of non-temporally (A/B)
+    const bool cached = partials && kKnobs.specCached;
 #define GS_TBY2(M, Z, U, P) do { \
         if (refit && M == GS_LINEAR) refit_chunks(&k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, P, false, U>, (int)(b.x * b.y * b.z), nz, 4, 64, true, 2.0, &zc, &g); \
-        hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, P, false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr); } while (0)
+        if (cached) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, false, false, Z, true, 0, P, false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr); \
+        else hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, P, false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr); } while (0)
 #define GS_TBY1(M, Z, U) GS_TBY2(M, Z, U, tby_pfd(M))
 #define GS_TBY(M, Z) do { if (k.unit) GS_TBY1(M, Z, true); else GS_TBY1(M, Z, false); } while (0)
 #define GS_TBX1(M, Z, P, U) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr)
