@@ -2215,7 +2215,12 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     }
     // ---- fused prolongation (PRO): coarse rows cyb .. cyb+NCR-1 lie under the wave's fine rows ----
     constexpr int NCR = RY / 2 + 2;
-    const int cxl = min(x >> 1, max(cnx, 0)); // the lane's coarse column (fine pair x odd, x+1 even)
+    // RBDPP (NEWTON column blocks, where every VGPR counts): b = c(cx+1) is the next lane's a (one DPP shift; lane
+    // 63 takes the next wave's first column as a wave-uniform load), so a is clamped to cnx+1 instead of cnx —
+    // the same b for every lane, a different a only for lanes past the row's end, which correct nothing
+    constexpr bool RBDPP = MODE == GS_NEWTON && XH && PRO == 1;
+    const int cxl = min(x >> 1, max(RBDPP ? cnx + 1 : cnx, 0)); // the lane's coarse column (fine pair x odd, x+1 even)
+    const int cxe = min((x0 >> 1) + WAVE, cnx + 1);             // RBDPP: lane 63's b column
     const int cyb = mir ? ((y0 - 1) >> 1) + RY / 2 : ((y0 - 1) >> 1) - 1;
     int64_t crow[NCR];
 #pragma unroll
@@ -2239,14 +2244,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         else return s == 0 ? W0[r] : W1[r];
     };
     auto hget = [&](int s, int r) -> double2 { return s == 2 ? Hm[HALF ? r : 0] : (s == 0 ? H0[HALF ? r : 0] : H1[HALF ? r : 0]); };
-    double RA[NCR], RB[NCR], SA[NCR], SB[NCR]; // raw c (and sub) of plane K+2, in flight
+    double RA[NCR], RB[RBDPP ? 1 : NCR], RE[RBDPP ? NCR : 1], SA[NCR], SB[NCR]; // raw c (and sub) of plane K+2, in flight
     auto craw = [&](int cz) {
         // coarse planes -1 .. cnz+2 exist in the layout; only those under corrected fine planes matter
-        const int64_t zo = (int64_t)min(max(cz, -1), cnz + 2) * cldz + cxl;
+        const int64_t zp = (int64_t)min(max(cz, -1), cnz + 2) * cldz, zo = zp + cxl;
 #pragma unroll
         for (int r = 0; r < NCR; r++) {
             RA[r] = pc[zo + crow[r]];
-            RB[r] = pc[zo + crow[r] + 1];
+            if constexpr (RBDPP) RE[r] = pc[zp + crow[r] + cxe];
+            else RB[r] = pc[zo + crow[r] + 1];
             if (PRO == 2) {
                 SA[r] = ps[zo + crow[r]];
                 SB[r] = ps[zo + crow[r] + 1];
@@ -2257,7 +2263,9 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     auto xpass = [&](int s) {
 #pragma unroll
         for (int r = 0; r < NCR; r++) {
-            const double a = PRO == 2 ? RA[r] - SA[r] : RA[r], b = PRO == 2 ? RB[r] - SB[r] : RB[r];
+            const double a = PRO == 2 ? RA[r] - SA[r] : RA[r];
+            const double b = RBDPP ? lane_from_right<true>(RA[r], RE[RBDPP ? r : 0])
+                                   : (PRO == 2 ? RB[r] - SB[r] : RB[RBDPP ? 0 : r]);
             const double2 X = make_double2(0.5 * a + 0.5 * b, b);
             if constexpr (HALF) {
                 const double2 Hh = make_double2(0.5 * X.x, 0.5 * X.y);
