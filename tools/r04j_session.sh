@@ -28,8 +28,8 @@ for r in 1 2 3; do
   python -c "import json; d=json.load(open('$OUT/newton_r$r.json')); print('newton r$r', d['newton']['ms_per_iteration'])"
 done
 step ranks8
-PROF=1 bash tools/bench_ranks.sh r04j/ranks8 8 256 --vcycles 2 --cpu-sweeps 0 --newton-iters 0 --config5 0 > "$OUT/ranks8.log" 2>&1 || { tail -30 "$OUT/ranks8.log"; exit 1; }
-python tools/rccl_grid.py gpurun_out/r04j/ranks8 > "$OUT/rccl_grid.txt" || true
+PROF=1 bash tools/bench_ranks.sh ${1:-r04j}/ranks8 8 256 --vcycles 2 --cpu-sweeps 0 --newton-iters 0 --config5 0 > "$OUT/ranks8.log" 2>&1 || { tail -30 "$OUT/ranks8.log"; exit 1; }
+python tools/rccl_grid.py gpurun_out/${1:-r04j}/ranks8 > "$OUT/rccl_grid.txt" || true
 head -4 "$OUT/rccl_grid.txt" || true
-python -c "import json; d=json.load(open('gpurun_out/r04j/ranks8/rank0.json')); print({k: d['multi_gpu'][k] for k in ('rccl_ctas', 'rccl_channels_per_peer', 'rank_halo_host_us_max')})" || true
+python -c "import json; d=json.load(open('gpurun_out/${1:-r04j}/ranks8/rank0.json')); print({k: d['multi_gpu'][k] for k in ('rccl_ctas', 'rccl_channels_per_peer', 'rank_halo_host_us_max')})" || true
 step done
