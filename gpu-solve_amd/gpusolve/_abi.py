@@ -79,6 +79,10 @@ KERNEL_API = {
                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(gs_level), C.c_int, C.c_void_p]),
     "gs_tiled_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int]),
+    "gs_smooth2_restrict_zero_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.POINTER(gs_level),
+                                                     C.c_int]),
+    "gs_smooth2_restrict_zero": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.POINTER(gs_level), C.c_void_p]),
     "gs_smooth2_restrict_tiled": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double,
                                             C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(gs_level), C.c_void_p]),
