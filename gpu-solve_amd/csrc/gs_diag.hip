@@ -9,6 +9,290 @@
 
 namespace {
 
+// ---------------------------------------------------------------------------------------------
+// The first pre-smoothing pair, the residual of its result and the full-weighting restriction in ONE
+// pass (k_prr, LINEAR; CpuSolver.cpp:94-99 with preSmoothing = 2: jacobi x2, compResidual, restrict).
+// Level 0 of a 2+2 V-cycle is then two passes instead of three: this kernel reads v and f once and
+// writes v'' and the coarse f (25 B per fine point instead of 24 + 17).
+// A block is the whole x-row — PRR_WX waves, ONE column per lane, so a lane's z-windows of four stages
+// fit its registers — times a tile of PRR_T = 4 output rows y0..y0+3 (y0 odd: the tile holds the
+// centres of coarse rows (y0+1)/2 and (y0+3)/2). The restriction needs r on rows y0..y0+4, r needs v''
+// on y0-1..y0+5, v'' needs sweep 1 on y0-2..y0+6 and sweep 1 needs v on y0-3..y0+7: every stage's
+// extra rows are recomputed in-lane (no y exchange). Wavefront along z, at step z: sweep 1 at plane
+// z, sweep 2 at z-1, r at z-2, and the restriction of coarse plane Z = (z-4)/2 from r at z-5..z-3
+// (one step late, so that every x-edge it reads was published before this step's one barrier).
+// x-neighbours: DPP lane shifts, the columns beyond a wave's edges (v, sweep 1, sweep 2) through LDS;
+// r goes to an LDS ring of five planes that the restriction reads directly. A block walks a chunk of
+// coarse planes Zb..Ze: fine output planes 2Zb-1..2Ze (the last chunk up to nz), with the pipeline's
+// z-halo (sweep 1 from 2Zb-3, r up to 2Ze+1) recomputed at the chunk ends. Every point uses the
+// expression of k_tb2y / k_rr2 (same order, same boundary values), so v'' and the coarse f are
+// bit-identical to gs_jacobi_sweep2 + gs_residual_restrict; the norm partials are those of r = f - A v
+// (the input), as the speculative pair's, in this kernel's block order.
+// MEASURED SLOWER than the two passes it replaces, so the driver does not use it: 1.45 vs 1.10 ms at
+// 512^3 (tools/prr_bench.py). Its traffic is 1.06 x the 25 B/point, but the in-lane recomputation
+// costs 21 stencil evaluations per 4 outputs against 15 for pair + k_rr2, and one column per lane
+// doubles the DPP shifts: PMC 1.54 x the VALU instructions of the two kernels at 254 VGPRs (no
+// prefetch room beyond one plane of v). Kept as a tested operator (tests/test_gpu_pair_restrict.py).
+// ZV (r04, gs_smooth2_restrict_zero): a coarse level's first step from v = 0, whose first sweep is pointwise in f
+// (q = +0): no v loads and no sweep-1 stencils, one pass over f instead of the zero-iterate pair + k_rr2 (17
+// instead of 33 B per point). Measured no faster: 122 vs 62 + 63 us at a 256^3 level, 38 vs 15 + 13 us at 128^3
+// (r04r, profiles/r04/r04r_zero_pair_restrict_ab.txt) — the in-lane recomputation is what costs, as at level 0.
+constexpr int PRR_WX = 8, PRR_T = 4, PRR_RS = 5; // x-waves, output rows per block, r ring planes
+
+// WXP: x-waves the block is sized for (the r ring's LDS): 8 for rows of 257-512 points, 4 / 2 for shorter rows,
+// so that a 256-point level holds two blocks per CU instead of one
+template <bool UN, bool ZV = false, int WXP = PRR_WX>
+__global__ __launch_bounds__(WAVE* WXP) void k_prr(Coef k, const double* __restrict__ v, const double* __restrict__ f,
+                                                      double* __restrict__ out, double* __restrict__ partials,
+                                                      double* __restrict__ ca, double* __restrict__ cb, int nx, int ny,
+                                                      int nz, int64_t ldy, int64_t ldz, int cnx, int cny, int cnz,
+                                                      int64_t cldy, int64_t cldz, int ZC)
+{
+    // local rows i (global y0 + i): v -3..7, sweep 1 -2..6, sweep 2 -1..5, r 0..4
+    constexpr int NV = 11, N1 = 9, N2 = 7, NR = 5;
+    constexpr int NE = N1 + N2 + NR; // x-edge values per wave side and plane parity
+    constexpr int RW = WAVE * WXP + 2; // r ring row: columns 0 .. 64 WX + 1
+    __shared__ double edge[2][WXP + 2][2][NE];
+    // r of the last planes, every column of the tile's rows 0..4: slot p mod 5 (the restriction at step z
+    // reads planes z-5..z-3 while a wave one step ahead writes z-1 — five slots keep them apart)
+    __shared__ double rring[PRR_RS][NR][RW];
+    __shared__ double red[WXP];
+    const int lane = threadIdx.x;
+    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int WX = blockDim.y;
+    const int tid = lane + WAVE * wx;
+    for (int i = tid; i < 2 * (WXP + 2) * 2 * NE; i += WAVE * WX) (&edge[0][0][0][0])[i] = 0.0;
+    for (int i = tid; i < PRR_RS * NR * RW; i += WAVE * WX) (&rring[0][0][0])[i] = 0.0;
+    __syncthreads();
+    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+    const int y0 = 1 + (int)(tile % gridDim.x) * PRR_T;
+    const int Zb = 1 + (int)(tile / gridDim.x) * ZC, Ze = min(Zb + ZC - 1, cnz);
+    const int zb = 2 * Zb - 1, ze = Ze == cnz ? nz : 2 * Ze; // output planes of v''
+    const int rlast = 2 * Ze + 1;                            // last plane of r
+    const int s2last = max(ze, rlast + 1), s1last = s2last + 1;
+    const int x = 1 + wx * WAVE + lane;
+    const int xl = min(x, nx + 1);
+    const bool okx = x <= nx;
+    int64_t roff[NV]; // rows -3..7 at index i + 3
+    bool rowc[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        const int y = y0 - 3 + i;
+        roff[i] = (int64_t)min(max(y, 0), ny + 1) * ldy;
+        rowc[i] = y >= 1 && y <= ny;
+    }
+    auto at = [&](const double* b, int i, int p) {
+        return b + xl + roff[i + 3] + (int64_t)min(max(p, 0), nz + 1) * ldz;
+    };
+    auto pin = [&](int p) { return p >= 1 && p <= nz; };
+    auto rslot = [](int p) { return ((p % PRR_RS) + PRR_RS) % PRR_RS; };
+
+    double Vm[N1], Vc[NV], Vn[NV], VL[NV]; // v at z-1 (rows -2..6), z, z+1, z+2 in flight (rows -3..7)
+    double F0[N1], F1[N2], F2[NR];        // f at z (rows -2..6), z-1 (-1..5), z-2 (0..4)
+    double S1a[N2], S1b[N1];              // sweep 1 at z-2 (rows -1..5), z-1 (-2..6)
+    double S2a[NR], S2b[N2];              // sweep 2 at z-3 (rows 0..4), z-2 (-1..5)
+#pragma unroll
+    for (int i = 0; i < N1; i++) Vm[i] = ZV ? 0.0 : *at(v, i - 2, zb - 3);
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        Vc[i] = ZV ? 0.0 : *at(v, i - 3, zb - 2);
+        Vn[i] = ZV ? 0.0 : *at(v, i - 3, zb - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < N2; i++) {
+        F1[i] = 0.0;
+        S1a[i] = 0.0;
+        S2b[i] = 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < N1; i++) S1b[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+        F2[i] = 0.0;
+        S2a[i] = 0.0;
+    }
+    double sumsq = 0.0;
+    auto lds_barrier = [] {
+        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): LDS only, the loads stay in flight
+        __builtin_amdgcn_s_barrier();
+    };
+
+    for (int z = zb - 2; z <= s1last + 1; z++) {
+        // ---- loads: v(z+2) for the next step, f(z) for this step's sweep 1 ----
+#pragma unroll
+        for (int i = 0; i < NV; i++) VL[i] = ZV ? 0.0 : *at(v, i - 3, z + 2);
+#pragma unroll
+        for (int i = 0; i < N1; i++) F0[i] = *at(f, i - 2, z);
+        // ---- publish x-edges: v(z) rows -2..6, sweep 1 (z-1) rows -1..5, sweep 2 (z-2) rows 0..4 ----
+        const int ph = z & 1;
+        if (lane == 0 || lane == WAVE - 1) {
+            const int sd = lane == 0 ? 0 : 1;
+#pragma unroll
+            for (int i = 0; i < N1; i++) edge[ph][wx + 1][sd][i] = Vc[i + 1];
+#pragma unroll
+            for (int i = 0; i < N2; i++) edge[ph][wx + 1][sd][N1 + i] = S1b[i + 1];
+#pragma unroll
+            for (int i = 0; i < NR; i++) edge[ph][wx + 1][sd][N1 + N2 + i] = S2b[i + 1];
+        }
+        lds_barrier();
+        // the columns left of lane 0 / right of lane 63 (LDS broadcast reads, straight into the DPP's old operand)
+        auto CL = [&](int i) { return edge[ph][wx][1][i]; };
+        auto CR = [&](int i) { return edge[ph][wx + 2][0][i]; };
+
+        // ---- restriction of coarse plane Z from r at 2Z-1, 2Z, 2Z+1 (= z-5, z-4, z-3), read from the ring ----
+        if (!(z & 1) && (z - 4) / 2 >= Zb && (z - 4) / 2 <= Ze) {
+            const int Z = (z - 4) / 2;
+            const int X = x >> 1;
+            const int sl[3] = {rslot(z - 5), rslot(z - 4), rslot(z - 3)};
+            if (!(x & 1) && X <= cnx) {
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const int Y = (y0 + 1) / 2 + t, ic = 1 + 2 * t; // centre row y0 + ic = 2Y
+                    if (Y > cny) continue;
+                    double acc = 0.0;
+#pragma unroll
+                    for (int a = -1; a <= 1; a++)
+#pragma unroll
+                        for (int b = -1; b <= 1; b++)
+#pragma unroll
+                            for (int c = -1; c <= 1; c++) {
+                                const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
+                                                   ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                                acc += wgt * rring[sl[c + 1]][ic + b][x + a];
+                            }
+                    const int64_t q = X + Y * cldy + (int64_t)Z * cldz;
+                    ca[q] = acc;
+                    if (cb) cb[q] = acc;
+                }
+            }
+        }
+
+        // ---- sweep 1 at plane z, rows -2..6 ----
+        double S1n[N1];
+        if (z <= s1last) {
+            double q[N1];
+            if constexpr (ZV) { // v = 0: the stencil over h^2 is +0 exactly (Coef::zq, checked by the launcher)
+#pragma unroll
+                for (int i = 0; i < N1; i++) q[i] = 0.0;
+            } else {
+#pragma unroll
+                for (int i = 0; i < N1; i++) {
+                    const double c = Vc[i + 1];
+                    const double xm = lane_from_left<true>(c, CL(i)), xp = lane_from_right<true>(c, CR(i));
+                    q[i] = stencil_sum<UN>(k, c, xp, xm, Vc[i + 2], Vc[i], Vn[i + 1], Vm[i]);
+                }
+                div_hh_n(k, q);
+            }
+            const bool pz = pin(z);
+            const bool own = partials && z >= zb && z <= ze && pz && okx;
+#pragma unroll
+            for (int i = 0; i < N1; i++) {
+                const double c = Vc[i + 1];
+                const double r0 = F0[i] - q[i];
+                const double n = jacobi_update<GS_LINEAR>(k, c, r0, 0.0);
+                S1n[i] = (pz && rowc[i + 1] && okx) ? n : c;
+                if (own && i >= 2 && i <= 5 && rowc[i + 1]) sumsq += r0 * r0;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < N1; i++) S1n[i] = 0.0;
+        }
+        // ---- sweep 2 at plane z-1, rows -1..5 (stored: rows 0..3 of the output planes) ----
+        double S2n[N2];
+        if (z - 1 >= zb - 1 && z - 1 <= s2last) {
+            double q[N2];
+#pragma unroll
+            for (int i = 0; i < N2; i++) {
+                const double c = S1b[i + 1];
+                const double xm = lane_from_left<true>(c, CL(N1 + i)), xp = lane_from_right<true>(c, CR(N1 + i));
+                q[i] = stencil_sum<UN>(k, c, xp, xm, S1b[i + 2], S1b[i], S1n[i + 1], S1a[i]);
+            }
+            div_hh_n(k, q);
+            const int p = z - 1;
+            const bool pz = pin(p);
+            const bool st = p >= zb && p <= ze && pz && okx;
+#pragma unroll
+            for (int i = 0; i < N2; i++) {
+                const double c = S1b[i + 1];
+                const double n = jacobi_update<GS_LINEAR>(k, c, F1[i] - q[i], 0.0);
+                S2n[i] = (pz && rowc[i + 2] && okx) ? n : c;
+                if (st && i >= 1 && i <= 4 && rowc[i + 2])
+                    __builtin_nontemporal_store(n, out + x + roff[i + 2] + (int64_t)p * ldz);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < N2; i++) S2n[i] = 0.0;
+        }
+        // ---- r = f - A v'' at plane z-2, rows 0..4 (0 outside the interior) -> the ring ----
+        if (z - 2 >= zb && z - 2 <= rlast) {
+            double q[NR];
+#pragma unroll
+            for (int i = 0; i < NR; i++) {
+                const double c = S2b[i + 1];
+                const double xm = lane_from_left<true>(c, CL(N1 + N2 + i)), xp = lane_from_right<true>(c, CR(N1 + N2 + i));
+                q[i] = stencil_sum<UN>(k, c, xp, xm, S2b[i + 2], S2b[i], S2n[i + 1], S2a[i]);
+            }
+            div_hh_n(k, q);
+            const bool pz = pin(z - 2);
+            const int sl = rslot(z - 2);
+#pragma unroll
+            for (int i = 0; i < NR; i++) rring[sl][i][x] = (pz && rowc[i + 3] && okx) ? F2[i] - q[i] : 0.0;
+        }
+        // ---- rotate ----
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            S2a[i] = S2b[i + 1];
+            F2[i] = F1[i + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < N2; i++) {
+            S2b[i] = S2n[i];
+            S1a[i] = S1b[i + 1];
+            F1[i] = F0[i + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < N1; i++) {
+            S1b[i] = S1n[i];
+            Vm[i] = Vc[i + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            Vc[i] = Vn[i];
+            Vn[i] = VL[i];
+        }
+    }
+    if (partials) {
+        sumsq = wave_sum(sumsq);
+        if (lane == 0) red[wx] = sumsq;
+        __syncthreads();
+        if (tid == 0) {
+            double t = 0.0;
+            for (int i = 0; i < WX; i++) t += red[i];
+            partials[tile] = t;
+        }
+    }
+}
+
+// k_prr geometry: the whole row in one block (<= 512 points), 4-row tiles, chunks of coarse planes for
+// ~512 blocks (one 8-wave block per CU, two rounds at 512^3; 4..64 coarse planes: the chunk ends
+// recompute five planes of the pipeline)
+static bool prr_plan(const gs_stencil* S, const gs_level* fl, const gs_level* cl, int mode, int* zc, dim3* g, dim3* b)
+{
+    if (!S || !valid_stencil(S) || !canonical_order(S) || mode != GS_LINEAR || bad_level(fl) || bad_level(cl) ||
+        !make_coef(S, fl, 0.0, 0.0).unit || // the unit-neighbour stencil sum (the general one spills here)
+        fl->z0 != 0 || cl->z0 != 0 || fl->nx < 1 || fl->nx > WAVE * PRR_WX || fl->ny < 1 || fl->nz < 2 ||
+        cl->nx != fl->nx / 2 || cl->ny != fl->ny / 2 || cl->nz != fl->nz / 2 || cl->nx < 1 || cl->ny < 1)
+        return false;
+    const int64_t tiles = (fl->ny + PRR_T - 1) / PRR_T;
+    int64_t c = (cl->nz * tiles + 511) / 512;
+    c = c < 4 ? 4 : (c > 64 ? 64 : c);
+    *zc = (int)c;
+    *g = dim3((unsigned)tiles, (unsigned)((cl->nz + c - 1) / c));
+    *b = dim3(WAVE, (unsigned)((fl->nx + WAVE - 1) / WAVE));
+    return true;
+}
+
+
 // ---- tuning variants of the LINEAR sweep (tools/kbench.py) -------------------------------------
 using RbKernel = void (*)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
                           int64_t, int);
@@ -144,6 +428,35 @@ int gs_jacobi_sweep2_restrict(const gs_stencil* S, const gs_level* fl, double om
     const Coef k = make_coef(S, fl, omega, 0.0);
     hipLaunchKernelGGL((k_prr<true>), g, b, 0, st, k, v_in, f, v_out, partials, ca, cb, (int)fl->nx, (int)fl->ny,
                        (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, zc);
+    return launch_status();
+}
+
+// a coarse level's first down-leg step from v = 0 in one pass (gs_device.hpp k_prr<UN=true, ZV=true>): the first
+// sweep of a zero iterate is pointwise in f (q = +0, Coef::zq), so sweep 2, the residual and the restriction
+// follow from f alone
+int gs_smooth2_restrict_zero_supported(const gs_stencil* S, const gs_level* fl, const gs_level* cl, int mode)
+{
+    int zc;
+    dim3 g, b;
+    return (prr_plan(S, fl, cl, mode, &zc, &g, &b) && make_coef(S, fl, 0.0, 0.0).zq) ? 1 : 0;
+}
+
+int gs_smooth2_restrict_zero(const gs_stencil* S, const gs_level* fl, double omega, double* v_out, const double* f,
+                             double* coarse_f, const gs_level* cl, hipStream_t st)
+{
+    int zc;
+    dim3 g, b;
+    if (!gs_smooth2_restrict_zero_supported(S, fl, cl, GS_LINEAR) || !v_out || !f || !coarse_f ||
+        !prr_plan(S, fl, cl, GS_LINEAR, &zc, &g, &b))
+        return GS_EINVAL;
+    const Coef k = make_coef(S, fl, omega, 0.0);
+#define GS_ZPRR(WXP) hipLaunchKernelGGL((k_prr<true, true, WXP>), g, b, 0, st, k, nullptr, f, v_out, nullptr, coarse_f, nullptr, \
+                       (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, \
+                       cl->ldy, cl->ldz, zc)
+    if (b.y <= 2) GS_ZPRR(2);
+    else if (b.y <= 4) GS_ZPRR(4);
+    else GS_ZPRR(PRR_WX);
+#undef GS_ZPRR
     return launch_status();
 }
 

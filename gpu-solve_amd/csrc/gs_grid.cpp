@@ -173,7 +173,6 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         sw.fusedProlong = !on("GS_NO_FUSED_PROLONG");
         sw.fusedRR = !on("GS_NO_FUSED_RR");
         sw.zeroGuess = !on("GS_NO_ZERO_GUESS");
-        sw.zeroPairRR = !on("GS_NO_ZPRR");
         sw.pipeline = !on("GS_NO_PIPELINE");
         sw.newtonFusedUpdate = !on("GS_NO_NEWTON_FUSED_UPDATE");
         if (const char* e = std::getenv("GS_NEWTON_PRO_POINTS")) sw.newtonProPoints = std::strtoll(e, nullptr, 10);
@@ -1027,25 +1026,6 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
             if (grid.trace) grid.rec("swap", {{"L", (long long)i}});
             L.vZero = false;
             C.vZero = true; // LINEAR / NEWTON: v^2h = 0 (CpuSolver.cpp:100-101), not stored
-            grid.clock.mark(s, (int)i, false);
-            continue;
-        }
-        // a LINEAR coarse level's step from v = 0 (rows <= 512 points, whole levels): the first sweep of a zero
-        // iterate is pointwise in f, so the pair, the residual and the restriction are ONE pass reading f once
-        // (gs_smooth2_restrict_zero: 17 instead of 16 + 17 B per point; GS_NO_ZPRR keeps the two passes)
-        if (i >= 1 && pre == 2 && L.vZero && grid.mode == GridParams::LINEAR && !L.distributed && !C.distributed &&
-            grid.sw.fusedSweeps && grid.sw.fusedRR && grid.sw.zeroGuess && grid.sw.zeroPairRR &&
-            gs_smooth2_restrict_zero_supported(&grid.stencilAbi, &L.geom, &C.geom, (int)grid.mode)) {
-            if (grid.trace)
-                grid.rec("zprr", {{"L", (long long)i}});
-            else
-                check(gs_smooth2_restrict_zero(&grid.stencilAbi, &L.geom, grid.omega, L.vAlt.data(), L.f.data(),
-                                               C.f.data(), &C.geom, s),
-                      "gs_smooth2_restrict_zero");
-            L.v.swap(L.vAlt);
-            if (grid.trace) grid.rec("swap", {{"L", (long long)i}});
-            L.vZero = false;
-            C.vZero = true; // v^2h = 0 (CpuSolver.cpp:114-116), not stored
             grid.clock.mark(s, (int)i, false);
             continue;
         }

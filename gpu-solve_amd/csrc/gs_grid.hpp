@@ -147,8 +147,6 @@ public:
         bool fusedProlong = true;  // GS_NO_FUSED_PROLONG: gs_prolong_add + the plain pair
         bool fusedRR = true;       // GS_NO_FUSED_RR: residual stored, then restricted
         bool zeroGuess = true;     // GS_NO_ZERO_GUESS: coarse v = 0 stored instead of flagged
-        bool zeroPairRR = true;    // GS_NO_ZPRR: a coarse level's first step from v = 0 as the pair + k_rr2, not
-                                   // one gs_smooth2_restrict_zero pass
         bool pipeline = true;      // GS_NO_PIPELINE: no overlap of the norm wait with the next cycle
         bool newtonFusedUpdate = true; // GS_NO_NEWTON_FUSED_UPDATE: newtonV += v, then compF (two passes)
         int64_t tilePoints = (int64_t)1 << 18; // GS_TILE_POINTS: levels of at most this many points (replicated,

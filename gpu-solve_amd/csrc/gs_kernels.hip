@@ -228,35 +228,6 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     return launch_status();
 }
 
-// a coarse level's first down-leg step from v = 0 in one pass (gs_device.hpp k_prr<UN=true, ZV=true>): the first
-// sweep of a zero iterate is pointwise in f (q = +0, Coef::zq), so sweep 2, the residual and the restriction
-// follow from f alone
-int gs_smooth2_restrict_zero_supported(const gs_stencil* S, const gs_level* fl, const gs_level* cl, int mode)
-{
-    int zc;
-    dim3 g, b;
-    return (prr_plan(S, fl, cl, mode, &zc, &g, &b) && make_coef(S, fl, 0.0, 0.0).zq) ? 1 : 0;
-}
-
-int gs_smooth2_restrict_zero(const gs_stencil* S, const gs_level* fl, double omega, double* v_out, const double* f,
-                             double* coarse_f, const gs_level* cl, hipStream_t st)
-{
-    int zc;
-    dim3 g, b;
-    if (!gs_smooth2_restrict_zero_supported(S, fl, cl, GS_LINEAR) || !v_out || !f || !coarse_f ||
-        !prr_plan(S, fl, cl, GS_LINEAR, &zc, &g, &b))
-        return GS_EINVAL;
-    const Coef k = make_coef(S, fl, omega, 0.0);
-#define GS_ZPRR(WXP) hipLaunchKernelGGL((k_prr<true, true, WXP>), g, b, 0, st, k, nullptr, f, v_out, nullptr, coarse_f, nullptr, \
-                       (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, \
-                       cl->ldy, cl->ldz, zc)
-    if (b.y <= 2) GS_ZPRR(2);
-    else if (b.y <= 4) GS_ZPRR(4);
-    else GS_ZPRR(PRR_WX);
-#undef GS_ZPRR
-    return launch_status();
-}
-
 // the small-level tiled kernels (gs_device.hpp k_tile_*): LINEAR / NEWTON, canonical stencil order, whole levels
 int gs_tiled_supported(const gs_stencil* S, const gs_level* L, int mode)
 {

@@ -79,10 +79,6 @@ KERNEL_API = {
                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(gs_level), C.c_int, C.c_void_p]),
     "gs_tiled_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int]),
-    "gs_smooth2_restrict_zero_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.POINTER(gs_level),
-                                                     C.c_int]),
-    "gs_smooth2_restrict_zero": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
-                                           C.c_void_p, C.c_void_p, C.POINTER(gs_level), C.c_void_p]),
     "gs_smooth2_restrict_tiled": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int, C.c_double,
                                             C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(gs_level), C.c_void_p]),
@@ -156,6 +152,10 @@ DRIVER_API = {
 
 # libgpusolve_diag.so (include/gpusolve_diag.h): tuning variants, bandwidth probes, k_prr — not the product
 DIAG_API = {
+    "gs_smooth2_restrict_zero_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.POINTER(gs_level),
+                                                     C.c_int]),
+    "gs_smooth2_restrict_zero": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.POINTER(gs_level), C.c_void_p]),
     "gs_jacobi_sweep2_restrict_supported": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level),
                                                       C.POINTER(gs_level), C.c_int]),
     "gs_jacobi_sweep2_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,

@@ -25,6 +25,16 @@ int gs_jacobi_sweep2_restrict(const gs_stencil* S, const gs_level* fine, double 
                               double* v_out, const double* f, double* partials, double* coarse_a, double* coarse_b,
                               const gs_level* coarse, hipStream_t stream);
 int64_t gs_jacobi_sweep2_restrict_num_partials(const gs_stencil* S, const gs_level* fine, const gs_level* coarse);
+/* Measured and not adopted (r04, DESIGN.md §9: 122 vs 125 us at a 256^3 level, 38 vs 28 us at 128^3):
+ * a coarse level's first down-leg step from v = 0 (LINEAR, canonical unit stencil, whole levels of rows <=
+ * 512 points, Coef-style finite weights and h^2 normal): the zero-iterate pair's first sweep is pointwise in
+ * f there, so ONE pass reads f once and writes v_out = S(S(0)) and coarse_f = R(f - A v_out)
+ *   == two jacobi sweeps from v = 0 + compResidual + restrict          CpuSolver.cpp:94-99,114-116,141-180,211-238
+ * bit-identical to gs_jacobi_sweep2 (v_in NULL) + gs_residual_restrict. Only interior points of v_out are
+ * written; coarse = fine / 2 per axis. */
+int gs_smooth2_restrict_zero_supported(const gs_stencil* S, const gs_level* fine, const gs_level* coarse, int mode);
+int gs_smooth2_restrict_zero(const gs_stencil* S, const gs_level* fine, double omega, double* v_out, const double* f,
+                             double* coarse_f, const gs_level* coarse, hipStream_t stream);
 
 /* ---- tuning / diagnostics (tools/kbench.py) ----
  * Alternative tilings of the LINEAR fused sweep (bit-identical results), and a streaming

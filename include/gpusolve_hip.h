@@ -154,15 +154,6 @@ int gs_smooth2_restrict_tiled(const gs_stencil* S, const gs_level* fine, int mod
 int gs_prolong_smooth2_tiled(const gs_stencil* S, const gs_level* fine, int mode, double omega, double gamma,
                              const double* v_in, const double* coarse_v, const gs_level* coarse, double* v_out,
                              const double* f, const double* w, hipStream_t stream);
-/* A coarse level's first down-leg step from v = 0 (LINEAR, canonical unit stencil, whole levels of rows <=
- * 512 points, Coef-style finite weights and h^2 normal): the zero-iterate pair's first sweep is pointwise in
- * f there, so ONE pass reads f once and writes v_out = S(S(0)) and coarse_f = R(f - A v_out)
- *   == two jacobi sweeps from v = 0 + compResidual + restrict          CpuSolver.cpp:94-99,114-116,141-180,211-238
- * bit-identical to gs_jacobi_sweep2 (v_in NULL) + gs_residual_restrict. Only interior points of v_out are
- * written; coarse = fine / 2 per axis. */
-int gs_smooth2_restrict_zero_supported(const gs_stencil* S, const gs_level* fine, const gs_level* coarse, int mode);
-int gs_smooth2_restrict_zero(const gs_stencil* S, const gs_level* fine, double omega, double* v_out, const double* f,
-                             double* coarse_f, const gs_level* coarse, hipStream_t stream);
 /* Which fused-pair kernel (and shape) gs_jacobi_sweep2 launches for this level and mode ("" if none). */
 const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int mode);
 

@@ -92,7 +92,7 @@ def test_pair_restrict_supported_cases():
 
 @pytest.mark.parametrize("shape", SHAPES + [(256, 256, 64), (255, 31, 17)])
 def test_zero_pair_restrict_equals_zero_pair_then_restrict(shape):
-    """gs_smooth2_restrict_zero (the product's one-pass form of a coarse level's first step from v = 0, r04) against
+    """gs_smooth2_restrict_zero (diagnostics library: a coarse level's first step from v = 0 in one pass, r04) against
     the zero-iterate pair (v_in NULL) followed by gs_residual_restrict, bit for bit on v'' and the coarse f."""
     S = gsv.Stencil().to_abi()
     rng = np.random.default_rng(abs(hash(shape)) % 2**32 + 5)
@@ -103,11 +103,11 @@ def test_zero_pair_restrict_equals_zero_pair_then_restrict(shape):
     cn = (nx // 2, ny // 2, nz // 2)
     c1, c2 = DevField(*cn, fill=-7.0), DevField(*cn, fill=-7.0)
     L, CL = f.level(h), c1.level(2 * h)
-    assert k().gs_smooth2_restrict_zero_supported(C.byref(S), C.byref(L), C.byref(CL), 0) == 1
+    assert gsv.diag().gs_smooth2_restrict_zero_supported(C.byref(S), C.byref(L), C.byref(CL), 0) == 1
     ok(k().gs_jacobi_sweep2(C.byref(S), C.byref(L), 0, 0.8, 1.0, None, out1.ptr, f.ptr, None, 0, 0, st()))
     ok(k().gs_residual_restrict(C.byref(S), C.byref(L), 0, 1.0, out1.ptr, f.ptr, None, c1.ptr, None, C.byref(CL),
                                 st()))
-    ok(k().gs_smooth2_restrict_zero(C.byref(S), C.byref(L), 0.8, out2.ptr, f.ptr, c2.ptr, C.byref(CL), st()))
+    ok(gsv.diag().gs_smooth2_restrict_zero(C.byref(S), C.byref(L), 0.8, out2.ptr, f.ptr, c2.ptr, C.byref(CL), st()))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out2.to_xyz(), out1.to_xyz())
     np.testing.assert_array_equal(c2.to_xyz(), c1.to_xyz())
@@ -117,13 +117,13 @@ def test_zero_pair_restrict_refusals():
     S = gsv.Stencil().to_abi()
     v, c = DevField(64, 16, 16), DevField(32, 8, 8)
     L, CL = v.level(1.0 / 17), c.level(2.0 / 17)
-    assert k().gs_smooth2_restrict_zero_supported(C.byref(S), C.byref(L), C.byref(CL), 0) == 1
+    assert gsv.diag().gs_smooth2_restrict_zero_supported(C.byref(S), C.byref(L), C.byref(CL), 0) == 1
     for mode in (1, 2):  # LINEAR only
-        assert k().gs_smooth2_restrict_zero_supported(C.byref(S), C.byref(L), C.byref(CL), mode) == 0
+        assert gsv.diag().gs_smooth2_restrict_zero_supported(C.byref(S), C.byref(L), C.byref(CL), mode) == 0
     wide, cw = DevField(513, 4, 4), DevField(256, 2, 2)  # rows > 512 points
-    assert k().gs_smooth2_restrict_zero_supported(C.byref(S), C.byref(wide.level(0.2)), C.byref(cw.level(0.4)), 0) == 0
+    assert gsv.diag().gs_smooth2_restrict_zero_supported(C.byref(S), C.byref(wide.level(0.2)), C.byref(cw.level(0.4)), 0) == 0
     gen = gsv.Stencil()
     gen.values = [6.5, -1, -1, -1, -1, -1, -1.5]  # not the unit-neighbour stencil
-    assert k().gs_smooth2_restrict_zero_supported(C.byref(gen.to_abi()), C.byref(L), C.byref(CL), 0) == 0
-    rc = k().gs_smooth2_restrict_zero(C.byref(gen.to_abi()), C.byref(L), 0.8, v.ptr, v.ptr, c.ptr, C.byref(CL), st())
+    assert gsv.diag().gs_smooth2_restrict_zero_supported(C.byref(gen.to_abi()), C.byref(L), C.byref(CL), 0) == 0
+    rc = gsv.diag().gs_smooth2_restrict_zero(C.byref(gen.to_abi()), C.byref(L), 0.8, v.ptr, v.ptr, c.ptr, C.byref(CL), st())
     assert rc == gsv._abi.GS_EINVAL

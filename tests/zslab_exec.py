@@ -485,11 +485,11 @@ class Rank:
                 self.op_restrict(L, Ls[kv["L"] + 1], src, dsts.split(","), kv["c1"], kv["c2"])
             elif op == "coarse":
                 self.op_coarse(kv["from"], kv["vzero"])
-            elif op in ("tiledpre", "zprr"):
-                # gs_smooth2_restrict_tiled / gs_smooth2_restrict_zero on a replicated level: the pair into vAlt,
-                # then the residual of that result restricted onto every coarse plane (zprr: from v = 0)
+            elif op == "tiledpre":
+                # gs_smooth2_restrict_tiled on a replicated level: the pair into vAlt, then the residual of
+                # that result restricted onto every coarse plane
                 C_ = Ls[kv["L"] + 1]
-                self.op_pair(L, 1, L.nz, 0, 0, kv.get("vzero", 1), 0)
+                self.op_pair(L, 1, L.nz, 0, 0, kv["vzero"], 0)
                 L.fields["v"], L.fields["vAlt"] = L.fields["vAlt"], L.fields["v"]
                 self.op_resrestrict(L, C_, 1, C_.nz)
                 L.fields["v"], L.fields["vAlt"] = L.fields["vAlt"], L.fields["v"]
