@@ -361,7 +361,12 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         const int64_t chunks = (2048 + rows - 1) / rows;
         int64_t zc = (cl->nz + chunks - 1) / chunks;
         zc = zc < 1 ? 1 : (zc > 32 ? 32 : zc);
-        if (kKnobs.rrZc > 0 && !big) zc = kKnobs.rrZc; // (A/B: fine levels of < 2^26 points)
+        // levels of >= 2^26 points: 64-coarse-plane chunks (512^3: 512 blocks, one round at two per CU): k_rr2
+        // 0.454-0.462 vs 0.496-0.500 ms, V-cycle 2.111-2.118 vs 2.145-2.148 ms; 1024^3: 4.06 vs 4.12 ms,
+        // V-cycle 16.71 vs 16.83-16.86 ms (16 / 32 / 128 planes all slower; profiles/r04/r04w_rr2_zc_big_ab.txt)
+        if (big) zc = cl->nz < 64 ? (cl->nz < 1 ? 1 : cl->nz) : 64;
+        if (kKnobs.rrZc > 0 && !big) zc = kKnobs.rrZc;       // (A/B: fine levels of < 2^26 points)
+        if (kKnobs.rrZcBig > 0 && big) zc = kKnobs.rrZcBig; // (A/B: fine levels of >= 2^26 points)
         const dim3 g((unsigned)rows, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
