@@ -120,11 +120,12 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_MID_ZC=n          z-chunk of pair launches over whole levels of < 2^26 points (A/B)
 //   GS_RR_ZC=n           z-chunk (coarse planes) of k_rr2 launches from fine levels of < 2^26 points (A/B)
 //   GS_RR_ZC_BIG=n       the same for fine levels of >= 2^26 points (A/B)
+//   GS_PAIR_ONE_ROUND_MID=1 LINEAR pair launches over levels of 2^24 .. 2^26 points in one round of blocks (A/B)
 //   GS_NEWTON_XH=0       NEWTON plain pairs on rows of 513-1024 points through k_tb2 instead of column blocks (A/B)
 //   GS_SPEC_CACHED=1     pairs with norm partials store through the caches, not non-temporally (A/B)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh, specCached;
-    int xhSwizzle, midZc, rrZc, rrZcBig;
+    int xhSwizzle, midZc, rrZc, rrZcBig, oneRoundMid;
     int slabZc, pairZc, rrNr, rrNtu, rrReverse;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
@@ -138,7 +139,7 @@ struct Knobs {
           bigChunks(num("GS_PAIR_BIG_CHUNKS", 1) != 0), oneRound(num("GS_PAIR_ONE_ROUND", 1) != 0),
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
           newtonXh(num("GS_NEWTON_XH", 1) != 0), specCached(num("GS_SPEC_CACHED", 0) != 0),
-          xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
+          xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), oneRoundMid(num("GS_PAIR_ONE_ROUND_MID", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
           rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 1)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
@@ -2768,6 +2769,17 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
         }
     }
     if (kKnobs.midZc > 0 && L->z0 == 0 && L->nx * L->ny * L->nz < ((int64_t)1 << 26)) c = std::max(2, kKnobs.midZc);
+    // GS_PAIR_ONE_ROUND_MID=1: LINEAR levels of 2^24 .. 2^26 points (256^3) in one round of blocks too (A/B)
+    if (kKnobs.oneRoundMid && mode == GS_LINEAR && (two || colb) && L->z0 == 0 &&
+        L->nx * L->ny * L->nz >= ((int64_t)1 << 24) && L->nx * L->ny * L->nz < ((int64_t)1 << 26)) {
+        const int64_t cus = device_cus();
+        if (tiles <= cus) {
+            const int64_t per = cus / tiles;
+            int64_t c1 = (L->nz + per - 1) / per;
+            c1 += c1 & 1;
+            if (c1 > c) c = c1;
+        }
+    }
     c &= ~(int64_t)1; // even: every chunk starts on an odd plane (the fused prolongation's parities)
     *zc = (int)c;
     *grid = dim3((unsigned)tiles, (unsigned)((L->nz + c - 1) / c));

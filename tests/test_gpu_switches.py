@@ -19,7 +19,7 @@ SWITCHES = ["GS_COARSE_POINTS", "GS_NEWTON_PRO_POINTS", "GS_RR_NR", "GS_RR_LDS",
             "GS_TBX_PFD", "GS_PAIR_BIG_CHUNKS", "GS_NO_UNIT_STENCIL", "GS_PAIR_MIN_BLOCKS", "GS_FIT_ROUNDS",
             "GS_NO_PIPELINE", "GS_NO_NEWTON_FUSED_UPDATE", "GS_RR_NTU", "GS_PAIR_ONE_ROUND", "GS_SLAB_ZC", "GS_PAIR_ZC",
             "GS_RR_REVERSE", "GS_HALO_ORDER", "GS_NO_ZERO_Q", "GS_XH_SWIZZLE",
-            "GS_MID_ZC", "GS_RR_ZC", "GS_NEWTON_XH", "GS_SPEC_CACHED", "GS_RR_ZC_BIG"]
+            "GS_MID_ZC", "GS_RR_ZC", "GS_NEWTON_XH", "GS_SPEC_CACHED", "GS_RR_ZC_BIG", "GS_PAIR_ONE_ROUND_MID"]
 
 # (case, solve args) -> the switches whose paths that problem exercises
 CASES = {
@@ -29,7 +29,7 @@ CASES = {
                                           ("GS_RR_NR", "2"), ("GS_NO_UNIT_STENCIL", "1"),
                                           ("GS_PAIR_MIN_BLOCKS", "512"), ("GS_FIT_ROUNDS", "0"),
                                           ("GS_COARSE_POINTS", "4096"), ("GS_NO_ZERO_Q", "1"),
-                                          ("GS_MID_ZC", "32"), ("GS_RR_ZC", "5")]),
+                                          ("GS_MID_ZC", "32"), ("GS_RR_ZC", "5"), ("GS_PAIR_ONE_ROUND_MID", "1")]),
     "linear2e26": ((0, 512, 512, 256, 2), [("GS_RR_NR", "1"), ("GS_PAIR_BIG_CHUNKS", "0"), ("GS_RR_NTU", "0"),
                                            ("GS_RR_ZC_BIG", "7")]),
     "linear512": ((0, 512, 512, 512, 2), [("GS_PAIR_ONE_ROUND", "0"), ("GS_PAIR_ZC", "96"), ("GS_RR_REVERSE", "0"),
