@@ -121,11 +121,12 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_RR_ZC=n           z-chunk (coarse planes) of k_rr2 launches from fine levels of < 2^26 points (A/B)
 //   GS_RR_ZC_BIG=n       the same for fine levels of >= 2^26 points (A/B)
 //   GS_PAIR_ONE_ROUND_MID=1 LINEAR pair launches over levels of 2^24 .. 2^26 points in one round of blocks (A/B)
+//   GS_RB_ZC=n           z-chunk of the one-point passes (k_rb sweeps / residuals, the Newton update pass) (A/B)
 //   GS_NEWTON_XH=0       NEWTON plain pairs on rows of 513-1024 points through k_tb2 instead of column blocks (A/B)
 //   GS_SPEC_CACHED=1     pairs with norm partials store through the caches, not non-temporally (A/B)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh, specCached;
-    int xhSwizzle, midZc, rrZc, rrZcBig, oneRoundMid;
+    int xhSwizzle, midZc, rrZc, rrZcBig, oneRoundMid, rbZc;
     int slabZc, pairZc, rrNr, rrNtu, rrReverse;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
@@ -139,7 +140,7 @@ struct Knobs {
           bigChunks(num("GS_PAIR_BIG_CHUNKS", 1) != 0), oneRound(num("GS_PAIR_ONE_ROUND", 1) != 0),
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
           newtonXh(num("GS_NEWTON_XH", 1) != 0), specCached(num("GS_SPEC_CACHED", 0) != 0),
-          xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), oneRoundMid(num("GS_PAIR_ONE_ROUND_MID", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
+          xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), oneRoundMid(num("GS_PAIR_ONE_ROUND_MID", 0)), rbZc(num("GS_RB_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
           rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 1)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
@@ -2817,6 +2818,7 @@ PassPlan pass_plan(const gs_stencil* S, const gs_level* L)
     }
     int64_t zc = L->nz * tiles / 2048;
     zc = zc < RB_ZCMIN ? RB_ZCMIN : (zc > RB_ZCMAX ? RB_ZCMAX : zc);
+    if (kKnobs.rbZc > 0) zc = kKnobs.rbZc + (kKnobs.rbZc & 1); // (A/B; even: the fused restriction's plane parity)
     p.rb = true;
     p.zc = (int)zc;
     p.grid = rb_grid(L, RB_RY, RB_W, p.zc);
