@@ -60,6 +60,9 @@ def parse():
                     help="N=1: also time config #5's 1024^3 grid on this GPU (the strong-scaling denominator)")
     ap.add_argument("--newton-iters", type=int, default=2,
                     help="timed Newton iterations of BASELINE config #4 (512^3 Newton 2+2) at N=1 (0: skip)")
+    ap.add_argument("--cta-ab", default="16,64",
+                    help="N > 1: after the headline, time the same sweeps on fresh RCCL communicators with these "
+                         "CTA budgets (ncclConfig_t::minCTAs = maxCTAs), interleaved twice ('' skips)")
     return ap.parse_args()
 
 
@@ -137,8 +140,9 @@ def global_dims(n, world):
     return table.get(world, (n, n, n * world))
 
 
-def make_grid(params, rank, world):
-    """Single-GPU grid, or this rank's Z-slab of an RCCL-partitioned grid."""
+def make_grid(params, rank, world, ctas=-1):
+    """Single-GPU grid, or this rank's Z-slab of an RCCL-partitioned grid (its own communicator, CTA budget
+    `ctas`; -1: the library's default)."""
     import ctypes as C
     if world == 1:
         return gsv.HipGridData(params)
@@ -152,7 +156,7 @@ def make_grid(params, rank, world):
     grid = gsv.HipGridData.__new__(gsv.HipGridData)
     grid.params = params
     grid._abi_params = params.to_abi()
-    grid.handle = drv.gs_grid_create_rccl(C.byref(grid._abi_params), rank, world, uid)
+    grid.handle = drv.gs_grid_create_rccl_ctas(C.byref(grid._abi_params), rank, world, uid, ctas)
     if not grid.handle:
         raise gsv.GpuSolveError(drv.gs_last_error().decode())
     return grid
@@ -273,37 +277,49 @@ def slab_local_pair_ms(grid, rank, world, k):
     return e0.elapsed_time(e1) / k
 
 
-def triad_ceiling(n):
-    """This GPU's achievable rate for the smoother's byte pattern (2 streamed reads + 1 streamed write,
-    24 B per element) on arrays of the level's size — the best of a few grid sizes of the streaming
-    triad kernel (gs_debug_bw). Boxes differ by up to ~25%, so the kernel's fraction of it is reported
-    next to the fraction of the 8 TB/s datasheet peak."""
-    kl = gsv.diag()  # the streaming probe lives in the diagnostics library
+CEILING_KINDS = {"read": (0, 8.0), "copy": (2, 16.0), "triad": (3, 24.0)}  # gs_debug_bw kind, bytes per element
+
+
+def stream_ceilings(n):
+    """This GPU's streaming ceilings on arrays of the level's size, measured in this run beside the kernels
+    they bound: the triad (2 streamed reads + 1 streamed write, 24 B per element: the smoother's byte mix),
+    a copy (1 read + 1 write) and a read-only stream, each 16 B per lane (dwordx4) in a grid-stride loop
+    (gs_debug_bw), the best over 1024 / 2048 / 4096 blocks x 1 / 4 loads in flight per lane x default /
+    non-temporal policy. Boxes differ by up to ~25 %, so the kernel's fraction of these is reported next
+    to the fraction of the 8 TB/s datasheet peak."""
+    kl = gsv.diag()  # the streaming probes live in the diagnostics library
     A = torch.rand(n, dtype=torch.float64, device="cuda")
     B = torch.rand(n, dtype=torch.float64, device="cuda")
     O = torch.empty(n, dtype=torch.float64, device="cuda")
     sink = torch.zeros(1, dtype=torch.float64, device="cuda")
     st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best = None
-    for blocks in (1024, 2048, 4096):
-        def run():
-            kl.gs_debug_bw(3, 1, 1, blocks, O.data_ptr(), A.data_ptr(), B.data_ptr(), n, sink.data_ptr(),
-                           st.cuda_stream)
-        for _ in range(2):
-            run()
-        e0.record(st)
-        for _ in range(10):
-            run()
-        e1.record(st)
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 10
-        if best is None or ms < best[0]:
-            best = (ms, blocks)
+    out = {}
+    for name, (kind, bpe) in CEILING_KINDS.items():
+        best = None
+        for blocks in (1024, 2048, 4096):
+            for unroll in (1, 4):
+                for nt in (1, 0):
+                    def run():
+                        rc = kl.gs_debug_bw(kind, unroll, nt, blocks, O.data_ptr(), A.data_ptr(), B.data_ptr(), n,
+                                            sink.data_ptr(), st.cuda_stream)
+                        assert rc == 0, rc
+                    for _ in range(2):
+                        run()
+                    e0.record(st)
+                    for _ in range(8):
+                        run()
+                    e1.record(st)
+                    torch.cuda.synchronize()
+                    ms = e0.elapsed_time(e1) / 8
+                    if best is None or ms < best[0]:
+                        best = (ms, blocks, unroll, nt)
+        ms, blocks, unroll, nt = best
+        out[name] = {"kernel": (f"streaming {name}, {int(bpe)} B per element, 16 B per lane, {blocks} blocks, "
+                                f"{unroll} load(s) in flight per lane, {'nt' if nt else 'default policy'}"),
+                     "elements": n, "ms": round(ms, 4), "gbps": round(bpe * n / (ms * 1e-3) / 1e9, 1)}
     del A, B, O
-    ms, blocks = best
-    return {"kernel": f"streaming triad out = a + 0.8 b, 24 B per element, nt, {blocks} blocks", "elements": n,
-            "ms": round(ms, 4), "gbps": round(24.0 * n / (ms * 1e-3) / 1e9, 1)}
+    return out
 
 
 def newton_timing(n, iters):
@@ -372,9 +388,52 @@ def config5_single_gpu(steps, vcycles, n=1024):
                 raise gsv.GpuSolveError(drv.gs_last_error().decode())
             out["vcycle_ms"] = round(ms.value / vcycles, 3)
             out["vcycles"] = vcycles
-    out["note"] = ("1024^3 linear 2+2 on one GPU (BASELINE config #5's grid): the denominator of "
-                   "speedup_vs_1gpu_same_grid in the N=8 line (profiles/config5_single_gpu.json holds the "
-                   "committed copy the N=8 run divides by)")
+    out["note"] = ("1024^3 linear 2+2 on one GPU (BASELINE config #5's grid): the N=8 line's strong-scaling "
+                   "denominator (speedup_vs_1gpu_same_grid: rank 0 measures it again in that job; the driver's copy "
+                   "of this object, profiles/config5_single_gpu.json, is its secondary denominator)")
+    return out
+
+
+RCCL_LINK = None
+
+
+def rccl_debug_setup():
+    """N > 1, before any communicator exists: RCCL's INFO log (connection set-up lines only: subsystems INIT,
+    P2P, NET) goes to a per-process file, so that the line can report the transport every peer connection
+    actually took (P2P/IPC over xGMI, P2P/direct pointer, SHM, NET/Socket ...). An explicit NCCL_DEBUG /
+    NCCL_DEBUG_FILE in the environment wins. Returns this process's log path or None."""
+    if os.environ.get("NCCL_DEBUG") and not os.environ.get("NCCL_DEBUG_FILE"):
+        return None  # the user's own logging (to stdout / stderr): nothing to parse
+    os.environ.setdefault("NCCL_DEBUG", "INFO")
+    os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,P2P,NET")
+    os.environ.setdefault("NCCL_DEBUG_FILE", os.path.join(
+        "/tmp", f"gs-rccl-{os.environ.get('MASTER_PORT', '0')}-{os.environ.get('RANK', '0')}-%h-%p.log"))
+    return os.environ["NCCL_DEBUG_FILE"].replace("%h", os.uname().nodename).replace("%p", str(os.getpid()))
+
+
+def rccl_transports(path):
+    """The peer connections in one process's RCCL INFO log: {communicator: {"nranks": n, "peers":
+    {peer: [transport, ...]}}}, e.g. {"0x5f..": {"nranks": 8, "peers": {"1": ["P2P/IPC/read"]}}}."""
+    import re
+    pat = re.compile(r"Channel \d+(?:/\d+)? : (\d+)\[[0-9a-fx]+\] -> (\d+)\[[0-9a-fx]+\] "
+                     r"(?:\[(send|receive)\] )?via (.+?) comm (\S+) nRanks (\d+)")
+    out = {}
+    try:
+        with open(path, errors="replace") as f:
+            for line in f:
+                m = pat.search(line)
+                if not m:
+                    continue
+                src, dst, _, via, comm, nr = m.groups()
+                c = out.setdefault(comm, {"nranks": int(nr), "peers": {}})
+                me = int(os.environ.get("RANK", "0"))
+                peer = dst if int(src) == me else src
+                t = c["peers"].setdefault(peer, [])
+                via = via.strip()
+                if via not in t:
+                    t.append(via)
+    except OSError as e:
+        return {"error": str(e)}
     return out
 
 
@@ -402,14 +461,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    rccl_log = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # RCCL's p2p channels per peer fill the halo communicator's CTA budget (GS_RCCL_CTAS, default 64: four
-        # send/recv per rank, so budget / 4 per peer; gs_comm.cpp). RCCL reads it once per process: before torch's
-        # communicator. An explicit value in the environment wins.
-        ctas = int(os.environ.get("GS_RCCL_CTAS") or 64)
-        if ctas > 0:
-            os.environ.setdefault("NCCL_NCHANNELS_PER_PEER", str(max(1, ctas // 4)))
+        # RCCL's p2p channels per peer fill the halo communicator's CTA budget (gs_rccl_channels_per_peer_hint:
+        # GS_RCCL_CTAS, default 64, over the four send/recv of a rank's grouped exchange). RCCL reads the variable
+        # once per process, so the launcher sets it before torch's communicator; an explicit value wins.
+        cpp = gsv.driver().gs_rccl_channels_per_peer_hint(-1)
+        if cpp > 0:
+            os.environ.setdefault("NCCL_NCHANNELS_PER_PEER", str(cpp))
+        rccl_log = rccl_debug_setup()
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local % max(1, torch.cuda.device_count())))
 
     def barrier():
@@ -434,14 +495,6 @@ def main():
                             postSmoothing=2)
     grid = make_grid(params, rank, world)
     drv = gsv.driver()
-    stream = torch.cuda.ExternalStream(grid.stream())
-
-    def sweeps(k):
-        """k level-0 Jacobi sweeps through the driver (fused pairs where the level allows)."""
-        rc = drv.gs_grid_jacobi(grid.handle, 0, k)
-        if rc:
-            raise gsv.GpuSolveError(drv.gs_last_error().decode())
-
     fused = drv.gs_grid_level_fused(grid.handle, 0) == 1
     # untimed ramp: the requested warm-up sweeps, then more until at least --ramp-ms of smoother launches
     # have run (cold launches run ~25 % slower: BENCH_r01 timed them inside a 7.8 ms window)
@@ -452,32 +505,44 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item() > 0
 
-    def run(k):
-        sweeps(k)
-        grid.sync()
+    def timed_window(g, warmup, ramp_ms, steps):
+        """Untimed warm-up + agreed ramp, then exactly `steps` sweeps bracketed by a barrier and a device
+        synchronisation on both sides, HIP events on the grid's own stream. Returns (max-over-ranks wall s,
+        this rank's wall s, this rank's average pass ms, ramp sweeps, warm-up ms)."""
+        gstream = torch.cuda.ExternalStream(g.stream())
 
-    tw = time.perf_counter()
-    run(a.warmup)
-    ramp, _ = ramp_sweeps(run, max(0.0, a.ramp_ms - (time.perf_counter() - tw) * 1e3), any_rank)
-    warmup_ms = (time.perf_counter() - tw) * 1e3
-    barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    sweeps(a.steps)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    # passes over the level: a fused pair reads v and f once and writes once, like a single sweep
+        def gsweeps(k):
+            if drv.gs_grid_jacobi(g.handle, 0, k):
+                raise gsv.GpuSolveError(drv.gs_last_error().decode())
+
+        def grun(k):
+            gsweeps(k)
+            g.sync()
+
+        tw = time.perf_counter()
+        grun(warmup)
+        rmp, _ = ramp_sweeps(grun, max(0.0, ramp_ms - (time.perf_counter() - tw) * 1e3), any_rank)
+        wms = (time.perf_counter() - tw) * 1e3
+        barrier()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(gstream)
+        gsweeps(steps)
+        ev1.record(gstream)
+        torch.cuda.synchronize()
+        barrier()
+        own = time.perf_counter() - t0
+        # passes over the level: a fused pair reads v and f once and writes once, like a single sweep
+        npass = (steps // 2 + steps % 2) if drv.gs_grid_level_fused(g.handle, 0) == 1 else steps
+        kms = ev0.elapsed_time(ev1) / npass  # average pass duration on the solver's stream
+        t = torch.tensor([own], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item(), own, kms, rmp, wms
+
+    elapsed, own_elapsed, kernel_ms, ramp, warmup_ms = timed_window(grid, a.warmup, a.ramp_ms, a.steps)
     passes = (a.steps // 2 + a.steps % 2) if fused else a.steps
-    kernel_ms = ev0.elapsed_time(ev1) / passes  # average pass duration on the solver's stream
-    own_elapsed = elapsed
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = t.item()
 
     multi = None
     if world > 1:  # per-rank view of the timed window, and the pair's cost without its exchange
@@ -503,7 +568,7 @@ def main():
                  "exchange_ms_per_pair_max": fin(max(gaps)) if gaps else None,
                  "rank_halo_host_us_per_call": [fin(r[3]) for r in rows],
                  "rank_halo_host_us_max": [fin(r[4]) for r in rows],
-                 "rccl_ctas": int(os.environ.get("GS_RCCL_CTAS", "0") or 0) or "default (gs_comm.cpp: 64)",
+                 "rccl_ctas": drv.gs_grid_comm_ctas(grid.handle),
                  "rccl_channels_per_peer": os.environ.get("NCCL_NCHANNELS_PER_PEER"),
                  "note": "rank_pair_ms: the overlapped pair (boundary planes, RCCL ghost exchange, interior) "
                          "per launch on each rank's compute stream; _no_exchange: the same pair on the same "
@@ -513,10 +578,11 @@ def main():
                          "boundary planes, after the next interior is already enqueued when it is still in "
                          "flight"}
 
-    single = ceiling = None
+    single = ceilings = ceiling = None
     if world == 1:
         single = single_sweep_timing(grid, dims, a.steps)
-        ceiling = triad_ceiling(int(dims[0]) * dims[1] * dims[2])
+        ceilings = stream_ceilings(int(dims[0]) * dims[1] * dims[2])
+        ceiling = ceilings["triad"]
 
     lups_per_rank = float(dims[0]) * dims[1] * dims[2] / world
     total_lups = lups_per_rank * a.steps * world
@@ -557,6 +623,58 @@ def main():
             if world == 1:  # the other two level-0 passes of the V-cycle, each alone
                 vc["level0_kernels"] = vcycle_level0_kernels(grid, max(4, min(a.steps, 20)))
 
+    cta_ab = None
+    if world > 1 and a.cta_ab:
+        # the RCCL CTA budget (ncclConfig_t::minCTAs = maxCTAs) on this node's transport: the same timed window
+        # on a fresh grid + communicator per value, interleaved twice; the headline above ran the default
+        cta_ab = {"note": "per value: max-over-ranks ms per sweep of the same timed window on a fresh grid whose "
+                          "RCCL communicator has this CTA budget (two interleaved rounds), and the slowest rank's "
+                          "overlapped pair ms; NCCL_NCHANNELS_PER_PEER is per process: " +
+                          str(os.environ.get("NCCL_NCHANNELS_PER_PEER"))}
+        for rnd in range(2):
+            for c in [int(x) for x in a.cta_ab.split(",") if x.strip()]:
+                err, res = None, None
+                g2 = None
+                try:
+                    g2 = make_grid(params, rank, world, ctas=c)
+                    el, _, kms, _, _ = timed_window(g2, a.warmup, min(a.ramp_ms, 200.0), a.steps)
+                    res = (el, kms)
+                except Exception as e:  # noqa: BLE001 (reported, never required)
+                    err = f"{type(e).__name__}: {e}"
+                finally:
+                    if g2 is not None:
+                        g2.close()
+                if any_rank(err is not None):
+                    cta_ab.setdefault(str(c), []).append({"error": err or "failed on another rank"})
+                    continue
+                km = torch.tensor([res[1]], dtype=torch.float64, device="cuda")
+                dist.all_reduce(km, op=dist.ReduceOp.MAX)
+                cta_ab.setdefault(str(c), []).append({"ms_per_step": round(res[0] / a.steps * 1e3, 4),
+                                                      "pair_ms_max_rank": round(km.item(), 4)})
+
+    transports = None
+    if world > 1 and rccl_log:
+        mine = rccl_transports(rccl_log)
+        allt = [None] * world
+        dist.all_gather_object(allt, mine)
+        # per rank: {peer: [transports]} merged over its communicators (torch's process group and the grids')
+        transports = {"per_rank": [], "log": "NCCL_DEBUG=INFO (subsystems INIT,P2P,NET) to NCCL_DEBUG_FILE, "
+                                             "connection set-up lines 'Channel .. -> .. via <transport>'"}
+        for r, t in enumerate(allt):
+            if not isinstance(t, dict) or "error" in t:
+                transports["per_rank"].append(t)
+                continue
+            peers = {}
+            for c in t.values():
+                for peer, vias in c["peers"].items():
+                    for v in vias:
+                        if v not in peers.setdefault(peer, []):
+                            peers[peer].append(v)
+            transports["per_rank"].append({"rank": r, "communicators": len(t), "peers": peers})
+        kinds = sorted({v.split("/")[0] for t in transports["per_rank"] if isinstance(t, dict) and "peers" in t
+                        for vs in t["peers"].values() for v in vs})
+        transports["kinds"] = kinds
+
     newton = None
     if world == 1 and a.newton_iters > 0:
         newton = newton_timing(n, a.newton_iters)
@@ -571,10 +689,12 @@ def main():
     speedup = None
     if world > 1 and tuple(dims) == (1024, 1024, 1024):
         # strong scaling on 1024^3 (north_star's >= 6x): this line's MLUPS over one GPU's on the same grid.
-        # "value" divides by rank 0's same-job measurement (same node, same run) when it exists, else by
-        # the driver's committed N=1 record; both ratios are reported
-        speedup = {"scaling": "strong", "note": "this line's MLUPS / one GPU's MLUPS on the same 1024^3 grid "
-                                                "(bench.py config5_single_gpu)"}
+        # "value" always divides by rank 0's same-job measurement (same node, same run, same software), so the
+        # ratio means the same in every round; the driver's committed N=1 record is a secondary field only
+        speedup = {"scaling": "strong", "value": None,
+                   "note": "value: this line's MLUPS / rank 0's one-GPU MLUPS on the same 1024^3 grid measured in "
+                           "this job before the slabs were built (bench.py config5_single_gpu); vs_driver_record: "
+                           "the same over the driver's committed N=1 record (secondary)"}
         try:
             with open(CONFIG5_FILE) as f:
                 ref1 = json.load(f)
@@ -587,14 +707,9 @@ def main():
         if c5_same_job and "mlups" in c5_same_job:
             speedup["value"] = round(value / float(c5_same_job["mlups"]), 3)
             speedup["one_gpu_mlups"] = c5_same_job["mlups"]
-            speedup["one_gpu_source"] = "same job: rank 0's GPU, before the slabs were built"
             speedup["one_gpu_pair_kernel_ms"] = c5_same_job.get("pair_kernel_ms")
-        elif "vs_driver_record" in speedup:
-            speedup["value"] = speedup["vs_driver_record"]
-            speedup["one_gpu_mlups"] = speedup["driver_record_mlups"]
-            speedup["one_gpu_source"] = speedup["driver_record_source"]
-            if c5_same_job:
-                speedup["same_job_error"] = c5_same_job.get("error")
+        else:
+            speedup["same_job_error"] = (c5_same_job or {}).get("error", "not measured (--config5 0)")
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_sweeps > 0:
@@ -603,6 +718,17 @@ def main():
         except Exception as e:  # the baseline is reported, never required
             cpu = {"error": str(e)}
 
+    # weak scaling: every N runs n^3 lattice points per rank (512^3 by default); only N = 8's grid is a
+    # BASELINE config (#5: 1024^3); N = 2 / 4 are weak-scaling shapes that keep the N = 1 run's row length
+    scaling = "weak" if int(lups_per_rank) == n ** 3 else "strong"
+    if world == 1:
+        workload = f"{n}^3 linear 7-point fused Jacobi sweep (level 0), BASELINE config #3"
+    elif tuple(dims) == (1024, 1024, 1024):
+        workload = (f"1024^3 linear 7-point fused Jacobi sweep (level 0) = BASELINE config #5's grid, Z-slab over "
+                    f"{world} GPUs ({dims[2] // world} planes per rank)")
+    else:
+        workload = (f"{dims[0]}x{dims[1]}x{dims[2]} linear 7-point fused Jacobi sweep (level 0), Z-slab over {world} "
+                    f"GPUs: a weak-scaling shape with {n}^3 points per rank (not a BASELINE config)")
     if rank == 0:
         line = {
             "metric": "MLUPS (Jacobi smoother) + V-cycle wall-time, 512³ fp64; achieved HBM GB/s %peak",
@@ -615,14 +741,11 @@ def main():
             "warmup_sweeps_total": a.warmup + ramp,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (analytic RHS of the reference, v0 = 0)",
-            "config": {"workload": (f"{n}^3 linear 7-point fused Jacobi sweep (level 0), BASELINE config #3"
-                                    if world == 1 else
-                                    f"{dims[0]}x{dims[1]}x{dims[2]} linear 7-point fused Jacobi sweep (level 0), "
-                                    f"Z-slab over {world} GPUs (BASELINE config #5 at N=8)"),
+            "config": {"workload": workload,
                        "grid": list(dims), "points_per_rank": int(lups_per_rank),
                        "per_rank_slab": [int(dims[0]), int(dims[1]), int(dims[2]) // world],
                        "per_rank_pair_kernel": pair_kernel.split(":")[0],
@@ -631,6 +754,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_GBPS, 4),
                          "frac_of_measured_ceiling": round(achieved / ceiling["gbps"], 4) if ceiling else None,
+                         "frac_of_best_ceiling": (round(achieved / max(c["gbps"] for c in ceilings.values()), 4)
+                                                  if ceilings else None),
+                         "ceiling_note": ("frac_of_measured_ceiling: of the streaming triad (the smoother's 2 reads + "
+                                          "1 write), frac_of_best_ceiling: of the fastest of the triad, copy and "
+                                          "read-only streams measured in this run (measured_ceilings)"),
                          "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
                          "kernel": (pair_kernel + ": two fused sweeps per launch (24 B per point per launch)"
                                     if fused else "k_rb: one sweep per launch (24 B per point per launch)"),
@@ -644,8 +772,11 @@ def main():
                                                  "NOT HBM traffic: the HBM-side figure is `achieved` "
                                                  "(24 B per point per launch / kernel_ms)")},
             "multi_gpu": multi,
+            "rccl_cta_ab": cta_ab,
+            "rccl_transports": transports,
             "single_sweep_kernel": single,
             "measured_ceiling": ceiling,
+            "measured_ceilings": ceilings,
             "vcycle": vc,
             "newton": newton,
             "config5_single_gpu": c5,

@@ -326,6 +326,15 @@ int gs_grid_comm_stats_max(void* grid, double* halo_host_max_ms)
     });
 }
 
+int gs_grid_comm_ctas(void* grid)
+{
+    if (!grid) return -1;
+    const auto* h = static_cast<Handle*>(grid);
+    return h->comm ? h->comm->ctas() : -1;
+}
+
+int gs_rccl_channels_per_peer_hint(int ctas) { return gs::rcclChannelsPerPeerHint(ctas); }
+
 int gs_grid_time_jacobi(void* grid, int level, int warmup, int sweeps, float* ms)
 {
     return guarded([&] {
@@ -434,14 +443,19 @@ int gs_rccl_unique_id(unsigned char uid[128])
 
 void* gs_grid_create_rccl(const gs_params* p, int rank, int nranks, const unsigned char uid[128])
 {
-    if (!p || !uid || rank < 0 || rank >= nranks) {
+    return gs_grid_create_rccl_ctas(p, rank, nranks, uid, -1);
+}
+
+void* gs_grid_create_rccl_ctas(const gs_params* p, int rank, int nranks, const unsigned char uid[128], int ctas)
+{
+    if (!p || !uid || rank < 0 || rank >= nranks || ctas < -1) {
         g_err = "bad arguments";
         return nullptr;
     }
     try {
         auto* h = new Handle;
         try {
-            h->comm = gs::makeRcclComm(rank, nranks, uid);
+            h->comm = gs::makeRcclComm(rank, nranks, uid, ctas);
             h->grid = std::make_unique<gs::HipGridData>(toParams(p), h->comm.get());
         } catch (...) {
             gs_grid_destroy(h);

@@ -44,7 +44,7 @@ void Comm::syncEvent(hipEvent_t e) { hipOk(hipEventSynchronize(e), "hipEventSync
 // group) is settled by polling ncclCommGetAsyncError, and sync() polls it beside hipStreamQuery.
 class RcclComm final : public Comm {
 public:
-    RcclComm(int rank, int nranks, const void* uid) : r_(rank), n_(nranks)
+    RcclComm(int rank, int nranks, const void* uid, int ctas) : r_(rank), n_(nranks), ctas_(ctas)
     {
         const char* inj = std::getenv("GS_COMM_INJECT_ERROR");
         injectAt_ = inj ? std::atol(inj) : 0;
@@ -53,15 +53,14 @@ public:
         std::memcpy(&id, uid, sizeof(id));
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.blocking = 0;
-        if (const int ctas = rcclCtas(); ctas > 0) {
-            cfg.minCTAs = ctas;
-            cfg.maxCTAs = ctas;
-            // the CTA budget caps RCCL's send/recv grid, the p2p channels per peer fill it: a rank's grouped
-            // exchange is four send/recv operations, so ctas / 4 channels per peer give it the whole budget
-            // (the 8-rank rehearsal's bulk launches: 4 workgroups by default, 16 at 16 channels per peer,
-            // profiles/r04/r04i_rccl_grid_cpp16.txt). A value in the environment wins; RCCL reads it once
-            // per process, so bench.py sets it before torch's own communicator exists
-            setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(std::max(1, ctas / 4)).c_str(), 0);
+        if (ctas_ > 0) {
+            // the CTA budget caps RCCL's send/recv grid; the p2p channels per peer fill it (a rank's grouped
+            // exchange is four send/recv operations, so NCCL_NCHANNELS_PER_PEER = ctas / 4 gives it the whole
+            // budget: profiles/r04/r04i_rccl_grid_cpp16.txt). RCCL reads that variable once per process, so
+            // the LAUNCHER sets it before any communicator exists (GpuSolve-hip's main, bench.py;
+            // rcclChannelsPerPeerHint); the library never writes the process environment
+            cfg.minCTAs = ctas_;
+            cfg.maxCTAs = ctas_;
         }
         const ncclResult_t e = ncclCommInitRankConfig(&c_, nranks, id, rank, &cfg);
         if (e != ncclSuccess && e != ncclInProgress) {
@@ -100,12 +99,14 @@ public:
         }
         call(ncclGroupEnd(), "ncclGroupEnd");
         pending_ = true;
+        // counted here, once per exchange, whichever of haloReady / haloSettle completes it
+        pendingInject_ = injectNow();
     }
 
     bool haloReady() override
     {
         if (!pending_) return true;
-        const int a = asyncState(false);
+        const int a = asyncState(pendingInject_);
         if (a > 1) abortAndThrow(std::string("halo exchange: ") + ncclGetErrorString((ncclResult_t)(a - 2)));
         if (a == 0) pending_ = false;
         return !pending_;
@@ -115,8 +116,9 @@ public:
     {
         if (!pending_) return;
         pending_ = false;
-        settle("halo exchange", timeout_);
+        settleAs("halo exchange", timeout_, pendingInject_);
     }
+    int ctas() const override { return ctas_; }
 
     void allgather1(const double* in, double* out, hipStream_t s) override
     {
@@ -187,11 +189,12 @@ private:
     {
         if (e != ncclSuccess && e != ncclInProgress) abortAndThrow(std::string(what) + ": " + ncclGetErrorString(e));
     }
-    // GS_COMM_INJECT_ERROR=k: the k-th settle / sync of this communicator sees ncclInternalError
+    // GS_COMM_INJECT_ERROR=k: the k-th settle / sync of this communicator sees ncclInternalError (an
+    // exchange counts once, when it is issued: haloIssue)
     bool injectNow() { return injectAt_ > 0 && ++calls_ == injectAt_; }
-    void settle(const char* what, double timeoutS)
+    void settle(const char* what, double timeoutS) { settleAs(what, timeoutS, injectNow()); }
+    void settleAs(const char* what, double timeoutS, bool inject)
     {
-        const bool inject = injectNow();
         const std::string err = boundedWait(
             [&] { return asyncState(inject); },
             [](int st) { return std::string(ncclGetErrorString((ncclResult_t)(st - 2))); }, timeoutS, what);
@@ -208,11 +211,12 @@ private:
         throw Error(std::string(what) + " " + msg + " (rank " + std::to_string(r_) + " of " + std::to_string(n_) +
                     "); communicator aborted");
     }
-    int r_, n_;
+    int r_, n_, ctas_;
     ncclComm_t c_ = nullptr;
     long injectAt_ = 0, calls_ = 0;
     double timeout_ = 120.0;
-    bool pending_ = false; // an issued halo exchange not yet settled
+    bool pending_ = false;       // an issued halo exchange not yet settled
+    bool pendingInject_ = false; // GS_COMM_INJECT_ERROR picked that exchange
 };
 
 int rcclCtas()
@@ -224,9 +228,15 @@ int rcclCtas()
     return n;
 }
 
-std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid)
+std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid, int ctas)
 {
-    return std::make_unique<RcclComm>(rank, nranks, uid);
+    return std::make_unique<RcclComm>(rank, nranks, uid, ctas < 0 ? rcclCtas() : ctas);
+}
+
+int rcclChannelsPerPeerHint(int ctas)
+{
+    if (ctas < 0) ctas = rcclCtas();
+    return ctas > 0 ? std::max(1, ctas / 4) : 0;
 }
 
 void rcclUniqueId(void* uid)

@@ -56,6 +56,8 @@ public:
     virtual void sync(hipStream_t s);
     // The same wait for one event (work enqueued on the stream after it is not waited for).
     virtual void syncEvent(hipEvent_t e);
+    // RCCL: the communicator's CTA budget (ncclConfig_t::minCTAs = maxCTAs; 0: RCCL's own); -1 otherwise
+    virtual int ctas() const { return -1; }
 };
 
 // RCCL (NCCL API); uid is the 128-byte ncclUniqueId created by rank 0 (rcclUniqueId) and shared.
@@ -63,12 +65,18 @@ public:
 // call are settled by polling ncclCommGetAsyncError under a deadline (GS_COMM_INIT_TIMEOUT_S, default
 // 300 s; GS_COMM_TIMEOUT_S, default 120 s, also for sync()). On an error or a timeout the communicator
 // is aborted (ncclCommAbort) and gs::Error("RCCL ... (rank r of n)") is thrown. GS_COMM_INJECT_ERROR=k
-// (tests) makes the k-th settle or sync of the communicator see ncclInternalError. GS_RCCL_CTAS=n (read once,
-// at creation) sets ncclConfig_t::minCTAs = maxCTAs = n: the workgroups RCCL's kernels take for a
-// send/recv group, which share the CUs with the interior sweep they overlap (0: RCCL's own choice).
-std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid);
-// the CTA budget makeRcclComm gives a communicator (GS_RCCL_CTAS, else the default below; 0: RCCL's)
+// (tests) makes the k-th settle or sync of the communicator see ncclInternalError (a halo exchange counts
+// once, at its issue). ctas sets ncclConfig_t::minCTAs = maxCTAs: the workgroups RCCL's kernels take for a
+// send/recv group, which share the CUs with the interior sweep they overlap (0: RCCL's own choice; -1: the
+// process default rcclCtas()).
+std::unique_ptr<Comm> makeRcclComm(int rank, int nranks, const void* uid, int ctas = -1);
+// the process default CTA budget (GS_RCCL_CTAS, read once, else 64; 0: RCCL's)
 int rcclCtas();
+// NCCL_NCHANNELS_PER_PEER that gives a grouped exchange (four send/recv per rank) the whole budget `ctas`
+// (-1: rcclCtas()): ctas / 4, 0 for RCCL's default. RCCL reads the variable once per process, so a LAUNCHER
+// (GpuSolve-hip's main, bench.py) sets it, unless already set, before its first communicator; the library
+// itself never writes the environment.
+int rcclChannelsPerPeerHint(int ctas = -1);
 void rcclUniqueId(void* uid);
 
 // The rank-0 id file hand-off (publishUid / awaitUid / uidPath), the bounded wait and the loopback

@@ -279,6 +279,19 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
     check(gs_rhs_init(&levels_[0].geom, levels_[0].f.data(), (int)mode, 1.0 / (gridDim[1] + 1), gamma, s),
           "gs_rhs_init");
     halo(levels_[0], levels_[0].f, s); // the fused pair's first sweep reads f on a ghost plane
+    // GS_METRICS is read by each process, but the per-level clock changes the collective schedule (no
+    // pipelined cycles; the last closing norm is kept): a distributed grid runs it only if EVERY rank has it
+    // on, so that all ranks issue the same exchanges and collectives
+    if (comm_ && comm_->size() > 1) {
+        const double on = clock.on ? 1.0 : 0.0;
+        std::vector<double> all((std::size_t)comm_->size(), 0.0);
+        check((int)hipMemcpyAsync(dNorm_, &on, sizeof(double), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+        comm_->allgather1(dNorm_, dRankSums_, s);
+        check((int)hipMemcpyAsync(all.data(), dRankSums_, sizeof(double) * all.size(), hipMemcpyDeviceToHost, s),
+              "hipMemcpyAsync");
+        comm_->sync(s);
+        for (const double a : all) clock.on = clock.on && a != 0.0;
+    }
     // the fused prolongation pair's edge-column workspaces (column-block rows), one per stream, at their
     // largest size now: proPlanes never reallocates them
     for (int l = 0; l + 1 < nlev; l++) {
@@ -648,7 +661,8 @@ void HipSolver::solve(HipGridData& grid)
     // reads it — no progress print, no history, no per-level clock; NewtonSolver::findError's inner solves — that
     // cycle ends with its up-leg and the norm's pass (a whole level-0 pair at 512^3) is not run
     // (rank-uniform: every rank must run the same exchanges and collectives, so the decision rests on the
-    // grid's printProgress, not on `print`, which only rank 0 has)
+    // grid's printProgress, not on `print`, which only rank 0 has, and on clock.on, which a distributed grid
+    // agrees across ranks at creation)
     const bool lastNormDead = !grid.printProgress && history == nullptr && !grid.clock.on;
     if (spec) {
         runCycles(grid, &pending, grid.maxiter, onNorm, lastNormDead);

@@ -116,6 +116,13 @@ int main(int argc, char* argv[])
     }
     const int world = envInt("WORLD_SIZE", 1), rank = envInt("RANK", 0);
     const bool distributed = world > 1 || envInt("GS_FORCE_RCCL", 0) != 0;
+    if (distributed) {
+        // RCCL's p2p channels per peer fill the communicator's CTA budget (gs_comm.hpp): RCCL reads the
+        // variable once per process, so it is set here, before HIP, RCCL or any thread starts (an explicit
+        // value in the environment wins)
+        if (const int cpp = gs::rcclChannelsPerPeerHint(); cpp > 0)
+            setenv("NCCL_NCHANNELS_PER_PEER", std::to_string(cpp).c_str(), 0);
+    }
     if (rank == 0) std::cout << "Using config file " << std::quoted(path) << '\n';
     if (st == gs::ConfigStatus::InvalidMode) {
         std::cerr << "Invalid mode\n";

@@ -143,6 +143,9 @@ DRIVER_API = {
     "gs_uid_default_path": (C.c_int, [C.c_char_p, C.c_int]),
     "gs_uid_await": (C.c_int, [C.c_char_p, C.c_double, C.POINTER(C.c_ubyte)]),
     "gs_grid_create_rccl": (C.c_void_p, [C.POINTER(gs_params), C.c_int, C.c_int, C.POINTER(C.c_ubyte)]),
+    "gs_grid_create_rccl_ctas": (C.c_void_p, [C.POINTER(gs_params), C.c_int, C.c_int, C.POINTER(C.c_ubyte), C.c_int]),
+    "gs_grid_comm_ctas": (C.c_int, [C.c_void_p]),
+    "gs_rccl_channels_per_peer_hint": (C.c_int, [C.c_int]),
     "gs_zslab_loopback_run": (C.c_int, [C.POINTER(gs_params), C.c_int, i64, C.c_int, C.c_int, dptr, C.c_int,
                                         C.POINTER(C.c_int), dptr]),
     "gs_debug_bounded_wait": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_char_p, C.c_int]),

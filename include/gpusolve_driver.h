@@ -107,6 +107,17 @@ int gs_rccl_unique_id(unsigned char uid[128]);
  * current HIP device). The other gs_grid_* calls then run the distributed solver; fields and
  * levels describe this rank's slab; rank 0 prints. */
 void* gs_grid_create_rccl(const gs_params* p, int rank, int nranks, const unsigned char uid[128]);
+/* The same with an explicit RCCL CTA budget for this grid's communicator (ncclConfig_t::minCTAs = maxCTAs =
+ * ctas: the workgroups RCCL's send/recv kernels take beside the interior sweep; 0: RCCL's own choice; -1: the
+ * process default, GS_RCCL_CTAS or 64). gs_grid_create_rccl is ctas = -1. */
+void* gs_grid_create_rccl_ctas(const gs_params* p, int rank, int nranks, const unsigned char uid[128], int ctas);
+/* The CTA budget of the grid's RCCL communicator; -1 for single-GPU / loopback grids. */
+int gs_grid_comm_ctas(void* grid);
+/* NCCL_NCHANNELS_PER_PEER that gives one grouped ghost exchange (four send/recv per rank) the whole CTA budget
+ * `ctas` (-1: the process default): ctas / 4, 0 for RCCL's default. RCCL reads the variable once per process,
+ * so the LAUNCHER sets it (unless already set) before its first communicator — GpuSolve-hip's main and bench.py
+ * do; the library never writes the process environment. */
+int gs_rccl_channels_per_peer_hint(int ctas);
 /* The id's file hand-off of a multi-process GpuSolve-hip run (one launcher, one node): rank 0
  * publishes (temporary file renamed into place), the others wait up to timeout_s for all 128 bytes.
  * 0 on success, else non-zero with gs_last_error(). */

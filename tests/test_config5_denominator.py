@@ -1,6 +1,7 @@
-"""The N=8 bench line's strong-scaling ratio (speedup_vs_1gpu_same_grid, bench.py) divides by
-profiles/config5_single_gpu.json: that number must be the DRIVER's own N=1 measurement of config #5's
-1024^3 grid (a BENCH_rNN.json record), never a builder box's."""
+"""The N=8 bench line's strong-scaling ratio (speedup_vs_1gpu_same_grid, bench.py): its `value` divides by rank
+0's same-job one-GPU measurement of the 1024^3 grid; the secondary `vs_driver_record` divides by
+profiles/config5_single_gpu.json, which must be the DRIVER's own N=1 measurement of config #5's grid (a
+BENCH_rNN.json record), never a builder box's."""
 import json
 import os
 import re

@@ -1,5 +1,6 @@
-"""Regenerate profiles/config5_single_gpu.json — the one-GPU 1024^3 MLUPS the N=8 bench line divides by
-(speedup_vs_1gpu_same_grid) — from a DRIVER record of bench.py's N=1 run:
+"""Regenerate profiles/config5_single_gpu.json — the driver's one-GPU 1024^3 MLUPS, the SECONDARY denominator of
+the N=8 bench line's strong-scaling ratio (speedup_vs_1gpu_same_grid.vs_driver_record; its `value` divides by
+rank 0's same-job measurement) — from a DRIVER record of bench.py's N=1 run:
     python tools/config5_denominator.py BENCH_r03.json
 The driver's own record is the only accepted source (tests/test_config5_denominator.py checks it)."""
 import json
@@ -30,9 +31,9 @@ def main(path):
            "vcycle_ms": c5.get("vcycle_ms"), "grid": c5["grid"], "source": name, "source_kind": "driver",
            "source_detail": f"the driver's round-end bench ({rec.get('cmd', '?')}, {rec.get('where', '?')}, "
                             f"head {rec.get('head', '?')}): its config5_single_gpu object",
-           "note": "1024^3 linear 2+2 on ONE MI355X: the denominator the N=8 line divides its MLUPS by (strong "
-                   "scaling on BASELINE config #5's grid). Regenerate with tools/config5_denominator.py "
-                   "<BENCH_rNN.json>."}
+           "note": "1024^3 linear 2+2 on ONE MI355X, the driver's record: the secondary denominator of the N=8 "
+                   "line's strong-scaling ratio (speedup_vs_1gpu_same_grid.vs_driver_record; `value` divides by "
+                   "rank 0's same-job measurement). Regenerate with tools/config5_denominator.py <BENCH_rNN.json>."}
     with open(os.path.join(REPO, "profiles", "config5_single_gpu.json"), "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")
