@@ -50,6 +50,10 @@ namespace {
 
 constexpr int WAVE = 64;
 
+// NEWTON's two forms (include/gpusolve_hip.h): GS_NEWTON reads newtonV as w, GS_NEWTON_B reads the precomputed
+// linearisation factor B = gamma (1 + newtonV) exp(newtonV) (gs_newton_bfac) as w. Both carry a w operand.
+constexpr bool newtonish(int m) { return m == GS_NEWTON || m == GS_NEWTON_B; }
+
 // compile-time / run-time booleans for code specialised per wave (BoolC) or selected per use (RtBool)
 template <bool B>
 struct BoolC {
@@ -240,7 +244,7 @@ __device__ __forceinline__ void div_hh_n(const Coef& k, double (&s)[N])
 template <int MODE>
 __device__ __forceinline__ void div_hh_row(const Coef& k, double (&q)[2])
 {
-    if (MODE == GS_NEWTON) {
+    if (newtonish(MODE)) {
         q[0] = div_hh(k, q[0]);
         q[1] = div_hh(k, q[1]);
     } else {
@@ -286,6 +290,8 @@ __device__ __forceinline__ double op_finish(const Coef& k, double q, double c, d
     if (MODE == GS_NEWTON) {
         const double ew = exp(w);
         q += k.gamma * (1 + w) * c * ew;
+    } else if (MODE == GS_NEWTON_B) {
+        q += w * c; // w = B = gamma (1 + newtonV) exp(newtonV)
     } else if (MODE == GS_NONLINEAR) {
         const double ev = exp(c);
         const double nl = k.gamma * c * ev;
@@ -301,15 +307,7 @@ __device__ __forceinline__ double op_value(const Coef& k, double c, double xp, d
 {
     double s = stencil_sum<UN>(k, c, xp, xm, yp, ym, zp, zm);
     s = div_hh(k, s);
-    if (MODE == GS_NEWTON) {
-        const double ew = exp(w);
-        s += k.gamma * (1 + w) * c * ew;
-    } else if (MODE == GS_NONLINEAR) {
-        const double ev = exp(c);
-        const double nl = k.gamma * c * ev;
-        s += nl;
-    }
-    return s;
+    return op_finish<MODE>(k, s, c, w);
 }
 
 // Jacobi point update from the old value and its residual — CpuSolver.cpp:157-171
@@ -317,6 +315,7 @@ template <int MODE>
 __device__ __forceinline__ double jacobi_update(const Coef& k, double v, double r, double w)
 {
     if (MODE == GS_LINEAR) return v + k.omega * (k.alpha * r);
+    if (MODE == GS_NEWTON_B) return v + k.omega * (r / (k.preFac + w)); // preFac + B: the reference's den, bit for bit
     const double u = (MODE == GS_NONLINEAR) ? v : w;
     const double eu = exp(u);
     const double den = k.preFac + k.gamma * (1 + u) * eu;
@@ -336,6 +335,19 @@ __device__ __forceinline__ double newton_update(const Coef& k, double v, double 
 #else
     return v + k.omega * (r / den);
 #endif
+}
+
+// A and E of a point from its w operand: GS_NEWTON_B's w is B itself, so A = B and E = 1 (A * c * E = B * c and
+// preFac + A * E = preFac + B exactly: the products by 1.0 fold away)
+template <int MODE>
+__device__ __forceinline__ double newton_A(const Coef& k, double w)
+{
+    return MODE == GS_NEWTON_B ? w : k.gamma * (1 + w);
+}
+template <int MODE>
+__device__ __forceinline__ double newton_E(double w)
+{
+    return MODE == GS_NEWTON_B ? 1.0 : exp(w);
 }
 
 __device__ __forceinline__ double wave_sum(double x)
@@ -511,7 +523,7 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
         for (int r = 0; r < RY; r++) {
             NL[s][r] = ldv2<ZV, NTV>(v + xl + roff[r + 1] + z2);
             if (KIND != 2 || ADD) FL[s][r] = ld2s<NT>(fin + xl + roff[r + 1] + z1);
-            if (MODE == GS_NEWTON) WL[s][r] = ld2(w + xl + roff[r + 1] + z1);
+            if (newtonish(MODE)) WL[s][r] = ld2(w + xl + roff[r + 1] + z1);
             EL[s][r] = ldv1<ZV>(v + xle + roff[r + 1] + z1);
             ER[s][r] = ldv1<ZV>(v + xre + roff[r + 1] + z1);
         }
@@ -544,12 +556,12 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
                 const double2 zm = P[r], zp = NL[cs][r];
                 const double xm0 = lane_from_left<DPP>(c.y, EL[cs][r]);
                 const double xp1 = lane_from_right<DPP>(c.x, ER[cs][r]);
-                const double wx = (MODE == GS_NEWTON) ? WL[cs][r].x : 0.0;
-                const double wy = (MODE == GS_NEWTON) ? WL[cs][r].y : 0.0;
+                const double wx = newtonish(MODE) ? WL[cs][r].x : 0.0;
+                const double wy = newtonish(MODE) ? WL[cs][r].y : 0.0;
                 // NEWTON sweep: exp(w) once per point, shared by the operator and the update
-                constexpr bool NS = MODE == GS_NEWTON && KIND == 0;
-                const double Ax = NS ? k.gamma * (1 + wx) : 0.0, Ay = NS ? k.gamma * (1 + wy) : 0.0;
-                const double Ex = NS ? exp(wx) : 0.0, Ey = NS ? exp(wy) : 0.0;
+                constexpr bool NS = newtonish(MODE) && KIND == 0;
+                const double Ax = NS ? newton_A<MODE>(k, wx) : 0.0, Ay = NS ? newton_A<MODE>(k, wy) : 0.0;
+                const double Ex = NS ? newton_E<MODE>(wx) : 0.0, Ey = NS ? newton_E<MODE>(wy) : 0.0;
                 const double a0 = NS ? newton_op(div_hh(k, stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x)), c.x, Ax, Ex)
                                      : op_value<MODE, UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx);
                 const double a1 = NS ? newton_op(div_hh(k, stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)), c.y, Ay, Ey)
@@ -793,15 +805,8 @@ __global__ __launch_bounds__(256) void k_generic(Coef k, const double* __restric
         for (int i = 0; i < 7; i++) s += k.s[i] * (v ? v[p + k.off[i]] : 0.0);
         s = div_hh(k, s);
         const double c = v ? v[p] : 0.0;
-        const double wv = (MODE == GS_NEWTON) ? w[p] : 0.0;
-        if (MODE == GS_NEWTON) {
-            const double ew = exp(wv);
-            s += k.gamma * (1 + wv) * c * ew;
-        } else if (MODE == GS_NONLINEAR) {
-            const double ev = exp(c);
-            const double nl = k.gamma * c * ev;
-            s += nl;
-        }
+        const double wv = newtonish(MODE) ? w[p] : 0.0;
+        s = op_finish<MODE>(k, s, c, wv);
         if (KIND == 0) {
             const double r = f[p] - s;
             sumsq = r * r;
@@ -948,7 +953,7 @@ __global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so,
 #pragma unroll
         for (int i = 0; i < RR_NR; i++) {
             F[i] = f[roff[i] + zo];
-            if (MODE == GS_NEWTON) W[i] = w[roff[i] + zo];
+            if (newtonish(MODE)) W[i] = w[roff[i] + zo];
         }
     };
     // r on fine plane fz from the v ring (needs planes fz-1 .. fz+1 staged)
@@ -968,7 +973,7 @@ __global__ __launch_bounds__(RR_T) void k_resrestrict(Coef k, StencilOffsets so,
 #pragma unroll
                 for (int t = 0; t < 7; t++) sum += k.s[t] * lds[rpos[i] + toff[t]];
                 const double c = lds[rpos[i] + coff];
-                const double q = op_finish<MODE>(k, div_hh(k, sum), c, MODE == GS_NEWTON ? W[i] : 0.0);
+                const double q = op_finish<MODE>(k, div_hh(k, sum), c, newtonish(MODE) ? W[i] : 0.0);
                 r = F[i] - q;
             }
             lds[dst + tid + i * RR_T] = r;
@@ -1066,7 +1071,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
                                                          int64_t fldy, int64_t fldz, int cnx, int cny, int cnz, int64_t cldy,
                                                          int64_t cldz, int ZC, int zhi, int rev)
 {
-    static_assert(MODE != GS_NEWTON || !PF, "NEWTON: newtonV rows exceed the budget of the prefetch ring");
+    static_assert(!newtonish(MODE) || !PF, "NEWTON: newtonV rows exceed the budget of the prefetch ring");
     constexpr int RR = 2 * NR + 1; // computed fine rows; v rows 0 .. RR+1 (0 and RR+1: halo rows)
     // wave-edge columns [parity][1 + wave][side][plane * 3 + row] of v, and r at each wave's first fine
     // column [parity][1 + wave][plane * 3 + row]; slots 0 and WX+1 are the zero x-boundary
@@ -1114,7 +1119,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             VB[s][j] = uv ? ld2s<true>(at(v, j + 1, p + 2)) : ld2(at(v, j + 1, p + 2));
             F0[s][j] = uf ? ld2s<true>(at(f, j + 1, p)) : ld2(at(f, j + 1, p));
             F1[s][j] = uf ? ld2s<true>(at(f, j + 1, p + 1)) : ld2(at(f, j + 1, p + 1));
-            if (MODE == GS_NEWTON) {
+            if (newtonish(MODE)) {
                 W0[s][j] = uf ? ld2s<true>(at(w, j + 1, p)) : ld2(at(w, j + 1, p));
                 W1[s][j] = uf ? ld2s<true>(at(w, j + 1, p + 1)) : ld2(at(w, j + 1, p + 1));
             }
@@ -1180,7 +1185,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             const double2 ym = j == 0 ? H[0] : Vc[j - 1], yp = j == RR - 1 ? H[1] : Vc[j + 1];
             const double xm0 = lane_from_left<true>(c.y, CL[j]);
             const double xp1 = lane_from_right<true>(c.x, CR[j]);
-            const double w0 = MODE == GS_NEWTON ? W[j].x : 0.0, w1 = MODE == GS_NEWTON ? W[j].y : 0.0;
+            const double w0 = newtonish(MODE) ? W[j].x : 0.0, w1 = newtonish(MODE) ? W[j].y : 0.0;
             const double a0 = op_value<MODE, UN>(k, c.x, c.y, xm0, yp.x, ym.x, Vp[j].x, Vm[j].x, w0);
             const double a1 = op_value<MODE, UN>(k, c.y, xp1, c.x, yp.y, ym.y, Vp[j].y, Vm[j].y, w1);
             const bool ok = pin && rowc[j + 1];
@@ -1200,7 +1205,7 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             Vq[j] = ld2(at(v, j + 1, p));
             V0[j] = ld2(at(v, j + 1, p + 1));
             Fq[j] = ld2(at(f, j + 1, p));
-            Wq[j] = MODE == GS_NEWTON ? ld2(at(w, j + 1, p)) : make_double2(0.0, 0.0);
+            Wq[j] = newtonish(MODE) ? ld2(at(w, j + 1, p)) : make_double2(0.0, 0.0);
         }
         Hq[0] = ld2(at(v, 0, p));
         Hq[1] = ld2(at(v, RR + 1, p));
@@ -1412,7 +1417,7 @@ __device__ __forceinline__ void tile_sweep(const Coef& k, const double* src, dou
         double nv = c;
         if (gx >= 1 && gx <= nx && gy >= 1 && gy <= ny && gz >= 1 && gz <= nz) {
             const int qf = (i + fo) + fN * ((j + fo) + fN * (l + fo));
-            const double w = MODE == GS_NEWTON ? W[qf] : 0.0;
+            const double w = newtonish(MODE) ? W[qf] : 0.0;
             const double a = op_value<MODE, UN>(k, c, src[q + 1], src[q - 1], src[q + sN], src[q - sN],
                                                  src[q + sN * sN], src[q - sN * sN], w);
             nv = jacobi_update<MODE>(k, c, F[qf] - a, w);
@@ -1448,13 +1453,13 @@ __global__ __launch_bounds__(TS_T) void k_tile_pre_rr(Coef k, const double* __re
                                                       int64_t ldz, int cnx, int cny, int cnz, int64_t cldy, int64_t cldz)
 {
     constexpr int NV = TS + 7, N1 = TS + 5, N2 = TS + 3, NR = TS + 1, NF = TS + 5;
-    constexpr int NW = MODE == GS_NEWTON ? NF : 1;
+    constexpr int NW = newtonish(MODE) ? NF : 1;
     __shared__ double sv[NV * NV * NV], s1[N1 * N1 * N1], s2[N2 * N2 * N2], sf[NF * NF * NF], sw[NW * NW * NW];
     double* sr = sv; // the residual tile reuses v's storage once sweep 1 is done
     const int tx = 1 + TS * (int)blockIdx.x, ty = 1 + TS * (int)blockIdx.y, tz = 1 + TS * (int)blockIdx.z;
     tile_load<ZV>(v, sv, NV, tx - 3, ty - 3, tz - 3, nx, ny, nz, ldy, ldz);
     tile_load<false>(f, sf, NF, tx - 2, ty - 2, tz - 2, nx, ny, nz, ldy, ldz);
-    if (MODE == GS_NEWTON) tile_load<false>(w, sw, NF, tx - 2, ty - 2, tz - 2, nx, ny, nz, ldy, ldz);
+    if (newtonish(MODE)) tile_load<false>(w, sw, NF, tx - 2, ty - 2, tz - 2, nx, ny, nz, ldy, ldz);
     __syncthreads();
     tile_sweep<MODE, UN>(k, sv, s1, N1, sf, sw, NF, 0, tx - 2, ty - 2, tz - 2, nx, ny, nz);
     __syncthreads();
@@ -1477,7 +1482,7 @@ __global__ __launch_bounds__(TS_T) void k_tile_pre_rr(Coef k, const double* __re
             const int qf = (i + 2) + NF * ((j + 2) + NF * (l + 2));
             const double c = s2[q];
             const double a = op_value<MODE, UN>(k, c, s2[q + 1], s2[q - 1], s2[q + N2], s2[q - N2], s2[q + N2 * N2],
-                                                 s2[q - N2 * N2], MODE == GS_NEWTON ? sw[qf] : 0.0);
+                                                 s2[q - N2 * N2], newtonish(MODE) ? sw[qf] : 0.0);
             r = sf[qf] - a;
         }
         sr[t] = r;
@@ -1515,7 +1520,7 @@ __global__ __launch_bounds__(TS_T) void k_tile_pro2(Coef k, const double* __rest
                                                     int64_t ldz, int64_t cldy, int64_t cldz)
 {
     constexpr int NU = TS + 4, N1 = TS + 2, NF = TS + 2;
-    constexpr int NW = MODE == GS_NEWTON ? NF : 1;
+    constexpr int NW = newtonish(MODE) ? NF : 1;
     __shared__ double su[NU * NU * NU], s1[N1 * N1 * N1], sf[NF * NF * NF], sw[NW * NW * NW];
     const int tx = 1 + TS * (int)blockIdx.x, ty = 1 + TS * (int)blockIdx.y, tz = 1 + TS * (int)blockIdx.z;
     for (int t = threadIdx.x; t < NU * NU * NU; t += TS_T) {
@@ -1528,7 +1533,7 @@ __global__ __launch_bounds__(TS_T) void k_tile_pro2(Coef k, const double* __rest
         su[t] = u;
     }
     tile_load<false>(f, sf, NF, tx - 1, ty - 1, tz - 1, nx, ny, nz, ldy, ldz);
-    if (MODE == GS_NEWTON) tile_load<false>(w, sw, NF, tx - 1, ty - 1, tz - 1, nx, ny, nz, ldy, ldz);
+    if (newtonish(MODE)) tile_load<false>(w, sw, NF, tx - 1, ty - 1, tz - 1, nx, ny, nz, ldy, ldz);
     __syncthreads();
     tile_sweep<MODE, UN>(k, su, s1, N1, sf, sw, NF, 0, tx - 1, ty - 1, tz - 1, nx, ny, nz);
     __syncthreads();
@@ -1539,7 +1544,7 @@ __global__ __launch_bounds__(TS_T) void k_tile_pro2(Coef k, const double* __rest
         const int q = (i + 1) + N1 * ((j + 1) + N1 * (l + 1));
         const int qf = (i + 1) + NF * ((j + 1) + NF * (l + 1));
         const double cc = s1[q];
-        const double wv = MODE == GS_NEWTON ? sw[qf] : 0.0;
+        const double wv = newtonish(MODE) ? sw[qf] : 0.0;
         const double a = op_value<MODE, UN>(k, cc, s1[q + 1], s1[q - 1], s1[q + N1], s1[q - N1], s1[q + N1 * N1],
                                              s1[q - N1 * N1], wv);
         vout[gx + (int64_t)gy * ldy + (int64_t)gz * ldz] = jacobi_update<MODE>(k, cc, sf[qf] - a, wv);
@@ -1613,6 +1618,29 @@ __global__ __launch_bounds__(256) void k_copy(double* __restrict__ dst, const do
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (head) dst[0] = src[0];
         if ((n - head) & 1) dst[n - 1] = src[n - 1];
+    }
+}
+
+// GS_NEWTON_B's linearisation factor b = gamma (1 + w) exp(w), evaluated as the reference's Jacobi denominator
+// evaluates its product, (gamma * (1 + w)) * exp(w) (CpuSolver.cpp:166-172): elementwise over n elements,
+// dwordx4 streams when both arrays share an alignment (head: 0 or 1 leading element), else one per thread (-1)
+__device__ __forceinline__ double bfac_of(double gamma, double w) { return gamma * (1 + w) * exp(w); }
+__global__ __launch_bounds__(256) void k_bfac(double* __restrict__ b, const double* __restrict__ w, int64_t n,
+                                              double gamma, int head)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (head < 0) {
+        for (int64_t i = t0; i < n; i += stride) b[i] = bfac_of(gamma, w[i]);
+        return;
+    }
+    const int64_t n2 = (n - head) / 2;
+    for (int64_t i = t0; i < n2; i += stride) {
+        const double2 t = ld2s<true>(w + head + 2 * i);
+        st2s<true>(b + head + 2 * i, bfac_of(gamma, t.x), bfac_of(gamma, t.y));
+    }
+    if (t0 == 0) {
+        if (head) b[0] = bfac_of(gamma, w[0]);
+        if ((n - head) & 1) b[n - 1] = bfac_of(gamma, w[n - 1]);
     }
 }
 
@@ -1700,16 +1728,8 @@ __device__ __forceinline__ double cc_op(const Coef& k, const double* __restrict_
     for (int i = 0; i < 7; i++) s += k.s[i] * (uz ? 0.0 : u[p + k.off[i]]);
     s = div_hh(k, s);
     c = uz ? 0.0 : u[p];
-    wv = (MODE == GS_NEWTON) ? w[p] : 0.0;
-    if (MODE == GS_NEWTON) {
-        const double ew = exp(wv);
-        s += k.gamma * (1 + wv) * c * ew;
-    } else if (MODE == GS_NONLINEAR) {
-        const double ev = exp(c);
-        const double nl = k.gamma * c * ev;
-        s += nl;
-    }
-    return s;
+    wv = newtonish(MODE) ? w[p] : 0.0;
+    return op_finish<MODE>(k, s, c, wv);
 }
 
 template <int MODE>
@@ -1896,7 +1916,7 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
         for (int j = 1; j <= NV; j++) {
             VL[s][j - 1] = ldv2<ZV>(at(v, j, zv));
             FL[s][j - 1] = ld2s<NTF>(at(f, j, z));
-            if (MODE == GS_NEWTON) WL[s][j - 1] = ld2(at(w, j, z));
+            if (newtonish(MODE)) WL[s][j - 1] = ld2(at(w, j, z));
         }
         HL[s][0] = ldv2<ZV>(at(v, 0, z));
         HL[s][1] = ldv2<ZV>(at(v, RY + 3, z));
@@ -1948,8 +1968,8 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
                 const double2 ym = j == 1 ? HL[cs][0] : Vc[j - 2], yp = j == NV ? HL[cs][1] : Vc[j];
                 const double xm0 = lane_from_left<true>(c.y, CL[j - 1]);
                 const double xp1 = lane_from_right<true>(c.x, CR[j - 1]);
-                const double wx0 = (MODE == GS_NEWTON) ? WL[cs][j - 1].x : 0.0;
-                const double wx1 = (MODE == GS_NEWTON) ? WL[cs][j - 1].y : 0.0;
+                const double wx0 = newtonish(MODE) ? WL[cs][j - 1].x : 0.0;
+                const double wx1 = newtonish(MODE) ? WL[cs][j - 1].y : 0.0;
                 const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
                 const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
                 const double r0 = FL[cs][j - 1].x - a0, r1 = FL[cs][j - 1].y - a1;
@@ -1970,8 +1990,8 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
                     const double2 c = V1c[j - 1], ym = V1c[j - 2], yp = V1c[j], zm = V1p[j - 2], zp = V1n[j - 1];
                     const double xm0 = lane_from_left<true>(c.y, CL[NV + j - 2]);
                     const double xp1 = lane_from_right<true>(c.x, CR[NV + j - 2]);
-                    const double wx0 = (MODE == GS_NEWTON) ? Wprev[j - 2].x : 0.0;
-                    const double wx1 = (MODE == GS_NEWTON) ? Wprev[j - 2].y : 0.0;
+                    const double wx0 = newtonish(MODE) ? Wprev[j - 2].x : 0.0;
+                    const double wx1 = newtonish(MODE) ? Wprev[j - 2].y : 0.0;
                     const double a0 = op_value<MODE>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, wx0);
                     const double a1 = op_value<MODE>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, wx1);
                     const double o0 = jacobi_update<MODE>(k, c.x, Fprev[j - 2].x - a0, wx0);
@@ -1988,7 +2008,7 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
             for (int j = 0; j < RY; j++) {
                 V1p[j] = V1c[j + 1];
                 Fprev[j] = FL[cs][j + 1];
-                if (MODE == GS_NEWTON) Wprev[j] = WL[cs][j + 1];
+                if (newtonish(MODE)) Wprev[j] = WL[cs][j + 1];
             }
 #pragma unroll
             for (int j = 0; j < NV; j++) {
@@ -2044,7 +2064,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     static_assert(PRO == 0 || (SPEC && !ZV && RY % 2 == 0), "fused prolongation: per-wave code, even RY");
     static_assert(!TS || (PRO == 0 && !XH), "timestamps: plain pairs (es carries the buffer)");
     const uint64_t tstart = TS ? wall_clock64() : 0;
-    static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR || MODE == GS_NEWTON) && RY + 2 <= WAVE),
+    static_assert(!XH || ((PRO == 0 || MODE == GS_LINEAR || newtonish(MODE)) && RY + 2 <= WAVE),
                   "column blocks: every pair, LINEAR / NEWTON prolongation pairs");
     constexpr int NV = RY + 1;  // sweep-1 rows j = 0..RY
     constexpr int NE = NV + RY; // x-edge values per wave side: v rows 0..RY, sweep-1 rows 1..RY
@@ -2129,14 +2149,15 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // NEWTON with the fused prolongation: no room for Aprev / Eprev, so sweep 2 recomputes A from the
     // newtonV rows at z-1 and reads E = exp(w) from LDS (same expressions, same values)
     // NEWTON column blocks (XH) likewise: their edge-column state leaves no room for Aprev / Eprev / Fprev
-    constexpr bool RECOMP = MODE == GS_NEWTON && (PRO != 0 || XH);
+    constexpr bool RECOMP = newtonish(MODE) && (PRO != 0 || XH);
+    constexpr bool ELDS = RECOMP && MODE == GS_NEWTON; // E in LDS (GS_NEWTON_B: E = 1, A = B from wprev_l)
     constexpr bool WLDS = RECOMP && PRO != 0; // the coarse X-pass rows in LDS (prolongation pairs)
     // (Wprev, Fprev: sweep 2's newtonV / f rows at z-1, in LDS like the coarse rows below)
     __shared__ double2 wprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
     __shared__ double2 fprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
     // exp(w) of sweep 1's own rows, by plane parity: sweep 2 reads the previous plane's (each lane its own
     // values, no barrier) instead of evaluating exp a second time (+32 KB: 148 KB, one block per CU as before)
-    __shared__ double2 eprev_l[RECOMP ? 2 : 1][RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
+    __shared__ double2 eprev_l[ELDS ? 2 : 1][ELDS ? RY : 1][ELDS ? 2 * WXMAX : 1][ELDS ? WAVE : 1];
 #pragma unroll
     for (int j = 0; j < NV; j++) V1c[j] = make_double2(0.0, 0.0);
 #pragma unroll
@@ -2147,7 +2168,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // (0 v or the corrected v at plane z+1, 1 / 2 its x-neighbours at plane z, 3 f, 4 newtonV) of local row r,
     // and the edge computation takes them with lane permutes. The prefetch distance stays one step, at 2
     // VGPRs per slot instead of 10 (the NEWTON column-block pairs spilled with five slot arrays)
-    constexpr bool EPK = XH && MODE == GS_NEWTON;
+    constexpr bool EPK = XH && newtonish(MODE);
     constexpr int NES = (XH && !EPK) ? NS : 1;
     double EA[NES], EXm[NES], EXp[NES], EF[NES], EP = 0.0, EC = 0.0, ES1c = 0.0;
     double EPS[EPK ? NS : 1]; // EPK: the packed slots
@@ -2194,7 +2215,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         for (int j = 0; j < NV; j++) {
             VL[s][j] = ldv2<ZV>(at(v, j, zv));
             FL[s][j] = ld2s<NTF>(at(f, j, z));
-            if (MODE == GS_NEWTON) WL[s][j] = ld2(at(w, j, z));
+            if (newtonish(MODE)) WL[s][j] = ld2(at(w, j, z));
 #ifdef GS_EXP_EFIELD
             if (MODE == GS_NEWTON) XL[s][j] = ld2(at(w, j, z) + k.efoff);
 #endif
@@ -2221,7 +2242,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // RBDPP (NEWTON column blocks, where every VGPR counts): b = c(cx+1) is the next lane's a (one DPP shift; lane
     // 63 takes the next wave's first column as a wave-uniform load), so a is clamped to cnx+1 instead of cnx —
     // the same b for every lane, a different a only for lanes past the row's end, which correct nothing
-    constexpr bool RBDPP = MODE == GS_NEWTON && XH && PRO == 1;
+    constexpr bool RBDPP = newtonish(MODE) && XH && PRO == 1;
     const int cxl = min(x >> 1, max(RBDPP ? cnx + 1 : cnx, 0)); // the lane's coarse column (fine pair x odd, x+1 even)
     const int cxe = min((x0 >> 1) + WAVE, cnx + 1);             // RBDPP: lane 63's b column
     const int cyb = mir ? ((y0 - 1) >> 1) + RY / 2 : ((y0 - 1) >> 1) - 1;
@@ -2421,8 +2442,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                                 return (ZV && k.zq) ? 0.0 : div_hh(k, stencil_sum<UN>(k, c, EXp[cs], EXm[cs], yp, ym, EA[cs], EP));
                             }
                         };
-                        if constexpr (MODE == GS_NEWTON) { // the interior rows' NEWTON expressions, exp once
-                            const double we = efld(cs, 4), A = k.gamma * (1 + we), E = exp(we);
+                        if constexpr (newtonish(MODE)) { // the interior rows' NEWTON expressions, exp once
+                            const double we = efld(cs, 4), A = newton_A<MODE>(k, we), E = newton_E<MODE>(we);
                             const double a = newton_op(qe(), c, A, E);
                             nv = newton_update(k, c, efld(cs, 3) - a, A, E);
                         } else {
@@ -2458,19 +2479,19 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         div_hh_row<MODE>(k, q);
                     }
                     double a0, a1, n0, n1;
-                    if constexpr (MODE == GS_NEWTON) {
+                    if constexpr (newtonish(MODE)) {
                         const double2 wv = WL[cs][j];
-                        const double2 A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
+                        const double2 A = make_double2(newton_A<MODE>(k, wv.x), newton_A<MODE>(k, wv.y));
 #ifdef GS_EXP_EFIELD
                         const double2 E = XL[cs][j];
 #else
-                        const double2 E = make_double2(exp(wv.x), exp(wv.y));
+                        const double2 E = make_double2(newton_E<MODE>(wv.x), newton_E<MODE>(wv.y));
 #endif
                         if (!RECOMP && j >= 1) {
                             Acur[j - 1] = A;
                             Ecur[j - 1] = E;
                         }
-                        if (RECOMP && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
+                        if (ELDS && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
                         a0 = newton_op(q[0], c.x, A.x, E.x);
                         a1 = newton_op(q[1], c.y, A.y, E.y);
                         n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
@@ -2503,12 +2524,13 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                                        stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y)};
                         div_hh_row<MODE>(k, q);
                         double o0, o1;
-                        if constexpr (MODE == GS_NEWTON) {
+                        if constexpr (newtonish(MODE)) {
                             double2 A, E;
                             if constexpr (RECOMP) {
                                 const double2 wv = wprev_l[j - 1][wx + WX * wy][lane];
-                                A = make_double2(k.gamma * (1 + wv.x), k.gamma * (1 + wv.y));
-                                E = eprev_l[ph ^ 1][j - 1][wx + WX * wy][lane];
+                                A = make_double2(newton_A<MODE>(k, wv.x), newton_A<MODE>(k, wv.y));
+                                if constexpr (ELDS) E = eprev_l[ph ^ 1][j - 1][wx + WX * wy][lane];
+                                else E = make_double2(1.0, 1.0);
                             } else {
                                 A = Aprev[j - 1];
                                 E = Eprev[j - 1];
@@ -2546,7 +2568,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                 if constexpr (RECOMP) {
                     wprev_l[j - 1][wx + WX * wy][lane] = WL[cs][j];
                     fprev_l[j - 1][wx + WX * wy][lane] = FL[cs][j];
-                } else if (MODE == GS_NEWTON) {
+                } else if (newtonish(MODE)) {
                     Aprev[j - 1] = Acur[j - 1];
                     Eprev[j - 1] = Ecur[j - 1];
                 }
@@ -2712,10 +2734,10 @@ int tb2_plan(const gs_stencil* S, const gs_level* L, int* zc, dim3* grid, dim3* 
     // 166-167 ms (profiles/r04/r04i_newton_1023.txt); GS_NEWTON_XH=0 keeps k_tb2 for the plain pairs (A/B).
     // NEWTON prolongation pairs (pro) have no k_tb2 form
     const bool colb = !two && xh_enabled() && L->nx <= (int64_t)1 << 20 &&
-                      (mode != GS_NEWTON || pro || kKnobs.newtonXh || L->nx > 2 * WAVE * TB_WX_B);
+                      (!newtonish(mode) || pro || kKnobs.newtonXh || L->nx > 2 * WAVE * TB_WX_B);
     if (!two && !colb && L->nx > 2 * WAVE * TB_WX_B) return 0;
     const int64_t nh = colb ? (L->nx + 2 * WAVE * TBY_WX - 1) / (2 * WAVE * TBY_WX) : 1;
-    const int rows = (two || colb) ? 2 * (mode == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block
+    const int rows = (two || colb) ? 2 * (newtonish(mode) ? TBY_RY_NEWTON : TBY_RY) : TB_RY_B; // output rows per block
     const int64_t tiles = (L->ny + rows - 1) / rows * nh;
     // the block count (of 4-plane chunks) from which the pair is the level's smoother: 128 takes 64^3
     // (256 blocks: ZV pair + prolongation pair 23.5 us vs 4 one-point sweeps + prolongation 24.7 us) and
@@ -2832,7 +2854,7 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
     // v == NULL: the zero iterate (sweeps only, not in NONLINEAR mode, whose coarse iterates are
     // restrictions, never zero)
     if (!S || bad_level(L) || !valid_stencil(S) || (!v && (KIND != 0 || mode == GS_NONLINEAR))) return GS_EINVAL;
-    if (mode < GS_LINEAR || mode > GS_NEWTON) return GS_EINVAL;
+    if (mode < GS_LINEAR || mode > GS_NEWTON_B || (KIND == 2 && mode != GS_NONLINEAR)) return GS_EINVAL;
     if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;
     const Coef k = make_coef(S, L, omega, gamma);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
@@ -2844,18 +2866,24 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
         if (!v) {
             if constexpr (KIND == 0 && !ADD) {
                 if (mode == GS_LINEAR) GS_RB(GS_LINEAR, true);
+                else if (mode == GS_NEWTON_B) GS_RB(GS_NEWTON_B, true);
                 else GS_RB(GS_NEWTON, true);
             }
+        } else if constexpr (KIND == 2) {
+            GS_RB(GS_NONLINEAR, false); // the FAS operator (NONLINEAR only)
         } else if (mode == GS_LINEAR) GS_RB(GS_LINEAR, false);
         else if (mode == GS_NONLINEAR) GS_RB(GS_NONLINEAR, false);
+        else if (mode == GS_NEWTON_B) GS_RB(GS_NEWTON_B, false);
         else GS_RB(GS_NEWTON, false);
 #undef GS_RB
 #undef GS_RBU
     } else {
         const dim3 g = plan.grid, b(GN_BX, GN_BY);
 #define GS_GN(M) hipLaunchKernelGGL((k_generic<M, KIND, ADD>), g, b, 0, st, k, v, f, w, out, partials, nx, ny, nz, L->ldy, L->ldz)
-        if (mode == GS_LINEAR) GS_GN(GS_LINEAR);
+        if constexpr (KIND == 2) GS_GN(GS_NONLINEAR);
+        else if (mode == GS_LINEAR) GS_GN(GS_LINEAR);
         else if (mode == GS_NONLINEAR) GS_GN(GS_NONLINEAR);
+        else if (mode == GS_NEWTON_B) GS_GN(GS_NEWTON_B);
         else GS_GN(GS_NEWTON);
 #undef GS_GN
     }

@@ -175,6 +175,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         sw.zeroGuess = !on("GS_NO_ZERO_GUESS");
         sw.pipeline = !on("GS_NO_PIPELINE");
         sw.newtonFusedUpdate = !on("GS_NO_NEWTON_FUSED_UPDATE");
+        sw.newtonB = !on("GS_NO_NEWTON_B");
         if (const char* e = std::getenv("GS_NEWTON_PRO_POINTS")) sw.newtonProPoints = std::strtoll(e, nullptr, 10);
         if (const char* e = std::getenv("GS_TILE_POINTS")) sw.tilePoints = std::strtoll(e, nullptr, 10);
         if (const char* e = std::getenv("GS_HALO_ORDER")) sw.haloOrder = std::atoi(e);
@@ -217,6 +218,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         if (l + 1 < nlev) L.r = DeviceField(nx, ny, nz, s, dry); // restriction source
         if (mode == NONLINEAR && l > 0) L.restV = DeviceField(nx, ny, nz, s, dry);
         if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s, dry);
+        if (mode == NEWTON && sw.newtonB) L.bfac = DeviceField(nx, ny, nz, s, dry);
         if (mode == NEWTON && l == 1 && nlev >= 3 && !L.distributed) L.newtonVNext = DeviceField(nx, ny, nz, s, dry);
         L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), L.lo - 1, L.h};
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
@@ -336,6 +338,7 @@ const char* HipGridData::fieldName(const LevelData& L, const DeviceField& f)
     if (&f == &L.r) return "r";
     if (&f == &L.restV) return "restV";
     if (&f == &L.newtonV) return "newtonV";
+    if (&f == &L.bfac) return "bfac";
     return "?";
 }
 
@@ -475,8 +478,8 @@ int64_t sweepPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64
         g.rec("sweep", {{"L", (long long)g.levelIndex(L)}, {"z1", z1}, {"z2", z2}, {"vzero", L.vZero}, {"norm", partials != nullptr}});
         return partials ? 1 : 0;
     }
-    check(gs_jacobi_sweep_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.vZero ? nullptr : L.v.data() + off,
-                               L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
+    check(gs_jacobi_sweep_norm(&g.stencilAbi, &sub, g.kmode(), g.omega, g.gamma, L.vZero ? nullptr : L.v.data() + off,
+                               L.vAlt.data() + off, L.f.data() + off, g.wOf(L) ? g.wOf(L) + off : nullptr,
                                partials, s),
           "gs_jacobi_sweep");
     return partials ? gs_residual_num_partials(&g.stencilAbi, &sub) : 0;
@@ -501,8 +504,8 @@ int64_t pairPlanes(HipGridData& g, HipGridData::LevelData& L, int64_t z1, int64_
                        {"vzero", L.vZero}, {"norm", partials != nullptr}});
         return partials ? 1 : 0;
     }
-    check(gs_jacobi_sweep2_norm(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, L.vZero ? nullptr : L.v.data() + off,
-                                L.vAlt.data() + off, L.f.data() + off, L.newtonV ? L.newtonV.data() + off : nullptr,
+    check(gs_jacobi_sweep2_norm(&g.stencilAbi, &sub, g.kmode(), g.omega, g.gamma, L.vZero ? nullptr : L.v.data() + off,
+                                L.vAlt.data() + off, L.f.data() + off, g.wOf(L) ? g.wOf(L) + off : nullptr,
                                 zlo, zhi, partials, s),
           "gs_jacobi_sweep2");
     return partials ? gs_jacobi_sweep2_num_partials(&g.stencilAbi, &sub, (int)g.mode) : 0;
@@ -535,9 +538,9 @@ void proPlanes(HipGridData& g, HipGridData::LevelData& F, HipGridData::LevelData
     DeviceBuf& wb = F.proWs[s == g.stream() ? 0 : 1];
     if (wsn > wb.size()) throw Error("gs_jacobi_sweep2_prolong: workspace not sized at grid creation");
     double* ws = wsn > 0 ? wb.get(wsn) : nullptr;
-    check(gs_jacobi_sweep2_prolong_ws(&g.stencilAbi, &sub, (int)g.mode, g.omega, g.gamma, F.v.data() + off,
+    check(gs_jacobi_sweep2_prolong_ws(&g.stencilAbi, &sub, g.kmode(), g.omega, g.gamma, F.v.data() + off,
                                       C.v.data(), nullptr, &C.geom, F.vAlt.data() + off, F.f.data() + off,
-                                      F.newtonV ? F.newtonV.data() + off : nullptr, zlo, zhi, ws, wsn, s),
+                                      g.wOf(F) ? g.wOf(F) + off : nullptr, zlo, zhi, ws, wsn, s),
           "gs_jacobi_sweep2_prolong");
 }
 
@@ -716,8 +719,8 @@ double HipSolver::compResidual(HipGridData& grid, std::size_t l, bool storeR, bo
     if (grid.trace)
         grid.rec("residual", {{"L", (long long)l}, {"store", storeR}, {"norm", norm}});
     else
-        check(gs_residual(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(), L.f.data(),
-                          L.newtonV ? L.newtonV.data() : nullptr, storeR ? L.r.data() : nullptr,
+        check(gs_residual(&grid.stencilAbi, &L.geom, grid.kmode(), grid.gamma, L.v.data(), L.f.data(),
+                          grid.wOf(L), storeR ? L.r.data() : nullptr,
                           norm ? grid.partials() : nullptr, s),
               "gs_residual");
     if (storeR) grid.halo(L, L.r, s);
@@ -871,13 +874,13 @@ void HipSolver::coarseCycle(HipGridData& grid, std::size_t from)
     for (int j = 0; j < n; j++) {
         auto& L = grid.getLevel(from + j);
         lv[j] = gs_coarse_level{L.v.data(), L.vAlt.data(), L.f.data(), L.r ? L.r.data() : nullptr,
-                                L.restV ? L.restV.data() : nullptr, L.newtonV ? L.newtonV.data() : nullptr,
+                                L.restV ? L.restV.data() : nullptr, const_cast<double*>(grid.wOf(L)),
                                 L.geom, j == 0 ? (L.vZero ? 1 : 0) : (grid.mode != GridParams::NONLINEAR ? 1 : 0)};
     }
     if (grid.trace)
         grid.rec("coarse", {{"from", (long long)from}, {"vzero", lv[0].v_zero}});
     else
-        check(gs_coarse_cycle(&grid.stencilAbi, lv, n, (int)grid.mode, grid.omega, grid.gamma, (int)grid.preSmoothing,
+        check(gs_coarse_cycle(&grid.stencilAbi, lv, n, grid.kmode(), grid.omega, grid.gamma, (int)grid.preSmoothing,
                               (int)grid.postSmoothing, grid.stream()),
               "gs_coarse_cycle");
     const bool odd = ((grid.preSmoothing + grid.postSmoothing) & 1) != 0; // every level swept pre+post times
@@ -951,9 +954,9 @@ void HipSolver::upLeg(HipGridData& grid, std::size_t i)
         if (grid.trace)
             grid.rec("tiledpro", {{"L", (long long)(i - 1)}});
         else
-            check(gs_prolong_smooth2_tiled(&grid.stencilAbi, &F.geom, (int)grid.mode, grid.omega, grid.gamma,
+            check(gs_prolong_smooth2_tiled(&grid.stencilAbi, &F.geom, grid.kmode(), grid.omega, grid.gamma,
                                            F.v.data(), C.v.data(), &C.geom, F.vAlt.data(), F.f.data(),
-                                           F.newtonV ? F.newtonV.data() : nullptr, s),
+                                           grid.wOf(F), s),
                   "gs_prolong_smooth2_tiled");
         F.v.swap(F.vAlt);
         if (grid.trace) grid.rec("swap", {{"L", (long long)(i - 1)}});
@@ -1032,9 +1035,9 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
             if (grid.trace)
                 grid.rec("tiledpre", {{"L", (long long)i}, {"vzero", L.vZero}});
             else
-                check(gs_smooth2_restrict_tiled(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.omega, grid.gamma,
+                check(gs_smooth2_restrict_tiled(&grid.stencilAbi, &L.geom, grid.kmode(), grid.omega, grid.gamma,
                                                 L.vZero ? nullptr : L.v.data(), L.vAlt.data(), L.f.data(),
-                                                L.newtonV ? L.newtonV.data() : nullptr, C.f.data(), &C.geom, s),
+                                                grid.wOf(L), C.f.data(), &C.geom, s),
                       "gs_smooth2_restrict_tiled");
             L.v.swap(L.vAlt);
             if (grid.trace) grid.rec("swap", {{"L", (long long)i}});
@@ -1048,12 +1051,12 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
         bool fused = false;
         if (grid.sw.fusedRR) {
             materialize(grid, i);
-            const double* w = L.newtonV ? L.newtonV.data() : nullptr;
+            const double* w = grid.wOf(L);
             if (!(L.distributed && grid.nranks() > 1)) {
                 if (grid.trace)
                     grid.rec("resrestrict", {{"L", (long long)i}, {"c1", 1}, {"c2", C.geom.nz}, {"zhi", 0}});
                 else
-                    check(gs_residual_restrict(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma, L.v.data(),
+                    check(gs_residual_restrict(&grid.stencilAbi, &L.geom, grid.kmode(), grid.gamma, L.v.data(),
                                                L.f.data(), w, C.f.data(), nullptr, &C.geom, s),
                           "gs_residual_restrict");
                 fused = true;
@@ -1075,7 +1078,7 @@ void HipSolver::cycleDown(HipGridData& grid, int* pending)
                     if (cg.nz > 0 && grid.trace)
                         grid.rec("resrestrict", {{"L", (long long)i}, {"c1", cg.z0 + 1}, {"c2", cg.z0 + cg.nz}, {"zhi", zhi}});
                     else if (cg.nz > 0)
-                        check(gs_residual_restrict_slab(&grid.stencilAbi, &L.geom, (int)grid.mode, grid.gamma,
+                        check(gs_residual_restrict_slab(&grid.stencilAbi, &L.geom, grid.kmode(), grid.gamma,
                                                         L.v.data(), L.f.data(), w, C.f.data() + off, nullptr, &cg,
                                                         zhi, s),
                               "gs_residual_restrict_slab");
@@ -1305,6 +1308,17 @@ bool NewtonSolver::findError(HipGridData& grid)
         }
         HipSolver::restrict(grid, grid.getLevel(i - 1).newtonV, i - 1, grid.getLevel(i).newtonV);
     }
+    // GS_NEWTON_B: every level's factor B = gamma (1 + w) exp(w) of the newtonV the inner solve linearises at
+    // (whole local arrays, ghost planes included: each level's newtonV ghosts are current here), so its ten
+    // V-cycles evaluate no exp(newtonV) (include/gpusolve_hip.h)
+    if (grid.sw.newtonB) {
+        for (std::size_t i = 0; i < grid.numLevels(); i++) {
+            auto& L = grid.getLevel(i);
+            if (grid.trace) grid.rec("bfac", {{"L", (long long)i}});
+            else check(gs_newton_bfac(&L.geom, grid.gamma, L.newtonV.data(), L.bfac.data(), grid.stream()), "gs_newton_bfac");
+        }
+        grid.newtonB_ = true;
+    }
 
     const bool keepPrint = grid.printProgress;
     grid.printProgress = false;
@@ -1314,7 +1328,13 @@ bool NewtonSolver::findError(HipGridData& grid)
     grid.tol = 0.1;
     std::vector<double>* keep = HipSolver::history;
     HipSolver::history = nullptr;
-    HipSolver::solve(grid);
+    try {
+        HipSolver::solve(grid);
+    } catch (...) {
+        grid.newtonB_ = false;
+        throw;
+    }
+    grid.newtonB_ = false; // newtonV changes next (newtonV += v): the factors are stale from here on
     HipSolver::history = keep;
     grid.printProgress = keepPrint;
     grid.maxiter = origIter;

@@ -103,6 +103,8 @@ public:
                                  // in by the next findError — until then newtonV keeps the reference's value
         DeviceField f;       // right-hand side
         DeviceField r;       // residual (restriction source)
+        DeviceField bfac;    // NEWTON (GS_NEWTON_B): B = gamma (1 + newtonV) exp(newtonV) of the inner solve's
+                             // linearisation point, set by findError (gs_newton_bfac)
         std::array<std::size_t, 3> levelDim{}; // global interior extents
         double h = 0.0;
         gs_level geom{};     // kernel-side geometry of the stored array (slab or full level)
@@ -149,6 +151,8 @@ public:
         bool zeroGuess = true;     // GS_NO_ZERO_GUESS: coarse v = 0 stored instead of flagged
         bool pipeline = true;      // GS_NO_PIPELINE: no overlap of the norm wait with the next cycle
         bool newtonFusedUpdate = true; // GS_NO_NEWTON_FUSED_UPDATE: newtonV += v, then compF (two passes)
+        bool newtonB = true; // GS_NO_NEWTON_B: inner Newton solves read newtonV (GS_NEWTON) instead of the
+                             // precomputed factor B (GS_NEWTON_B: exp(newtonV) once per point and Newton iteration)
         int64_t tilePoints = (int64_t)1 << 18; // GS_TILE_POINTS: levels of at most this many points (replicated,
                                                // LINEAR) run the tiled one-launch down/up-leg steps; 0 = off
         int64_t newtonProPoints = (int64_t)1 << 24; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
@@ -178,6 +182,13 @@ public:
     double readNormEnd();
     void sync();       // stream sync (bounded, error-polling when distributed over RCCL)
 
+    // the mode and the w operand the V-cycle's kernels take: GS_NEWTON_B and B while findError's inner solve runs
+    // with the factor fields current (newtonB_), else the grid's mode and newtonV (reference expressions)
+    int kmode() const { return newtonB_ ? GS_NEWTON_B : (int)mode; }
+    const double* wOf(const LevelData& L) const
+    {
+        return newtonB_ ? L.bfac.data() : (L.newtonV ? L.newtonV.data() : nullptr);
+    }
     // ghost planes of a distributed level's field (no-op otherwise); depth 2 where possible for
     // iterate fields (the fused pair reads two ghost planes of v)
     void halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth = 1);
@@ -214,6 +225,7 @@ private:
     bool haloPending_ = false; // an exchange issued by haloIssue, not settled
     friend class NewtonSolver;
     bool newtonR1_ = false;    // level 1's newtonVNext holds R(level 0's newtonV) (gs_newton_F_update_restrict)
+    bool newtonB_ = false;     // every level's bfac holds B of its current newtonV (set for the inner solve)
     double haloCurMs_ = 0.0;   // host ms spent on that exchange so far
     double traceNorm();
     friend class HipSolver;

@@ -40,7 +40,7 @@ int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, doubl
                          const double* v_in, double* v_out, const double* f, const double* w, double* partials,
                          hipStream_t st)
 {
-    if (!v_out || !f || v_in == v_out || (mode == GS_NEWTON && !w)) return GS_EINVAL;
+    if (!v_out || !f || v_in == v_out || (newtonish(mode) && !w)) return GS_EINVAL;
     if (partials && L && (L->nx == 0 || L->ny == 0 || L->nz == 0))
         return (int)hipMemsetAsync(partials, 0, sizeof(double), st);
     return launch_pass<0, false>(S, L, mode, omega, gamma, v_in, f, w, v_out, partials, st);
@@ -50,7 +50,7 @@ int gs_jacobi_sweep2_supported_mode(const gs_stencil* S, const gs_level* L, int 
 {
     int zc;
     dim3 g, b;
-    if (mode < GS_LINEAR || mode > GS_NEWTON) return 0;
+    if (mode < GS_LINEAR || mode > GS_NEWTON_B) return 0;
     return (!bad_level(L) && valid_stencil(S)) ? tb2_plan(S, L, &zc, &g, &b, nullptr, mode) : 0;
 }
 
@@ -98,7 +98,7 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     dim3 g, b;
     bool y2 = false, xh = false;
     if (!S || bad_level(L) || !valid_stencil(S) || !v_out || !f || v_in == v_out || (!v_in && mode == GS_NONLINEAR) ||
-        (mode == GS_NEWTON && !w) || mode < GS_LINEAR || mode > GS_NEWTON ||
+        (newtonish(mode) && !w) || mode < GS_LINEAR || mode > GS_NEWTON_B ||
         !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh))
         return GS_EINVAL;
     const Coef k = make_coef(S, L, omega, gamma);
@@ -113,9 +113,9 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     // next, last planes first) store through the caches instead of non-temporally (A/B)
     const bool cached = partials && kKnobs.specCached;
 #define GS_TBY2(M, Z, U, P) do { \
-        if (refit && M == GS_LINEAR) refit_chunks(&k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, P, false, U>, (int)(b.x * b.y * b.z), nz, 4, 64, true, 2.0, &zc, &g); \
-        if (cached) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, false, false, Z, true, 0, P, false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr); \
-        else hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, P, false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr); } while (0)
+        if (refit && M == GS_LINEAR) refit_chunks(&k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, P, false, U>, (int)(b.x * b.y * b.z), nz, 4, 64, true, 2.0, &zc, &g); \
+        if (cached) hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, TBY_WX, false, false, Z, true, 0, P, false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr); \
+        else hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, TBY_WX, true, false, Z, true, 0, P, false, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr); } while (0)
 #define GS_TBY1(M, Z, U) GS_TBY2(M, Z, U, tby_pfd(M))
 #define GS_TBY(M, Z) do { if (k.unit) GS_TBY1(M, Z, true); else GS_TBY1(M, Z, false); } while (0)
 #define GS_TBX1(M, Z, P, U) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr)
@@ -127,6 +127,8 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
             else if (tbx_pfd2()) GS_TBX(GS_LINEAR, false, 2);
             else GS_TBX(GS_LINEAR, false, 1);
         } else if (mode == GS_NONLINEAR) GS_TBX(GS_NONLINEAR, false, 1);
+        else if (mode == GS_NEWTON_B && zv) GS_TBX(GS_NEWTON_B, true, 1);
+        else if (mode == GS_NEWTON_B) GS_TBX(GS_NEWTON_B, false, 1);
         else if (zv) GS_TBX(GS_NEWTON, true, 1);
         else GS_TBX(GS_NEWTON, false, 1);
     } else if (y2) {
@@ -134,6 +136,8 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
             if (zv) GS_TBY(GS_LINEAR, true);
             else GS_TBY(GS_LINEAR, false);
         } else if (mode == GS_NONLINEAR) GS_TBY(GS_NONLINEAR, false);
+        else if (mode == GS_NEWTON_B && zv) GS_TBY(GS_NEWTON_B, true);
+        else if (mode == GS_NEWTON_B) GS_TBY(GS_NEWTON_B, false);
         else if (zv) GS_TBY(GS_NEWTON, true);
         else GS_TBY(GS_NEWTON, false);
     } else {
@@ -141,6 +145,8 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
             if (zv) GS_TB(GS_LINEAR, true);
             else GS_TB(GS_LINEAR, false);
         } else if (mode == GS_NONLINEAR) GS_TB(GS_NONLINEAR, false);
+        else if (mode == GS_NEWTON_B && zv) GS_TB(GS_NEWTON_B, true);
+        else if (mode == GS_NEWTON_B) GS_TB(GS_NEWTON_B, false);
         else if (zv) GS_TB(GS_NEWTON, true);
         else GS_TB(GS_NEWTON, false);
     }
@@ -162,7 +168,7 @@ int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, i
     // NEWTON too since r04) with the workspace of gs_jacobi_sweep2_prolong_ws_elems (the corrected edge
     // columns). The fine planes' parities must be the global ones (even z0): they select each plane's
     // combination
-    return !bad_level(L) && valid_stencil(S) && (mode == GS_LINEAR || mode == GS_NEWTON) && L->z0 % 2 == 0 &&
+    return !bad_level(L) && valid_stencil(S) && (mode == GS_LINEAR || newtonish(mode)) && L->z0 % 2 == 0 &&
            tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh, true) && (y2 || xh);
 }
 
@@ -196,7 +202,7 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     // coarse plane of fine local plane z: (z >> 1) + czoff, z0 even (a slab, or a plane range of one)
     const int64_t czoff = cl ? L->z0 / 2 - cl->z0 : 0;
     if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || bad_level(cl) || czoff < 0 || !v_in || !coarse_v ||
-        !v_out || !f || v_in == v_out || (mode == GS_NONLINEAR) != (coarse_sub != nullptr) || (mode == GS_NEWTON && !w) ||
+        !v_out || !f || v_in == v_out || (mode == GS_NONLINEAR) != (coarse_sub != nullptr) || (newtonish(mode) && !w) ||
         (L->nx + 1) / 2 > cl->nx + 1 || (L->ny + 1) / 2 > cl->ny + 1 || (L->nz + 1) / 2 + czoff > cl->nz + 1 ||
         !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh, true))
         return GS_EINVAL;
@@ -212,13 +218,16 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
                            dim3(256), 0, st, v_in, coarse_v, nullptr, ws, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy,
                            L->ldz, cl->ldy, cl->ldz, bw, zlo ? 1 : 0, zhi ? 1 : 0);
     }
-#define GS_TBP1(M, P, U, X, WM) hipLaunchKernelGGL((k_tb2y<M, M == GS_NEWTON ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, 1, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
+#define GS_TBP1(M, P, U, X, WM) hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, 1, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
 #define GS_TBP(M, P, X, WM) do { if (k.unit) GS_TBP1(M, P, true, X, WM); else GS_TBP1(M, P, false, X, WM); } while (0)
     // NEWTON's variant keeps ~37 KB of state per x-wave in LDS (its RECOMP rows): rows of <= 256 points
     // (two x-waves) take the instance sized for two, so that two blocks share a CU (8 waves, the VGPR
     // limit) instead of one block of 4 waves holding the whole LDS of a four-x-wave instance
     // (NEWTON column blocks: the RECOMP LDS state and the edge columns together, 144 B per lane spilled)
-    if (mode == GS_NEWTON && xh) GS_TBP(GS_NEWTON, 1, true, TBY_WX);
+    if (mode == GS_NEWTON_B && xh) GS_TBP(GS_NEWTON_B, 1, true, TBY_WX);
+    else if (mode == GS_NEWTON_B && b.y <= 2) GS_TBP(GS_NEWTON_B, 1, false, 2);
+    else if (mode == GS_NEWTON_B) GS_TBP(GS_NEWTON_B, 1, false, TBY_WX);
+    else if (mode == GS_NEWTON && xh) GS_TBP(GS_NEWTON, 1, true, TBY_WX);
     else if (mode == GS_NEWTON && b.y <= 2) GS_TBP(GS_NEWTON, 1, false, 2);
     else if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1, false, TBY_WX);
     else if (xh) GS_TBP(GS_LINEAR, 1, true, TBY_WX);
@@ -231,7 +240,7 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
 // the small-level tiled kernels (gs_device.hpp k_tile_*): LINEAR / NEWTON, canonical stencil order, whole levels
 int gs_tiled_supported(const gs_stencil* S, const gs_level* L, int mode)
 {
-    return S && valid_stencil(S) && canonical_order(S) && (mode == GS_LINEAR || mode == GS_NEWTON) && !bad_level(L) &&
+    return S && valid_stencil(S) && canonical_order(S) && (mode == GS_LINEAR || newtonish(mode)) && !bad_level(L) &&
            L->z0 == 0 && L->nx >= 1 && L->ny >= 1 && L->nz >= 1;
 }
 
@@ -240,7 +249,7 @@ int gs_smooth2_restrict_tiled(const gs_stencil* S, const gs_level* fl, int mode,
                               const gs_level* cl, hipStream_t st)
 {
     if (!gs_tiled_supported(S, fl, mode) || bad_level(cl) || cl->z0 != 0 || !v_out || !f || !coarse_f ||
-        v_in == v_out || (mode == GS_NEWTON && !w) || cl->nx != fl->nx / 2 || cl->ny != fl->ny / 2 ||
+        v_in == v_out || (newtonish(mode) && !w) || cl->nx != fl->nx / 2 || cl->ny != fl->ny / 2 ||
         cl->nz != fl->nz / 2)
         return GS_EINVAL;
     const Coef k = make_coef(S, fl, omega, gamma);
@@ -249,7 +258,8 @@ int gs_smooth2_restrict_tiled(const gs_stencil* S, const gs_level* fl, int mode,
 #define GS_TPRM(M) do { \
         if (!v_in) { if (k.unit) GS_TPR(M, true, true); else GS_TPR(M, true, false); } \
         else { if (k.unit) GS_TPR(M, false, true); else GS_TPR(M, false, false); } } while (0)
-    if (mode == GS_NEWTON) GS_TPRM(GS_NEWTON);
+    if (mode == GS_NEWTON_B) GS_TPRM(GS_NEWTON_B);
+    else if (mode == GS_NEWTON) GS_TPRM(GS_NEWTON);
     else GS_TPRM(GS_LINEAR);
 #undef GS_TPRM
 #undef GS_TPR
@@ -261,13 +271,16 @@ int gs_prolong_smooth2_tiled(const gs_stencil* S, const gs_level* fl, int mode, 
                              const double* f, const double* w, hipStream_t st)
 {
     if (!gs_tiled_supported(S, fl, mode) || bad_level(cl) || cl->z0 != 0 || !v_in || !coarse_v || !v_out || !f ||
-        v_in == v_out || (mode == GS_NEWTON && !w) || (fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 ||
+        v_in == v_out || (newtonish(mode) && !w) || (fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 ||
         (fl->nz + 1) / 2 > cl->nz + 1)
         return GS_EINVAL;
     const Coef k = make_coef(S, fl, omega, gamma);
     const dim3 g((unsigned)((fl->nx + TS - 1) / TS), (unsigned)((fl->ny + TS - 1) / TS), (unsigned)((fl->nz + TS - 1) / TS));
 #define GS_TP2(M, U) hipLaunchKernelGGL((k_tile_pro2<M, U>), g, dim3(TS_T), 0, st, k, v_in, coarse_v, f, w, v_out, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, cl->ldy, cl->ldz)
-    if (mode == GS_NEWTON) {
+    if (mode == GS_NEWTON_B) {
+        if (k.unit) GS_TP2(GS_NEWTON_B, true);
+        else GS_TP2(GS_NEWTON_B, false);
+    } else if (mode == GS_NEWTON) {
         if (k.unit) GS_TP2(GS_NEWTON, true);
         else GS_TP2(GS_NEWTON, false);
     } else {
@@ -289,7 +302,7 @@ int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L)
 int gs_residual(const gs_stencil* S, const gs_level* L, int mode, double gamma, const double* v, const double* f,
                 const double* w, double* r, double* partials, hipStream_t st)
 {
-    if (!f || (mode == GS_NEWTON && !w)) return GS_EINVAL;
+    if (!f || (newtonish(mode) && !w)) return GS_EINVAL;
     if (partials && (L && (L->nx == 0 || L->ny == 0 || L->nz == 0)))
         return (int)hipMemsetAsync(partials, 0, sizeof(double), st);
     return launch_pass<1, false>(S, L, mode, 0.0, gamma, v, f, w, r, partials, st);
@@ -333,8 +346,8 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
                               const double* f, const double* w, double* ca, double* cb, const gs_level* cl, int zhi,
                               hipStream_t st)
 {
-    if (!S || !valid_stencil(S) || !v || !f || !ca || (mode == GS_NEWTON && !w) || mode < GS_LINEAR ||
-        mode > GS_NEWTON || bad_level(fl) || bad_level(cl))
+    if (!S || !valid_stencil(S) || !v || !f || !ca || (newtonish(mode) && !w) || mode < GS_LINEAR ||
+        mode > GS_NEWTON_B || bad_level(fl) || bad_level(cl))
         return GS_EINVAL;
     if (cl->nx == 0 || cl->ny == 0 || cl->nz == 0) return 0;
     const int64_t zoff = 2 * cl->z0 - fl->z0; // fine local centre plane = 2 z + zoff
@@ -380,6 +393,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         if (mode == GS_LINEAR && nr == 2) GS_RR2(GS_LINEAR, 2);
         else if (mode == GS_LINEAR) GS_RR2(GS_LINEAR, 1);
         else if (mode == GS_NONLINEAR) GS_RR2(GS_NONLINEAR, 1);
+        else if (mode == GS_NEWTON_B) GS_RR2(GS_NEWTON_B, 1);
         else GS_RR2(GS_NEWTON, 1);
 #undef GS_RR2
 #undef GS_RR2U
@@ -399,6 +413,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
 #define GS_RR(M) hipLaunchKernelGGL(k_resrestrict<M>, g, dim3(RR_T), 0, st, k, so, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zoff, (int)zc)
     if (mode == GS_LINEAR) GS_RR(GS_LINEAR);
     else if (mode == GS_NONLINEAR) GS_RR(GS_NONLINEAR);
+    else if (mode == GS_NEWTON_B) GS_RR(GS_NEWTON_B);
     else GS_RR(GS_NEWTON);
 #undef GS_RR
     return launch_status();
@@ -508,6 +523,20 @@ int gs_newton_F_update_restrict(const gs_stencil* S, const gs_level* L, double g
     return launch_status();
 }
 
+int gs_newton_bfac(const gs_level* L, double gamma, const double* w, double* b, hipStream_t st)
+{
+    if (bad_level(L) || !w || !b) return GS_EINVAL;
+    const int64_t n = L->ldz * (L->nz + 4); // planes -1 .. nz+2
+    const double *ws = w - L->ldz;
+    double* bs = b - L->ldz;
+    if (ws < bs + n && bs < ws + n) return GS_EINVAL;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(bs), c = reinterpret_cast<uintptr_t>(ws);
+    if ((a & 7) || (c & 7)) return GS_EINVAL;
+    const int head = ((a ^ c) & 15) ? -1 : (int)((a & 15) / 8); // -1: no common dwordx4 alignment
+    hipLaunchKernelGGL(k_bfac, dim3(1024), dim3(256), 0, st, bs, ws, n, gamma, head);
+    return launch_status();
+}
+
 int gs_copy(double* dst, const double* src, int64_t n, hipStream_t st)
 {
     if (!dst || !src || n < 0) return GS_EINVAL;
@@ -534,7 +563,7 @@ int gs_coarse_cycle_max_levels(void) { return CC_MAXLEV; }
 int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int mode, double omega, double gamma,
                     int pre, int post, hipStream_t st)
 {
-    if (!S || !valid_stencil(S) || !lv || n < 1 || n > CC_MAXLEV || mode < GS_LINEAR || mode > GS_NEWTON ||
+    if (!S || !valid_stencil(S) || !lv || n < 1 || n > CC_MAXLEV || mode < GS_LINEAR || mode > GS_NEWTON_B ||
         pre < 0 || post < 0)
         return GS_EINVAL;
     CcPlan P{};
@@ -546,7 +575,7 @@ int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int m
         const gs_level* g = &a.geom;
         if (bad_level(g) || g->z0 != 0 || g->nx < 1 || g->ny < 1 || g->nz < 1 ||
             g->nx * g->ny * g->nz > (int64_t)INT32_MAX || !a.v || !a.v_alt || a.v == a.v_alt || !a.f ||
-            (l + 1 < n && !a.r) || (mode == GS_NEWTON && !a.newton_v) ||
+            (l + 1 < n && !a.r) || (newtonish(mode) && !a.newton_v) ||
             (mode == GS_NONLINEAR && ((l > 0 && !a.rest_v) || a.v_zero)))
             return GS_EINVAL;
         if (l > 0) { // consecutive levels of one hierarchy (the restriction / prolongation bounds)
@@ -570,6 +599,7 @@ int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int m
     }
     if (mode == GS_LINEAR) hipLaunchKernelGGL(k_coarse_cycle<GS_LINEAR>, dim3(1), dim3(CC_T), 0, st, P);
     else if (mode == GS_NONLINEAR) hipLaunchKernelGGL(k_coarse_cycle<GS_NONLINEAR>, dim3(1), dim3(CC_T), 0, st, P);
+    else if (mode == GS_NEWTON_B) hipLaunchKernelGGL(k_coarse_cycle<GS_NEWTON_B>, dim3(1), dim3(CC_T), 0, st, P);
     else hipLaunchKernelGGL(k_coarse_cycle<GS_NEWTON>, dim3(1), dim3(CC_T), 0, st, P);
     return launch_status();
 }

@@ -16,6 +16,7 @@ DRIVER_LIB = os.path.join(LIB_DIR, "libgpusolve_driver.so")
 EXECUTABLE = os.path.join(BIN_DIR, "GpuSolve-hip")
 
 GS_LINEAR, GS_NONLINEAR, GS_NEWTON = 0, 1, 2
+GS_NEWTON_B = 3  # NEWTON with the precomputed linearisation factor B (include/gpusolve_hip.h)
 GS_EINVAL = 100001
 
 dptr = C.POINTER(C.c_double)
@@ -101,6 +102,7 @@ KERNEL_API = {
     "gs_newton_F_update_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                               C.POINTER(gs_level), C.c_void_p]),
+    "gs_newton_bfac": (C.c_int, [C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_newton_F_update": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_copy": (C.c_int, [C.c_void_p, C.c_void_p, i64, C.c_void_p]),

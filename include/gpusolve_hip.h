@@ -52,6 +52,14 @@ extern "C" {
 #define GS_EINVAL 100001 /* bad argument (shape, stencil offset outside {-1,0,1}, null pointer) */
 
 enum { GS_LINEAR = 0, GS_NONLINEAR = 1, GS_NEWTON = 2 }; /* GridParams::Mode, src/gridParams.h:29-33 */
+/* Not a reference mode (added): NEWTON's linearised operator with the point's linearisation factor precomputed.
+ * Every launcher that takes `mode` and a `w` operand accepts it; `w` then holds B = gamma*(1+newtonV)*exp(newtonV)
+ * (gs_newton_bfac) instead of newtonV. The Jacobi denominator preFac + B is bit for bit the reference's
+ * preFac + gamma*(1+w)*exp(w) (CpuSolver.cpp:166-172); the operator term is B*v instead of the reference's
+ * (gamma*(1+w)*v)*exp(w) (CpuSolver.cpp:63-66), one product re-associated (a rounding of the term, like glibc's
+ * vs ocml's exp). The host driver's inner Newton solves run in this mode: exp(newtonV) is evaluated once per
+ * point and Newton iteration instead of in every sweep, residual and restriction of the ten inner V-cycles. */
+enum { GS_NEWTON_B = 3 };
 
 /* GridParams::stencil (src/gridParams.h:7-27): values + (x,y,z) offsets, config order. */
 typedef struct {
@@ -224,6 +232,11 @@ int gs_newton_F_update_restrict(const gs_stencil* S, const gs_level* L, double g
                                 const double* F, double* w_out, double* f, double* partials, double* coarse_w,
                                 const gs_level* coarse, hipStream_t stream);
 
+/* The linearisation factor of GS_NEWTON_B (added): b = gamma*(1+w)*exp(w), in that evaluation order, at every
+ * element of planes -1 .. nz+2 of a field laid out by gs_field_layout (interior, boundary and ghost planes, the
+ * row padding included), so a Z-slab's B is current wherever its w is. w and b must not overlap. */
+int gs_newton_bfac(const gs_level* L, double gamma, const double* w, double* b, hipStream_t stream);
+
 /* dst[i] = src[i] for i < n (Vector3 copy-assignment: NewtonSolver.cpp:12 newtonF = f), non-temporal
  * streams; the buffers must not overlap unless dst == src. */
 int gs_copy(double* dst, const double* src, int64_t n, hipStream_t stream);
@@ -247,7 +260,7 @@ typedef struct {
     double *v, *v_alt, *f;
     double* r;        /* residual scratch */
     double* rest_v;   /* NONLINEAR: restricted iterate; else NULL */
-    double* newton_v; /* NEWTON: the linearisation point; else NULL */
+    double* newton_v; /* NEWTON: the linearisation point (GS_NEWTON_B: its factor B); else NULL */
     gs_level geom;
     int v_zero;
 } gs_coarse_level;

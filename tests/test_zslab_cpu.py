@@ -273,6 +273,8 @@ def _replay_newton_worker(rank, world, port, params, min_points, q, env):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ops = X.schedule(params, world, rank, min_points)
+        if env.get("GS_TEST_MUTATE"):
+            ops = X.mutate(ops, env["GS_TEST_MUTATE"])
         R = X.Rank(params, rank, world, min_points)
         R.run(ops)
         lo, hi, v = R.owned_v("v")
@@ -285,19 +287,23 @@ def _replay_newton_worker(rank, world, port, params, min_points, q, env):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fused", [True])  # (False, the two-pass axpy path, replays too: ~2 min more)
-def test_gloo_replay_newton_schedule(fused):
+@pytest.mark.parametrize("fused,stale", [(True, False), (True, True)])  # (fused False, the two-pass axpy path,
+def test_gloo_replay_newton_schedule(fused, stale):                        # replays too: ~2 min more)
     """NEWTON's Z-slab schedule (NewtonSolver: newtonF, the inner solves, findError's newtonV += v — fused into
     the next compF with the new newtonV's ghost planes formed from both operands, or the two-pass axpy with
     GS_NO_NEWTON_FUSED_UPDATE — and the per-level newtonV restriction) replayed on two gloo ranks with the
     oracle's point expressions: Newton history, newtonV and v against the single-domain oracle solve. numpy's
     exp stands in for libm's, so the comparison is to 1e-10, not bit for bit. A power-of-two grid: its inner
     solves never meet their tol-0.1 exit, so the traced schedule — whose placeholder norms
-    never stop a loop — runs the ten inner V-cycles the oracle runs."""
-    dims, world = (256, 512, 64), 2
+    never stop a loop — runs the ten inner V-cycles the oracle runs. The inner solves read the GS_NEWTON_B
+    factors ("bfac" ops, replayed as a snapshot of the newtonV each was computed from); stale: the schedule with
+    the second iteration's level-0 factor dropped must NOT reproduce the oracle."""
+    dims, world = ((64, 128, 64) if stale else (256, 512, 64)), 2
     params = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=2)
     # (the fused run also takes the NEWTON prolongation pair on every slab level: GS_NEWTON_PRO_POINTS=0)
     env = {"GS_NEWTON_PRO_POINTS": "0"} if fused else {"GS_NO_NEWTON_FUSED_UPDATE": "1"}
+    if stale:
+        env["GS_TEST_MUTATE"] = "bfac"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -312,9 +318,13 @@ def test_gloo_replay_newton_schedule(fused):
     og = O.Grid(dims, mode=O.NEWTON, maxiter=2)
     ref_hist = og.solve()
     ref_v, ref_w = og.field(0, "v").copy(), og.field(0, "newtonV").copy()
+    if stale:
+        same = all(all(abs(a - b) <= 1e-10 * abs(b) for a, b in zip(r[5], ref_hist)) for r in res)
+        assert not same, "a stale GS_NEWTON_B factor went unnoticed"
+        return
     for rank, lo, hi, v, w, hist, ops in res:
         assert ("newtonFupdate" in ops and "ghostsum" in ops) == fused and ("axpy" in ops) != fused, ops
-        assert ("pro" in ops) == fused, ops
+        assert ("pro" in ops) == fused and "bfac" in ops, ops
         assert len(hist) == len(ref_hist)
         for a, b in zip(hist, ref_hist):
             assert abs(a - b) <= 1e-10 * abs(b), (a, b)

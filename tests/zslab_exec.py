@@ -49,8 +49,13 @@ def schedule(params, nranks, rank, min_points):
 def mutate(ops, kind):
     """A deliberately broken schedule (tests the replay's power to catch one): "halo" drops the first
     ghost exchange of a level-1 iterate, "depth" exchanges level-0 iterate ghosts one plane deep only,
-    "range" shortens the first interior pair's plane range by one plane."""
+    "range" shortens the first interior pair's plane range by one plane, "bfac" drops the second Newton
+    iteration's GS_NEWTON_B factor of level 0 (its inner solve reads the first iteration's)."""
     out = [(op, dict(kv)) for op, kv in ops]
+    if kind == "bfac":
+        idx = [i for i, (op, kv) in enumerate(out) if op == "bfac" and kv["L"] == 0]
+        del out[idx[1]]
+        return out
     for i, (op, kv) in enumerate(out):
         if kind == "halo" and op == "halo" and kv.get("L") == 1 and kv["field"] == "vAlt":
             del out[i]
@@ -215,6 +220,7 @@ class Rank:
         self.history = []
         self.mode, self.gamma = params.mode, params.gamma
         self.newton_history, self._newton_norm = [], False
+        self.bmode = False  # the schedule computes GS_NEWTON_B factors (bfac ops)
 
     # ---- communication (gloo) ----
     def halo(self, L, name, depth):
@@ -269,8 +275,16 @@ class Rank:
     def v_in(self, L, vzero):
         return np.zeros_like(L.fields["v"]) if vzero else L.fields["v"]
 
+    def w_of(self, L):
+        """The linearisation point the smoothing kernels read: newtonV, or — once the schedule computes the
+        GS_NEWTON_B factors ("bfac") — the newtonV that level's factor was computed from (its snapshot at the
+        bfac op; a schedule that lets newtonV change without recomputing the factor replays the stale point)."""
+        if not self.bmode:
+            return L.fields["newtonV"]
+        return L.fields["bfacW"]
+
     def sw(self, L):
-        return dict(mode=self.mode, W=L.fields["newtonV"], gamma=self.gamma)
+        return dict(mode=self.mode, W=self.w_of(L), gamma=self.gamma)
 
     def op_pair(self, L, z1, z2, zlo, zhi, vzero, norm, V=None):
         g1, g2 = L.local_to_global(z1), L.local_to_global(z2)
@@ -335,7 +349,7 @@ class Rank:
         inner = [j for j, g in enumerate(gplanes) if 1 <= g <= L.nz]
         if inner:
             zi = np.array([L.idx(gplanes[j]) for j in inner])
-            a, _, _ = operator(L.fields["v"], zi, L, self.mode, L.fields["newtonV"], self.gamma)
+            a, _, _ = operator(L.fields["v"], zi, L, self.mode, self.w_of(L), self.gamma)
             R[1:-1, 1:-1, inner] = L.fields["f"][1:-1, 1:-1, zi] - a
         return R
 
@@ -379,7 +393,7 @@ class Rank:
         def vc(l, v):
             L = self.levels[l]
             f = arr(L, "f")
-            w = arr(L, "newtonV") if m == NEWTON else None
+            w = (arr(L, "bfacW") if self.bmode else arr(L, "newtonV")) if m == NEWTON else None
             if l == nl - 1:
                 return O.jacobi(v, f, L.h, m, p.omega, g, p.preSmoothing + p.postSmoothing, w=w)
             v = O.jacobi(v, f, L.h, m, p.omega, g, p.preSmoothing, w=w) if p.preSmoothing else v
@@ -457,6 +471,9 @@ class Rank:
                 L.fields["newtonV"][:, :, sl] = L.fields["newtonV"][:, :, sl] + 1.0 * L.fields["v"][:, :, sl]
             elif op == "nonorm":  # the last inner cycle's unread closing norm, not computed
                 pass
+            elif op == "bfac":  # gs_newton_bfac: the level's GS_NEWTON_B factor from its current newtonV
+                self.bmode = True
+                L.fields["bfacW"] = L.fields["newtonV"].copy()
             elif op == "halo":
                 self.halo(L, kv["field"], kv["depth"])
             elif op == "gather":

@@ -1,6 +1,7 @@
 """The three level-0 passes of a NEWTON V-cycle timed alone on a 512^3 grid through the kernel C ABI
 (and their LINEAR counterparts), HIP events around K launches each, interleaved over rounds:
     python tools/newton_kprobe.py [rounds] [K] [n]
+  (each in mode 3 = GS_NEWTON_B with the factor field from gs_newton_bfac, mode 2 = GS_NEWTON, mode 0)
   spec pair    gs_jacobi_sweep2_norm  (two sweeps + the norm partials of the input's residual), 32 B/point
   rr           gs_residual_restrict   (residual + full weighting), 25 B/point (LINEAR 17)
   pro pair     gs_jacobi_sweep2_prolong_ws (prolongation + correction + two sweeps), 33 B/point (LINEAR 25)
@@ -60,8 +61,11 @@ def main():
     parts = torch.zeros(max(1, kl.gs_jacobi_sweep2_num_partials(C.byref(S), C.byref(L), 2)) + 4096,
                         dtype=torch.float64, device="cuda")
     res = {}
-    for mode, name in ((2, "newton"), (0, "linear")):
-        wp = w.ptr if mode == 2 else None
+    # mode 3 (GS_NEWTON_B): the same kernels with the precomputed factor as their w operand
+    b = DevField(*dims)
+    assert kl.gs_newton_bfac(C.byref(w.level(h)), 1.0, w.ptr, b.ptr, None) == 0
+    for mode, name in ((3, "newtonb"), (2, "newton"), (0, "linear")):
+        wp = (w.ptr if mode == 2 else b.ptr) if mode >= 2 else None
         wsn = kl.gs_jacobi_sweep2_prolong_ws_elems(C.byref(S), C.byref(L), mode)
         ws = torch.empty(max(1, wsn), dtype=torch.float64, device="cuda")
 
@@ -80,8 +84,9 @@ def main():
         def padd():
             assert kl.gs_prolong_add(cv.ptr, None, C.byref(Lc), out.ptr, C.byref(L), s) == 0
 
-        bpp = {"pair": 32.0 if mode == 2 else 24.0, "rr": 25.0 if mode == 2 else 17.0,
-               "pro": 33.0 if mode == 2 else 25.0, "prolong_add": 16.0}
+        nw = mode >= 2
+        bpp = {"pair": 32.0 if nw else 24.0, "rr": 25.0 if nw else 17.0,
+               "pro": 33.0 if nw else 25.0, "prolong_add": 16.0}
         for _ in range(rounds):
             for kname, fn in (("pair", pair), ("rr", rr), ("pro", pro), ("prolong_add", padd)):
                 fn()
