@@ -402,12 +402,14 @@ def rccl_debug_setup():
     P2P, NET) goes to a per-process file, so that the line can report the transport every peer connection
     actually took (P2P/IPC over xGMI, P2P/direct pointer, SHM, NET/Socket ...). An explicit NCCL_DEBUG /
     NCCL_DEBUG_FILE in the environment wins. Returns this process's log path or None."""
-    if os.environ.get("NCCL_DEBUG") and not os.environ.get("NCCL_DEBUG_FILE"):
-        return None  # the user's own logging (to stdout / stderr): nothing to parse
-    os.environ.setdefault("NCCL_DEBUG", "INFO")
-    os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,P2P,NET")
-    os.environ.setdefault("NCCL_DEBUG_FILE", os.path.join(
-        "/tmp", f"gs-rccl-{os.environ.get('MASTER_PORT', '0')}-{os.environ.get('RANK', '0')}-%h-%p.log"))
+    if os.environ.get("NCCL_DEBUG_FILE"):  # the launcher's own log file: parsed if it logs at INFO
+        if os.environ.get("NCCL_DEBUG", "").upper() not in ("INFO", "TRACE"):
+            return None
+    else:  # (a preset NCCL_DEBUG level without a file would print to stdout / stderr: the file takes over)
+        os.environ["NCCL_DEBUG"] = "INFO"
+        os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,NET"
+        os.environ["NCCL_DEBUG_FILE"] = os.path.join(
+            "/tmp", f"gs-rccl-{os.environ.get('MASTER_PORT', '0')}-{os.environ.get('RANK', '0')}-%h-%p.log")
     return os.environ["NCCL_DEBUG_FILE"].replace("%h", os.uname().nodename).replace("%p", str(os.getpid()))
 
 
@@ -653,6 +655,8 @@ def main():
                                                       "pair_ms_max_rank": round(km.item(), 4)})
 
     transports = None
+    if world > 1 and not rccl_log:
+        transports = {"error": "NCCL_DEBUG_FILE preset without NCCL_DEBUG=INFO: no connection log to parse"}
     if world > 1 and rccl_log:
         mine = rccl_transports(rccl_log)
         allt = [None] * world

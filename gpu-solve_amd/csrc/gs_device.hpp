@@ -128,10 +128,11 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_RB_ZC=n           z-chunk of the one-point passes (k_rb sweeps / residuals, the Newton update pass) (A/B)
 //   GS_NEWTON_XH=0       NEWTON plain pairs on rows of 513-1024 points through k_tb2 instead of column blocks (A/B)
 //   GS_SPEC_CACHED=1     pairs with norm partials store through the caches, not non-temporally (A/B)
+//   GS_RR_NG=1|2         k_rr2 groups of coarse rows per block (default: 2 on levels of >= 2^26 points)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh, specCached;
     int xhSwizzle, midZc, rrZc, rrZcBig, oneRoundMid, rbZc;
-    int slabZc, pairZc, rrNr, rrNtu, rrReverse;
+    int slabZc, pairZc, rrNr, rrNtu, rrReverse, rrNg;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
     {
@@ -145,7 +146,7 @@ struct Knobs {
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
           newtonXh(num("GS_NEWTON_XH", 1) != 0), specCached(num("GS_SPEC_CACHED", 0) != 0),
           xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), oneRoundMid(num("GS_PAIR_ONE_ROUND_MID", 0)), rbZc(num("GS_RB_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
-          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 1)),
+          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 1)), rrNg(num("GS_RR_NG", 0)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
     }
@@ -336,6 +337,10 @@ __device__ __forceinline__ double newton_update(const Coef& k, double v, double 
     return v + k.omega * (r / den);
 #endif
 }
+
+// GS_NEWTON_B's linearisation factor of a point, b = gamma (1 + w) exp(w), evaluated as the reference's Jacobi
+// denominator evaluates its product, (gamma * (1 + w)) * exp(w) (CpuSolver.cpp:166-172)
+__device__ __forceinline__ double bfac_of(double gamma, double w) { return gamma * (1 + w) * exp(w); }
 
 // A and E of a point from its w operand: GS_NEWTON_B's w is B itself, so A = B and E = 1 (A * c * E = B * c and
 // preFac + A * E = preFac + B exactly: the products by 1.0 fold away)
@@ -623,13 +628,18 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
 // bit-identical to gs_restrict of the stored newtonV, whose 1.1 GB re-read at 512^3 it saves. The chunk of
 // planes is even; the last chunk runs one step past the level when nz is even (coarse plane nz / 2).
 // (three waves per SIMD, as the plain pass has: <= 168 VGPRs for the restriction's rings)
-template <int RY, int W, bool UN, bool RS = false>
-__global__ __launch_bounds__(WAVE* W, 3) void k_newton_upd(Coef k, const double* __restrict__ w,
+// BF: the next inner solve's GS_NEWTON_B factor of this level in the same pass — bout = bfac_of(w') at the
+// block's own points, from the exp(w') of compF's term (evaluated once): that level's gs_newton_bfac pass is not
+// needed (the coarse level's factor stays a gs_newton_bfac pass: its exp inside the restriction's register rings
+// spilled ~90 B per lane at three waves per SIMD). RS + BF runs at two waves per SIMD (at three it spills 20 B)
+template <int RY, int W, bool UN, bool RS = false, bool BF = false>
+__global__ __launch_bounds__(WAVE* W, (RS && BF) ? 2 : 3) void k_newton_upd(Coef k, const double* __restrict__ w,
                                                          const double* __restrict__ e, const double* __restrict__ F,
                                                          double* __restrict__ wout, double* __restrict__ fout,
                                                          double* __restrict__ partials, int nx, int ny, int nz,
                                                          int64_t ldy, int64_t ldz, int ZC, double* __restrict__ cw,
-                                                         int cnx, int cny, int cnz, int64_t cldy, int64_t cldz)
+                                                         int cnx, int cny, int cnz, int64_t cldy, int64_t cldz,
+                                                         double* __restrict__ bout)
 {
     static_assert(!RS || RY == 2, "the restriction takes two fine rows per wave");
     __shared__ double red[W];
@@ -710,8 +720,20 @@ __global__ __launch_bounds__(WAVE* W, 3) void k_newton_upd(Coef k, const double*
                 const double2 zm = P[r], zp = NL[cs][r];
                 const double xm0 = lane_from_left<true>(c.y, EL[cs][r]);
                 const double xp1 = lane_from_right<true>(c.x, ER[cs][r]);
-                const double a0 = op_value<GS_NONLINEAR, UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x, 0.0);
-                const double a1 = op_value<GS_NONLINEAR, UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y, 0.0);
+                // (compF's non-linear term gamma w' exp(w'), NewtonSolver.cpp:63-72, and B share exp(w'))
+                double a0 = div_hh(k, stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, zp.x, zm.x));
+                double a1 = div_hh(k, stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, zp.y, zm.y));
+                double b0 = 0.0, b1 = 0.0;
+                {
+                    const double E0 = exp(c.x), E1 = exp(c.y);
+                    const double nl0 = k.gamma * c.x * E0, nl1 = k.gamma * c.y * E1;
+                    a0 += nl0;
+                    a1 += nl1;
+                    if constexpr (BF) {
+                        b0 = k.gamma * (1 + c.x) * E0;
+                        b1 = k.gamma * (1 + c.y) * E1;
+                    }
+                }
                 const double r0 = FL[cs][r].x - a0, r1 = FL[cs][r].y - a1;
                 const bool rowok = real && y0 + r <= ny;
                 if (rowok && okx0) sumsq += r0 * r0;
@@ -721,9 +743,11 @@ __global__ __launch_bounds__(WAVE* W, 3) void k_newton_upd(Coef k, const double*
                     if (okx1) {
                         st2s<true>(fout + q, r0, r1);
                         st2s<true>(wout + q, c.x, c.y);
+                        if constexpr (BF) st2s<true>(bout + q, b0, b1);
                     } else if (okx0) {
                         fout[q] = r0;
                         wout[q] = c.x;
+                        if constexpr (BF) bout[q] = b0;
                     }
                 }
             }
@@ -1063,7 +1087,11 @@ constexpr int RR2_WXMAX = 8, RR2_NR2_LOG2_POINTS = 26;
 
 // NR: coarse rows per block (1: fine rows 2Y-1..2Y+1 computed; 2: 2Y-1..2Y+3, the shared row 2Y+1 and three
 // of the seven v rows once instead of twice)
-template <int MODE, bool PF, int NR = 1, bool UN = false, bool NTU = false> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
+// NG: groups of WX waves per block, group g owning coarse rows Y + NR g: the groups are y-neighbours that march
+// the same planes in lock-step (the per-plane barrier is the block's), so the v / f rows they share are
+// fetched by the one CU at the same time — an L1 / L2 hit for the second group — instead of by two blocks
+// that drift apart on different CUs (where the shared rows miss the 4 MB L2 a third of the time)
+template <int MODE, bool PF, int NR = 1, bool UN = false, bool NTU = false, int NG = 1> // PF: the next plane's operands in flight (two-slot ring), else loaded per step
 __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* __restrict__ v,
                                                          const double* __restrict__ f, const double* __restrict__ w,
                                                          double* __restrict__ ca,
@@ -1075,16 +1103,20 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     constexpr int RR = 2 * NR + 1; // computed fine rows; v rows 0 .. RR+1 (0 and RR+1: halo rows)
     // wave-edge columns [parity][1 + wave][side][plane * 3 + row] of v, and r at each wave's first fine
     // column [parity][1 + wave][plane * 3 + row]; slots 0 and WX+1 are the zero x-boundary
-    __shared__ double ve[2][RR2_WXMAX + 2][2][2 * RR];
-    __shared__ double re[2][RR2_WXMAX + 2][2 * RR];
+    __shared__ double veA[NG][2][RR2_WXMAX + 2][2][2 * RR];
+    __shared__ double reA[NG][2][RR2_WXMAX + 2][2 * RR];
     const int lane = threadIdx.x;
     const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int grp = NG > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.z) : 0;
     const int WX = blockDim.y;
-    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 2 * 2 * RR; i += WAVE * WX) (&ve[0][0][0][0])[i] = 0.0;
-    for (int i = lane + WAVE * wx; i < 2 * (RR2_WXMAX + 2) * 2 * RR; i += WAVE * WX) (&re[0][0][0])[i] = 0.0;
+    const int tid = lane + WAVE * (wx + WX * grp);
+    for (int i = tid; i < NG * 2 * (RR2_WXMAX + 2) * 2 * 2 * RR; i += WAVE * WX * NG) (&veA[0][0][0][0][0])[i] = 0.0;
+    for (int i = tid; i < NG * 2 * (RR2_WXMAX + 2) * 2 * RR; i += WAVE * WX * NG) (&reA[0][0][0][0])[i] = 0.0;
     __syncthreads();
+    double (&ve)[2][RR2_WXMAX + 2][2][2 * RR] = veA[grp]; // this group's wave-edge exchange
+    double (&re)[2][RR2_WXMAX + 2][2 * RR] = reA[grp];
     const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-    const int Y = 1 + NR * (int)(tile % gridDim.x);
+    const int Y = 1 + NR * (NG * (int)(tile % gridDim.x) + grp);
     // rev (GS_RR_REVERSE): the z-chunks in descending order, so the first blocks read the planes the
     // preceding pair launch touched last
     const int zi = (int)(tile / gridDim.x);
@@ -1621,10 +1653,8 @@ __global__ __launch_bounds__(256) void k_copy(double* __restrict__ dst, const do
     }
 }
 
-// GS_NEWTON_B's linearisation factor b = gamma (1 + w) exp(w), evaluated as the reference's Jacobi denominator
-// evaluates its product, (gamma * (1 + w)) * exp(w) (CpuSolver.cpp:166-172): elementwise over n elements,
-// dwordx4 streams when both arrays share an alignment (head: 0 or 1 leading element), else one per thread (-1)
-__device__ __forceinline__ double bfac_of(double gamma, double w) { return gamma * (1 + w) * exp(w); }
+// GS_NEWTON_B's linearisation factor (bfac_of) elementwise over n elements, dwordx4 streams when both arrays
+// share an alignment (head: 0 or 1 leading element), else one per thread (-1)
 __global__ __launch_bounds__(256) void k_bfac(double* __restrict__ b, const double* __restrict__ w, int64_t n,
                                               double gamma, int head)
 {

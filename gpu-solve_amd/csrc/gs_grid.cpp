@@ -176,6 +176,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         sw.pipeline = !on("GS_NO_PIPELINE");
         sw.newtonFusedUpdate = !on("GS_NO_NEWTON_FUSED_UPDATE");
         sw.newtonB = !on("GS_NO_NEWTON_B");
+        if (const char* e = std::getenv("GS_NEWTON_B_FUSED")) sw.newtonBFused = std::atoi(e) != 0;
         if (const char* e = std::getenv("GS_NEWTON_PRO_POINTS")) sw.newtonProPoints = std::strtoll(e, nullptr, 10);
         if (const char* e = std::getenv("GS_TILE_POINTS")) sw.tilePoints = std::strtoll(e, nullptr, 10);
         if (const char* e = std::getenv("GS_HALO_ORDER")) sw.haloOrder = std::atoi(e);
@@ -1266,18 +1267,23 @@ double NewtonSolver::compFUpdate(HipGridData& grid)
     const bool r1 = grid.numLevels() >= 3 && !(L0.distributed && grid.nranks() > 1) &&
                     (grid.trace || grid.getLevel(1).newtonVNext.data() != nullptr) &&
                     gs_newton_F_update_restrict_supported(&grid.stencilAbi, &L0.geom, &grid.getLevel(1).geom) != 0;
+    // the same pass also writes the next inner solve's GS_NEWTON_B factor of level 0 (from the exp(w') compF
+    // evaluates anyway): findError then skips that level's gs_newton_bfac pass
+    const bool bf = r1 && grid.sw.newtonB && grid.sw.newtonBFused;
     if (grid.trace)
-        grid.rec("newtonFupdate", {{"L", 0}, {"restrict", r1}});
+        grid.rec("newtonFupdate", {{"L", 0}, {"restrict", r1}, {"bfac", bf}});
     else if (r1)
-        check(gs_newton_F_update_restrict(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
-                                          grid.newtonF.data(), L0.vAlt.data(), L0.f.data(), grid.partials(),
-                                          grid.getLevel(1).newtonVNext.data(), &grid.getLevel(1).geom, grid.stream()),
+        check(gs_newton_F_update_restrict_bfac(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
+                                               grid.newtonF.data(), L0.vAlt.data(), L0.f.data(), grid.partials(),
+                                               grid.getLevel(1).newtonVNext.data(), &grid.getLevel(1).geom,
+                                               bf ? L0.bfac.data() : nullptr, grid.stream()),
               "gs_newton_F_update_restrict");
     else
         check(gs_newton_F_update(&grid.stencilAbi, &L0.geom, grid.gamma, L0.newtonV.data(), L0.v.data(),
                                  grid.newtonF.data(), L0.vAlt.data(), L0.f.data(), grid.partials(), grid.stream()),
               "gs_newton_F_update");
     grid.newtonR1_ = r1;
+    grid.bfacFresh_ = bf ? 1u : 0u;
     if (L0.distributed && grid.nranks() > 1) {
         // the ghost planes of w' = newtonV + v (see fusedUpdate)
         const int64_t ldz = L0.v.ldz();
@@ -1314,11 +1320,13 @@ bool NewtonSolver::findError(HipGridData& grid)
     if (grid.sw.newtonB) {
         for (std::size_t i = 0; i < grid.numLevels(); i++) {
             auto& L = grid.getLevel(i);
+            if (i < 32 && (grid.bfacFresh_ >> i) & 1u) continue; // written by the last compFUpdate pass
             if (grid.trace) grid.rec("bfac", {{"L", (long long)i}});
             else check(gs_newton_bfac(&L.geom, grid.gamma, L.newtonV.data(), L.bfac.data(), grid.stream()), "gs_newton_bfac");
         }
         grid.newtonB_ = true;
     }
+    grid.bfacFresh_ = 0;
 
     const bool keepPrint = grid.printProgress;
     grid.printProgress = false;

@@ -153,6 +153,8 @@ public:
         bool newtonFusedUpdate = true; // GS_NO_NEWTON_FUSED_UPDATE: newtonV += v, then compF (two passes)
         bool newtonB = true; // GS_NO_NEWTON_B: inner Newton solves read newtonV (GS_NEWTON) instead of the
                              // precomputed factor B (GS_NEWTON_B: exp(newtonV) once per point and Newton iteration)
+        bool newtonBFused = true; // GS_NEWTON_B_FUSED=0: level 0's factor from its own gs_newton_bfac pass instead
+                                  // of the compF update pass (bit-identical)
         int64_t tilePoints = (int64_t)1 << 18; // GS_TILE_POINTS: levels of at most this many points (replicated,
                                                // LINEAR) run the tiled one-launch down/up-leg steps; 0 = off
         int64_t newtonProPoints = (int64_t)1 << 24; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
@@ -226,6 +228,7 @@ private:
     friend class NewtonSolver;
     bool newtonR1_ = false;    // level 1's newtonVNext holds R(level 0's newtonV) (gs_newton_F_update_restrict)
     bool newtonB_ = false;     // every level's bfac holds B of its current newtonV (set for the inner solve)
+    unsigned bfacFresh_ = 0;   // bit l: level l's bfac already holds B of the newtonV the next findError uses
     double haloCurMs_ = 0.0;   // host ms spent on that exchange so far
     double traceNorm();
     friend class HipSolver;

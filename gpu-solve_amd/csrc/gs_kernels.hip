@@ -370,7 +370,12 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         const bool big = fl->nx * fl->ny * fl->nz >= ((int64_t)1 << RR2_NR2_LOG2_POINTS);
         // (NEWTON with two rows spills 19 VGPRs: 40.5 vs 38.9 ms per 512^3 Newton iteration, gpurun_out/rrn)
         const int nr = mode == GS_LINEAR && (nr_env == 2 || (nr_env == 0 && big)) ? 2 : 1;
-        const int64_t rows = (cl->ny + nr - 1) / nr; // blocks along y
+        // groups of coarse rows per block (k_rr2 NG): two on levels of >= 2^26 points whose rows fit twice in
+        // a block, for the kernels at two waves per SIMD (LINEAR two-row, NEWTON: the 8-wave block is what a CU
+        // holds anyway; NONLINEAR's 157-VGPR form would lose its third wave per SIMD); GS_RR_NG=1|2 forces it (A/B)
+        const bool ngAuto = big && (nr == 2 || newtonish(mode));
+        const int ng = (kKnobs.rrNg == 1 || (kKnobs.rrNg == 0 && !ngAuto) || 2 * wxs > RR2_WXMAX) ? 1 : 2;
+        const int64_t rows = (cl->ny + nr * ng - 1) / (nr * ng); // blocks along y
         const int64_t chunks = (2048 + rows - 1) / rows;
         int64_t zc = (cl->nz + chunks - 1) / chunks;
         zc = zc < 1 ? 1 : (zc > 32 ? 32 : zc);
@@ -380,14 +385,15 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         if (big) zc = cl->nz < 64 ? (cl->nz < 1 ? 1 : cl->nz) : 64;
         if (kKnobs.rrZc > 0 && !big) zc = kKnobs.rrZc;       // (A/B: fine levels of < 2^26 points)
         if (kKnobs.rrZcBig > 0 && big) zc = kKnobs.rrZcBig; // (A/B: fine levels of >= 2^26 points)
-        const dim3 g((unsigned)rows, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
+        const dim3 g((unsigned)rows, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs, (unsigned)ng);
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
         // two-row blocks: the rows no neighbouring block reads are non-temporal loads (0.490 vs 0.505 ms at
         // 512^3, r02 tools/rr_ab_session.sh rrntu); GS_RR_NTU=0 keeps them cached (A/B)
         const int ntu_env = kKnobs.rrNtu;
         const bool ntu = ntu_env == 2 || (ntu_env == 1 && nr == 2);
-#define GS_RR2V(M, N, U, T) hipLaunchKernelGGL((k_rr2<M, false, N, U, T>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0, kKnobs.rrReverse)
+#define GS_RR2G(M, N, U, T, G) hipLaunchKernelGGL((k_rr2<M, false, N, U, T, G>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0, kKnobs.rrReverse)
+#define GS_RR2V(M, N, U, T) do { if (ng == 2) GS_RR2G(M, N, U, T, 2); else GS_RR2G(M, N, U, T, 1); } while (0)
 #define GS_RR2U(M, N, U) do { if (ntu) GS_RR2V(M, N, U, true); else GS_RR2V(M, N, U, false); } while (0)
 #define GS_RR2(M, N) do { if (k.unit) GS_RR2U(M, N, true); else GS_RR2U(M, N, false); } while (0)
         if (mode == GS_LINEAR && nr == 2) GS_RR2(GS_LINEAR, 2);
@@ -398,6 +404,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
 #undef GS_RR2
 #undef GS_RR2U
 #undef GS_RR2V
+#undef GS_RR2G
         return launch_status();
     }
     StencilOffsets so;
@@ -489,10 +496,10 @@ int gs_newton_F_update(const gs_stencil* S, const gs_level* L, double gamma, con
     const dim3 b(WAVE, RB_W);
     if (k.unit)
         hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, true>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials,
-                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, nullptr, 0, 0, 0, 0, 0);
+                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, nullptr, 0, 0, 0, 0, 0, nullptr);
     else
         hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, false>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials,
-                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, nullptr, 0, 0, 0, 0, 0);
+                           (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, nullptr, 0, 0, 0, 0, 0, nullptr);
     return launch_status();
 }
 
@@ -509,16 +516,29 @@ int gs_newton_F_update_restrict(const gs_stencil* S, const gs_level* L, double g
                                 const double* F, double* w_out, double* f, double* partials, double* coarse_w,
                                 const gs_level* cl, hipStream_t st)
 {
+    return gs_newton_F_update_restrict_bfac(S, L, gamma, w, e, F, w_out, f, partials, coarse_w, cl, nullptr, st);
+}
+
+int gs_newton_F_update_restrict_bfac(const gs_stencil* S, const gs_level* L, double gamma, const double* w,
+                                     const double* e, const double* F, double* w_out, double* f, double* partials,
+                                     double* coarse_w, const gs_level* cl, double* b_out, hipStream_t st)
+{
     if (!w || !e || !F || !w_out || !f || !coarse_w || w_out == w || w_out == e ||
+        (b_out && (b_out == w_out || b_out == w || b_out == e || b_out == f)) ||
         !gs_newton_F_update_restrict_supported(S, L, cl))
         return GS_EINVAL;
     static_assert(RB_RY == 2, "the fused restriction takes two fine rows per wave");
     const Coef k = make_coef(S, L, 0.0, gamma);
     const PassPlan plan = pass_plan(S, L); // the same grid / partials as gs_newton_F_update
     const dim3 b(WAVE, RB_W);
-#define GS_NUR(U) hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, U, true>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, coarse_w, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz)
-    if (k.unit) GS_NUR(true);
-    else GS_NUR(false);
+#define GS_NUR(U, B) hipLaunchKernelGGL((k_newton_upd<RB_RY, RB_W, U, true, B>), plan.grid, b, 0, st, k, w, e, F, w_out, f, partials, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, plan.zc, coarse_w, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, b_out)
+    if (b_out) {
+        if (k.unit) GS_NUR(true, true);
+        else GS_NUR(false, true);
+    } else {
+        if (k.unit) GS_NUR(true, false);
+        else GS_NUR(false, false);
+    }
 #undef GS_NUR
     return launch_status();
 }

@@ -102,6 +102,9 @@ KERNEL_API = {
     "gs_newton_F_update_restrict": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                               C.POINTER(gs_level), C.c_void_p]),
+    "gs_newton_F_update_restrict_bfac": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
+                                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p, C.POINTER(gs_level), C.c_void_p, C.c_void_p]),
     "gs_newton_bfac": (C.c_int, [C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_newton_F_update": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),

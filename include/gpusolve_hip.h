@@ -231,6 +231,12 @@ int gs_newton_F_update_restrict_supported(const gs_stencil* S, const gs_level* L
 int gs_newton_F_update_restrict(const gs_stencil* S, const gs_level* L, double gamma, const double* w, const double* e,
                                 const double* F, double* w_out, double* f, double* partials, double* coarse_w,
                                 const gs_level* coarse, hipStream_t stream);
+/* The same pass plus the next inner solve's GS_NEWTON_B factor of this level (added): b_out = bfac(w_out) at the
+ * interior points — gs_newton_bfac's values there, from the exp(w_out) compF evaluates anyway. NULL: exactly the
+ * call above. */
+int gs_newton_F_update_restrict_bfac(const gs_stencil* S, const gs_level* L, double gamma, const double* w,
+                                     const double* e, const double* F, double* w_out, double* f, double* partials,
+                                     double* coarse_w, const gs_level* coarse, double* b_out, hipStream_t stream);
 
 /* The linearisation factor of GS_NEWTON_B (added): b = gamma*(1+w)*exp(w), in that evaluation order, at every
  * element of planes -1 .. nz+2 of a field laid out by gs_field_layout (interior, boundary and ghost planes, the

@@ -1,0 +1,165 @@
+"""GS_NEWTON_B (include/gpusolve_hip.h): the inner Newton solves read the precomputed linearisation factor
+B = gamma (1 + newtonV) exp(newtonV) (gs_newton_bfac, once per level and Newton iteration) instead of evaluating
+exp(newtonV) in every sweep, residual and restriction. The Jacobi denominator preFac + B is the reference's
+bit for bit; the operator term B * v re-associates the reference's (gamma (1 + w) v) exp(w), so the mode-3
+kernels agree with the mode-2 ones to a few ulps, and whole Newton solves with GS_NO_NEWTON_B (mode 2 inside)
+to far below the 1e-10 field / 1e-9 history tolerances the oracle comparisons use (test_gpu_solver.py,
+test_gpu_zslab.py pin the default path to the reference itself)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import gpusolve as gsv  # noqa: E402
+from gpusolve.devfield import DevField  # noqa: E402
+
+NEWTON, NEWTON_B = gsv.GS_NEWTON, gsv.GS_NEWTON_B
+
+
+def k():
+    assert torch.cuda.is_available(), "GPU tests need a GPU (no CPU fallback exists)"
+    return gsv.kernels()
+
+
+def ok(rc):
+    assert rc == 0, k().gs_strerror(rc).decode()
+
+
+def st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class env:
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        self.old = {k_: os.environ.get(k_) for k_ in self.kw}
+        os.environ.update({k_: str(v) for k_, v in self.kw.items()})
+
+    def __exit__(self, *a):
+        for k_, v in self.old.items():
+            if v is None:
+                del os.environ[k_]
+            else:
+                os.environ[k_] = v
+
+
+def rand_field(rng, dims, lo, hi, interior_only=True):
+    a = np.zeros(tuple(d + 2 for d in dims))
+    if interior_only:
+        a[1:-1, 1:-1, 1:-1] = rng.uniform(lo, hi, dims)
+    else:
+        a[:] = rng.uniform(lo, hi, a.shape)
+    return a
+
+
+def bfac(w, gamma, dims, h):
+    b = DevField(*dims, fill=np.nan)
+    ok(k().gs_newton_bfac(C.byref(w.level(h)), gamma, w.ptr, b.ptr, st()))
+    return b
+
+
+@pytest.mark.parametrize("dims,gamma", [((64, 32, 16), 1.0), ((37, 11, 5), 2.5), ((130, 7, 3), 0.25)])
+def test_bfac_values(dims, gamma):
+    """b = gamma (1 + w) exp(w) at every element of planes -1 .. nz+2 (ghost planes and row padding included),
+    against numpy's exp: ocml's and glibc's exp differ by <= 1 ulp, the product by a few."""
+    rng = np.random.default_rng(7)
+    w = DevField(*dims)
+    w.zyx_ext.copy_(torch.from_numpy(rng.uniform(-3, 3, tuple(w.zyx_ext.shape))))
+    b = bfac(w, gamma, dims, 1.0 / (dims[1] + 1))
+    torch.cuda.synchronize()
+    wv, bv = w.zyx_ext.cpu().numpy(), b.zyx_ext.cpu().numpy()
+    ref = gamma * (1 + wv) * np.exp(wv)
+    assert np.all(np.isfinite(bv))
+    np.testing.assert_allclose(bv, ref, rtol=4e-16 * 8, atol=1e-300)
+
+
+def level_pair(rng, dims):
+    h = 1.0 / (dims[1] + 1)
+    v = DevField(*dims).from_xyz(rand_field(rng, dims, -0.5, 0.5))
+    f = DevField(*dims).from_xyz(rand_field(rng, dims, -2, 2))
+    w = DevField(*dims).from_xyz(rand_field(rng, dims, -0.8, 0.8))
+    return h, v, f, w
+
+
+def close(a, b, rel=1e-13):
+    a, b = a.to_xyz(), b.to_xyz()
+    scale = np.nanmax(np.abs(b))
+    assert np.all(np.isfinite(a) == np.isfinite(b))
+    d = np.nanmax(np.abs(a - b))
+    assert d <= rel * scale, (d, scale)
+
+
+@pytest.mark.parametrize("dims", [(128, 64, 32), (256, 32, 30), (700, 12, 10), (33, 31, 29)])
+def test_mode3_kernels_match_mode2(dims):
+    """Pair (+ norm partials), one sweep, residual, residual + restriction, fused prolongation pair: mode 3 on
+    B = bfac(w) against mode 2 on w, to a few ulps of the fields."""
+    S = gsv.Stencil().to_abi()
+    rng = np.random.default_rng(sum(dims))
+    h, v, f, w = level_pair(rng, dims)
+    b = bfac(w, 1.0, dims, h)
+    L = v.level(h)
+    cd = tuple(d // 2 for d in dims)
+    out2, out3 = DevField(*dims, fill=0.0), DevField(*dims, fill=0.0)
+    # one sweep and the residual (every level shape)
+    ok(k().gs_jacobi_sweep(C.byref(S), C.byref(L), NEWTON, 0.8, 1.0, v.ptr, out2.ptr, f.ptr, w.ptr, st()))
+    ok(k().gs_jacobi_sweep(C.byref(S), C.byref(L), NEWTON_B, 0.8, 1.0, v.ptr, out3.ptr, f.ptr, b.ptr, st()))
+    close(out3, out2)
+    ok(k().gs_residual(C.byref(S), C.byref(L), NEWTON, 1.0, v.ptr, f.ptr, w.ptr, out2.ptr, None, st()))
+    ok(k().gs_residual(C.byref(S), C.byref(L), NEWTON_B, 1.0, v.ptr, f.ptr, b.ptr, out3.ptr, None, st()))
+    close(out3, out2, 1e-12)  # (a residual is a difference of O(1) terms: relative to the largest)
+    # the fused pair, where the level has one
+    if k().gs_jacobi_sweep2_supported_mode(C.byref(S), C.byref(L), NEWTON):
+        for vin in (v.ptr, None):  # a loaded iterate and the zero iterate
+            ok(k().gs_jacobi_sweep2(C.byref(S), C.byref(L), NEWTON, 0.8, 1.0, vin, out2.ptr, f.ptr, w.ptr, 0, 0, st()))
+            ok(k().gs_jacobi_sweep2(C.byref(S), C.byref(L), NEWTON_B, 0.8, 1.0, vin, out3.ptr, f.ptr, b.ptr, 0, 0,
+                                    st()))
+            close(out3, out2)
+    # residual + restriction
+    if all(c >= 1 for c in cd):
+        c2, c3 = DevField(*cd, fill=0.0), DevField(*cd, fill=0.0)
+        Lc = c2.level(1.0 / (cd[1] + 1))
+        ok(k().gs_residual_restrict(C.byref(S), C.byref(L), NEWTON, 1.0, v.ptr, f.ptr, w.ptr, c2.ptr, None,
+                                    C.byref(Lc), st()))
+        ok(k().gs_residual_restrict(C.byref(S), C.byref(L), NEWTON_B, 1.0, v.ptr, f.ptr, b.ptr, c3.ptr, None,
+                                    C.byref(Lc), st()))
+        close(c3, c2, 1e-12)
+        # the fused prolongation pair
+        if k().gs_jacobi_sweep2_prolong_supported(C.byref(S), C.byref(L), NEWTON):
+            cv = DevField(*cd).from_xyz(rand_field(rng, cd, -0.1, 0.1))
+            wsn = k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(S), C.byref(L), NEWTON)
+            ws = torch.empty(max(1, wsn), dtype=torch.float64, device="cuda")
+            for mode, wp, o in ((NEWTON, w.ptr, out2), (NEWTON_B, b.ptr, out3)):
+                ok(k().gs_jacobi_sweep2_prolong_ws(C.byref(S), C.byref(L), mode, 0.8, 1.0, v.ptr, cv.ptr, None,
+                                                   C.byref(Lc), o.ptr, f.ptr, wp, 0, 0, ws.data_ptr(), wsn, st()))
+            close(out3, out2)
+
+
+def solve(params, **e):
+    with env(**e):
+        with gsv.HipGridData(params) as g:
+            hist = gsv.NewtonSolver.solve(g)
+            fields = {(l, n): g.field(l, n) for l in range(g.numLevels()) for n in ("v", "newtonV")}
+    return hist, fields
+
+
+@pytest.mark.parametrize("dims,pre,post", [((127, 127, 127), 2, 2), ((64, 64, 64), 3, 3), ((130, 66, 34), 2, 3),
+                                           ((1100, 20, 18), 2, 2)])
+def test_newton_solve_b_matches_reference_mode(dims, pre, post):
+    """Whole Newton solves: the default (GS_NEWTON_B inner solves) against GS_NO_NEWTON_B (mode 2, the reference's
+    expressions) — histories to 1e-11, level-0 fields to 1e-11 of their magnitude."""
+    p = gsv.GridParams(maxiter=3, tol=0.0, gridDim=dims, mode=NEWTON, preSmoothing=pre, postSmoothing=post)
+    h_ref, f_ref = solve(p, GS_NO_NEWTON_B=1)
+    h_b, f_b = solve(p)
+    assert np.all(np.isfinite(h_ref)), h_ref
+    assert len(h_b) == len(h_ref)
+    for a, c in zip(h_b, h_ref):
+        assert abs(a - c) <= 1e-11 * abs(c), (a, c)
+    for n in ("v", "newtonV"):
+        a, c = f_b[(0, n)], f_ref[(0, n)]
+        assert np.abs(a - c).max() <= 1e-11 * np.abs(c).max(), n

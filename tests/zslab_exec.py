@@ -456,6 +456,9 @@ class Rank:
                 W = self.op_newton_update(L)
                 if kv.get("restrict"):
                     self.op_newton_update_restrict(L, Ls[kv["L"] + 1], W)
+                if kv.get("bfac"):  # the next inner solve's factor of this level, from w'
+                    self.bmode = True
+                    L.fields["bfacW"] = W.copy()
             elif op == "ghostsum":  # a ghost plane of the new newtonV: newtonV + 1.0 v (the axpy's value)
                 g = L.local_to_global(kv["plane"])
                 L.fields["vAlt"][:, :, L.idx(g)] = L.fields["newtonV"][:, :, L.idx(g)] + 1.0 * L.fields["v"][:, :, L.idx(g)]
