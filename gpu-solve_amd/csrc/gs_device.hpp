@@ -128,7 +128,7 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_RB_ZC=n           z-chunk of the one-point passes (k_rb sweeps / residuals, the Newton update pass) (A/B)
 //   GS_NEWTON_XH=0       NEWTON plain pairs on rows of 513-1024 points through k_tb2 instead of column blocks (A/B)
 //   GS_SPEC_CACHED=1     pairs with norm partials store through the caches, not non-temporally (A/B)
-//   GS_RR_NG=1|2         k_rr2 groups of coarse rows per block (default: 2 on levels of >= 2^26 points)
+//   GS_RR_NG=2           k_rr2 with two groups of coarse rows per block (default 1: measured faster, r05b)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh, specCached;
     int xhSwizzle, midZc, rrZc, rrZcBig, oneRoundMid, rbZc;

@@ -370,11 +370,12 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         const bool big = fl->nx * fl->ny * fl->nz >= ((int64_t)1 << RR2_NR2_LOG2_POINTS);
         // (NEWTON with two rows spills 19 VGPRs: 40.5 vs 38.9 ms per 512^3 Newton iteration, gpurun_out/rrn)
         const int nr = mode == GS_LINEAR && (nr_env == 2 || (nr_env == 0 && big)) ? 2 : 1;
-        // groups of coarse rows per block (k_rr2 NG): two on levels of >= 2^26 points whose rows fit twice in
-        // a block, for the kernels at two waves per SIMD (LINEAR two-row, NEWTON: the 8-wave block is what a CU
-        // holds anyway; NONLINEAR's 157-VGPR form would lose its third wave per SIMD); GS_RR_NG=1|2 forces it (A/B)
-        const bool ngAuto = big && (nr == 2 || newtonish(mode));
-        const int ng = (kKnobs.rrNg == 1 || (kKnobs.rrNg == 0 && !ngAuto) || 2 * wxs > RR2_WXMAX) ? 1 : 2;
+        // groups of coarse rows per block (k_rr2 NG; GS_RR_NG=2 where the rows fit twice in a block, A/B): two
+        // y-neighbour rows in one 8-wave block cut the 512^3 launch's PMC reads from 1.139 to 1.089 x algorithmic
+        // (NEWTON 1.157 -> 1.087) but run slower — k_rr2 0.479-0.512 vs 0.406-0.453 ms, V-cycle 2.111 vs
+        // 2.055-2.065 ms, Newton 33.4-33.9 vs 32.8-33.4 ms (r05b, interleaved): two 4-wave blocks per CU at their
+        // own barrier phases hide more latency than the halo rows the shared block saves; default one group
+        const int ng = (kKnobs.rrNg == 2 && 2 * wxs <= RR2_WXMAX) ? 2 : 1;
         const int64_t rows = (cl->ny + nr * ng - 1) / (nr * ng); // blocks along y
         const int64_t chunks = (2048 + rows - 1) / rows;
         int64_t zc = (cl->nz + chunks - 1) / chunks;

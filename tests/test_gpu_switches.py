@@ -33,7 +33,7 @@ CASES = {
     "linear2e26": ((0, 512, 512, 256, 2), [("GS_RR_NR", "1"), ("GS_PAIR_BIG_CHUNKS", "0"), ("GS_RR_NTU", "0"),
                                            ("GS_RR_ZC_BIG", "7")]),
     "linear512": ((0, 512, 512, 512, 2), [("GS_PAIR_ONE_ROUND", "0"), ("GS_PAIR_ZC", "96"), ("GS_RR_REVERSE", "0"),
-                                          ("GS_SPEC_CACHED", "1"), ("GS_RR_NG", "1")]),
+                                          ("GS_SPEC_CACHED", "1"), ("GS_RR_NG", "2")]),
     "linear_rows700": ((0, 700, 64, 64, 3), [("GS_PAIR_XH", "0"), ("GS_TBX_PFD", "1"), ("GS_XH_SWIZZLE", "0")]),
     # two loopback slabs of 512^3: the interior launches of the overlapped sweeps (z0 != 0)
     "slabs512": ((0, 512, 512, 1024, 2, 2, 2, 2), [("GS_SLAB_ZC", "16"), ("GS_HALO_ORDER", "1")]),
