@@ -1,9 +1,9 @@
 #!/bin/bash
 # Interleaved A/B of two builds of the kernel library on the headline bench (and optionally Newton): the
-# alternative libgpusolve_hip.so is built here into gpu-solve_amd/lib_alt/ and swapped in between runs.
+# alternative libgpusolve_hip.so is built here into gpu-solve_amd/lib_exp/ (tools/exp_builds.sh; scratch, deleted after the round) and swapped in between runs.
 #   tools/lib_ab_session.sh <tag> [rounds] [newton-iters] [alt .so]   (through gpurun, from the repo root)
 set -o pipefail
-O=gpurun_out/${1:-libab}; R=${2:-3}; NI=${3:-0}; ALT=${4:-gpu-solve_amd/lib_alt/libgpusolve_hip.so}; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/${1:-libab}; R=${2:-3}; NI=${3:-0}; ALT=${4:-gpu-solve_amd/lib_exp/alt/libgpusolve_hip.so}; mkdir -p $O; export TMPDIR=/tmp
 L=gpu-solve_amd/lib
 cp $L/libgpusolve_hip.so $O/new.so
 restore() { cp $O/new.so $L/libgpusolve_hip.so; }
