@@ -583,7 +583,7 @@ def main():
     single = ceilings = ceiling = None
     if world == 1:
         single = single_sweep_timing(grid, dims, a.steps)
-        ceilings = stream_ceilings(int(dims[0]) * dims[1] * dims[2])
+        ceilings = stream_ceilings((int(dims[0]) * dims[1] * dims[2]) & ~1)  # (the probe streams element pairs)
         ceiling = ceilings["triad"]
 
     lups_per_rank = float(dims[0]) * dims[1] * dims[2] / world

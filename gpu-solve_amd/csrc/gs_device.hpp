@@ -355,40 +355,6 @@ __device__ __forceinline__ double newton_E(double w)
     return MODE == GS_NEWTON_B ? 1.0 : exp(w);
 }
 
-// GS_NEWTON_B's Jacobi quotient r / den (den = preFac + B) through den's refined reciprocal y = hh_recip(den), the
-// reciprocal the compiler's fp64 division forms (rcp + two Newton steps, see div_hh): q = r y, q' = fma(fma(-den, q,
-// r), y, q) is the division's unscaled path, bit for bit, when div_scale / div_fmas / div_fixup leave the operands
-// alone. Taken for den's biased exponent in [923, 1123] (|den| in [2^-100, 2^101)) and r's in [124, 1623]: then
-// r / den lies in [2^-999, 2^701), no operand or quotient is denormal, the exponent gap stays below 768, r's
-// exponent is above 53, so nothing is scaled; otherwise (zero, denormal, inf / nan, extreme values) r / den.
-// The fused pairs form y ONCE per point and pass and share it between the point's two sweeps (k_tb2y), so the
-// division's ~11 operations become 3 per sweep (+5 for y). GS_NO_NEWTON_RCP: timing-only build without it.
-__device__ __forceinline__ bool rcp_den_ok(double den)
-{
-    const unsigned e = ((unsigned)__double2hiint(den) >> 20) & 0x7ffu;
-    return e - 923u < 201u;
-}
-__device__ __forceinline__ double div_by_recip(double r, double den, double y)
-{
-    if (rcp_den_ok(den) && div_hh_fast_ok(r)) {
-        const double q = r * y;
-        const double e = __builtin_fma(-den, q, r);
-        return __builtin_fma(e, y, q);
-    }
-    return r / den;
-}
-// the NEWTON_B update from the point's B (A) and y = hh_recip(preFac + B)
-__device__ __forceinline__ double newton_update_y(const Coef& k, double v, double r, double B, double y)
-{
-    const double den = k.preFac + B;
-    return v + k.omega * div_by_recip(r, den, y);
-}
-#ifdef GS_NO_NEWTON_RCP
-constexpr bool kNewtonRcp = false;
-#else
-constexpr bool kNewtonRcp = true;
-#endif
-
 __device__ __forceinline__ double wave_sum(double x)
 {
 #pragma unroll
@@ -2214,9 +2180,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // newtonV rows at z-1 and reads E = exp(w) from LDS (same expressions, same values)
     // NEWTON column blocks (XH) likewise: their edge-column state leaves no room for Aprev / Eprev / Fprev
     constexpr bool RECOMP = newtonish(MODE) && (PRO != 0 || XH);
-    // RCPM (GS_NEWTON_B): the E slots carry y = hh_recip(preFac + B) instead (newton_update_y), shared by the sweeps
-    constexpr bool RCPM = MODE == GS_NEWTON_B && kNewtonRcp;
-    constexpr bool ELDS = RECOMP && (MODE == GS_NEWTON || RCPM); // E / y in LDS (GS_NEWTON_B alone: E = 1)
+    constexpr bool ELDS = RECOMP && MODE == GS_NEWTON; // E in LDS (GS_NEWTON_B: E = 1, A = B from wprev_l)
     constexpr bool WLDS = RECOMP && PRO != 0; // the coarse X-pass rows in LDS (prolongation pairs)
     // (Wprev, Fprev: sweep 2's newtonV / f rows at z-1, in LDS like the coarse rows below)
     __shared__ double2 wprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
@@ -2551,25 +2515,17 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 #ifdef GS_EXP_EFIELD
                         const double2 E = XL[cs][j];
 #else
-                        const double2 E = RCPM ? make_double2(hh_recip(k.preFac + A.x), hh_recip(k.preFac + A.y))
-                                               : make_double2(newton_E<MODE>(wv.x), newton_E<MODE>(wv.y));
+                        const double2 E = make_double2(newton_E<MODE>(wv.x), newton_E<MODE>(wv.y));
 #endif
                         if (!RECOMP && j >= 1) {
                             Acur[j - 1] = A;
                             Ecur[j - 1] = E;
                         }
                         if (ELDS && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
-                        if constexpr (RCPM) {
-                            a0 = newton_op(q[0], c.x, A.x, 1.0);
-                            a1 = newton_op(q[1], c.y, A.y, 1.0);
-                            n0 = newton_update_y(k, c.x, FL[cs][j].x - a0, A.x, E.x);
-                            n1 = newton_update_y(k, c.y, FL[cs][j].y - a1, A.y, E.y);
-                        } else {
-                            a0 = newton_op(q[0], c.x, A.x, E.x);
-                            a1 = newton_op(q[1], c.y, A.y, E.y);
-                            n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
-                            n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
-                        }
+                        a0 = newton_op(q[0], c.x, A.x, E.x);
+                        a1 = newton_op(q[1], c.y, A.y, E.y);
+                        n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
+                        n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
                     } else {
                         a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                         a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
@@ -2609,16 +2565,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                                 A = Aprev[j - 1];
                                 E = Eprev[j - 1];
                             }
-                            const double a0 = newton_op(q[0], c.x, A.x, RCPM ? 1.0 : E.x);
-                            const double a1 = newton_op(q[1], c.y, A.y, RCPM ? 1.0 : E.y);
+                            const double a0 = newton_op(q[0], c.x, A.x, E.x);
+                            const double a1 = newton_op(q[1], c.y, A.y, E.y);
                             const double2 fp = RECOMP ? fprev_l[j - 1][wx + WX * wy][lane] : Fprev[j - 1];
-                            if constexpr (RCPM) {
-                                o0 = newton_update_y(k, c.x, fp.x - a0, A.x, E.x);
-                                o1 = newton_update_y(k, c.y, fp.y - a1, A.y, E.y);
-                            } else {
-                                o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
-                                o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
-                            }
+                            o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
+                            o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
                         } else {
                             const double a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                             const double a1 = op_finish<MODE>(k, q[1], c.y, 0.0);

@@ -388,16 +388,6 @@ __global__ __launch_bounds__(256) void k_div_check(const double* __restrict__ a,
     ref[i] = a[i] / k.hh;
 }
 
-// div_by_recip (GS_NEWTON_B's quotient through den's refined reciprocal) against the IEEE division, per pair
-__global__ __launch_bounds__(256) void k_div_recip_check(const double* __restrict__ r, const double* __restrict__ den,
-                                                         int64_t n, double* __restrict__ fast, double* __restrict__ ref)
-{
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fast[i] = div_by_recip(r[i], den[i], hh_recip(den[i]));
-    ref[i] = r[i] / den[i];
-}
-
 __global__ __launch_bounds__(256) void k_triad(double* __restrict__ out, const double* __restrict__ a,
                                                const double* __restrict__ b, int64_t n2)
 {
@@ -640,14 +630,6 @@ int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, doub
     k.hh = hh;
     k.fastdiv = hh >= 0x1p-120 && hh <= 1.0;
     hipLaunchKernelGGL(k_div_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, n, k, fast, ref);
-    return launch_status();
-}
-
-int gs_debug_div_recip_check(const double* r, const double* den, int64_t n, double* fast, double* ref, hipStream_t st)
-{
-    if (!r || !den || !fast || !ref || n < 0) return GS_EINVAL;
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_div_recip_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, r, den, n, fast, ref);
     return launch_status();
 }
 

@@ -42,32 +42,3 @@ def test_div_hh_bitwise(n):
     assert np.array_equal(rb[~nan], want[~nan])
 
 
-
-def test_div_by_recip_bitwise():
-    """GS_NEWTON_B's Jacobi quotient r / den through den's refined reciprocal (div_by_recip: rcp + two Newton steps,
-    then the division's unscaled tail) against the IEEE division, bit for bit: every binade of r against
-    denominators across and beyond the window [2^-100, 2^101) (both signs, zero, denormals, inf / nan, the
-    edges), and the denominators the solver meets (preFac + B, preFac = 6 (n+1)^2)."""
-    rng = np.random.default_rng(20261018)
-    r = numerators(rng)
-    m = r.size
-    de = rng.integers(-1074, 1024, m)
-    den = np.ldexp(rng.uniform(1.0, 2.0, m), de) * rng.choice([-1.0, 1.0], m)
-    edges = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, np.ldexp(1.0, -100), np.ldexp(1.0, -101),
-                      np.nextafter(np.ldexp(1.0, -100), 0), np.ldexp(1.0, 101), np.nextafter(np.ldexp(1.0, 101), 0),
-                      np.ldexp(1.0, 102), 1.0, -1.0, 3.0])
-    den[: edges.size] = edges
-    # solver-like: preFac + B, B = gamma (1 + w) e^w with w in [-3, 3]
-    w = rng.uniform(-3, 3, m // 2)
-    den[edges.size: edges.size + w.size] = 6.0 * 513.0 ** 2 + (1 + w) * np.exp(w)
-    rng.shuffle(r)
-    R, D = torch.from_numpy(r).cuda(), torch.from_numpy(den).cuda()
-    fast, ref = torch.empty_like(R), torch.empty_like(R)
-    assert gsv.diag().gs_debug_div_recip_check(R.data_ptr(), D.data_ptr(), R.numel(), fast.data_ptr(),
-                                               ref.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
-    torch.cuda.synchronize()
-    fb, rb = fast.cpu().numpy().view(np.uint64), ref.cpu().numpy().view(np.uint64)
-    nan = np.isnan(ref.cpu().numpy())
-    bad = np.nonzero((fb != rb) & ~nan)[0]
-    assert bad.size == 0, [(r[i], den[i], fast[i].item(), ref[i].item()) for i in bad[:5]]
-    assert np.all(np.isnan(fast.cpu().numpy()[nan]))
