@@ -201,7 +201,9 @@ double* gs_grid_field(void* grid, int level, int field)
     switch (field) {
     case 0: return L.v ? L.v.data() : nullptr;
     case 1: return L.restV ? L.restV.data() : nullptr;
-    case 2: return L.newtonV ? L.newtonV.data() : nullptr;
+    case 2: // (a caller may write through the pointer: the driver no longer assumes newtonV = 0)
+        g.newtonVTouched();
+        return L.newtonV ? L.newtonV.data() : nullptr;
     case 3: return L.f ? L.f.data() : nullptr;
     case 4: return L.r ? L.r.data() : nullptr;
     case 5: return (level == 0 && g.newtonF) ? g.newtonF.data() : nullptr;

@@ -1674,6 +1674,12 @@ __global__ __launch_bounds__(256) void k_bfac(double* __restrict__ b, const doub
     }
 }
 
+__global__ __launch_bounds__(256) void k_fill(double* __restrict__ dst, double value, int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = value;
+}
+
 __global__ __launch_bounds__(256) void k_axpy(double* __restrict__ y, const double* __restrict__ x, double a,
                                               int64_t n)
 {

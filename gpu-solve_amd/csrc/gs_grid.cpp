@@ -251,6 +251,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
             }
     }
     if (mode == NEWTON) newtonF = DeviceField(levels_[0].geom.nx, levels_[0].geom.ny, levels_[0].geom.nz, s, dry);
+    newtonVZero_ = mode == NEWTON; // (every field is created zero-filled)
     {
         const char* e = std::getenv("GS_METRICS");
         clock.on = !dry && e && *e && *e != '0';
@@ -1284,6 +1285,7 @@ double NewtonSolver::compFUpdate(HipGridData& grid)
               "gs_newton_F_update");
     grid.newtonR1_ = r1;
     grid.bfacFresh_ = bf ? 1u : 0u;
+    grid.newtonVZero_ = false;
     if (L0.distributed && grid.nranks() > 1) {
         // the ghost planes of w' = newtonV + v (see fusedUpdate)
         const int64_t ldz = L0.v.ldz();
@@ -1305,7 +1307,10 @@ double NewtonSolver::compFUpdate(HipGridData& grid)
 // NewtonSolver.cpp:83-108
 bool NewtonSolver::findError(HipGridData& grid)
 {
-    for (std::size_t i = 1; i + 1 < grid.numLevels(); i++) {
+    // newtonV is still the zero every level's field was created with (the first Newton iteration): its
+    // restrictions are those zeros (nothing to compute) and every factor is B = gamma (1 + 0) exp(0) = gamma
+    const bool zeroW = grid.newtonVZero_;
+    for (std::size_t i = 1; !zeroW && i + 1 < grid.numLevels(); i++) {
         if (i == 1 && grid.newtonR1_) { // restricted by the last compFUpdate; level 0's newtonV unchanged since
             grid.getLevel(1).newtonV.swap(grid.getLevel(1).newtonVNext);
             if (grid.trace) grid.rec("swapnewton", {{"L", 1}});
@@ -1322,6 +1327,10 @@ bool NewtonSolver::findError(HipGridData& grid)
             auto& L = grid.getLevel(i);
             if (i < 32 && (grid.bfacFresh_ >> i) & 1u) continue; // written by the last compFUpdate pass
             if (grid.trace) grid.rec("bfac", {{"L", (long long)i}});
+            else if (zeroW) // (planes -1 .. nz+2, as gs_newton_bfac covers)
+                check(gs_fill(L.bfac.data() - L.bfac.ldz(), grid.gamma * (1 + 0.0) * std::exp(0.0),
+                              L.bfac.ldz() * (L.geom.nz + 4), grid.stream()),
+                      "gs_fill");
             else check(gs_newton_bfac(&L.geom, grid.gamma, L.newtonV.data(), L.bfac.data(), grid.stream()), "gs_newton_bfac");
         }
         grid.newtonB_ = true;
@@ -1354,6 +1363,7 @@ bool NewtonSolver::findError(HipGridData& grid)
     if (grid.trace) grid.rec("axpy", {{"L", 0}}, "newtonV+=v");
     else check(gs_axpy(L0.newtonV.data(), L0.v.data(), 1.0, L0.v.span(), grid.stream()), "gs_axpy");
     grid.newtonR1_ = false;
+    grid.newtonVZero_ = false;
     return false;
 }
 

@@ -191,6 +191,8 @@ public:
     {
         return newtonB_ ? L.bfac.data() : (L.newtonV ? L.newtonV.data() : nullptr);
     }
+    // newtonV may have been written from outside the solvers (the C ABI's field pointer): see newtonVZero_
+    void newtonVTouched() { newtonVZero_ = false; }
     // ghost planes of a distributed level's field (no-op otherwise); depth 2 where possible for
     // iterate fields (the fused pair reads two ghost planes of v)
     void halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth = 1);
@@ -229,6 +231,7 @@ private:
     bool newtonR1_ = false;    // level 1's newtonVNext holds R(level 0's newtonV) (gs_newton_F_update_restrict)
     bool newtonB_ = false;     // every level's bfac holds B of its current newtonV (set for the inner solve)
     unsigned bfacFresh_ = 0;   // bit l: level l's bfac already holds B of the newtonV the next findError uses
+    bool newtonVZero_ = false; // every level's newtonV is still the zero of grid creation (the first findError)
     double haloCurMs_ = 0.0;   // host ms spent on that exchange so far
     double traceNorm();
     friend class HipSolver;

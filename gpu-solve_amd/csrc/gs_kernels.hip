@@ -558,6 +558,16 @@ int gs_newton_bfac(const gs_level* L, double gamma, const double* w, double* b, 
     return launch_status();
 }
 
+int gs_fill(double* dst, double value, int64_t n, hipStream_t st)
+{
+    if (!dst || n < 0) return GS_EINVAL;
+    if (n == 0) return 0;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(256), 0, st, dst, value, n);
+    return launch_status();
+}
+
 int gs_copy(double* dst, const double* src, int64_t n, hipStream_t st)
 {
     if (!dst || !src || n < 0) return GS_EINVAL;

@@ -108,6 +108,7 @@ KERNEL_API = {
     "gs_newton_bfac": (C.c_int, [C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_newton_F_update": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gs_fill": (C.c_int, [C.c_void_p, C.c_double, i64, C.c_void_p]),
     "gs_copy": (C.c_int, [C.c_void_p, C.c_void_p, i64, C.c_void_p]),
     "gs_axpy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_double, i64, C.c_void_p]),
     "gs_coarse_cycle_max_levels": (C.c_int, []),

@@ -243,6 +243,9 @@ int gs_newton_F_update_restrict_bfac(const gs_stencil* S, const gs_level* L, dou
  * row padding included), so a Z-slab's B is current wherever its w is. w and b must not overlap. */
 int gs_newton_bfac(const gs_level* L, double gamma, const double* w, double* b, hipStream_t stream);
 
+/* dst[i] = value for i < n (Vector3::fill, src/cpu/Vector3.cpp:29-32). */
+int gs_fill(double* dst, double value, int64_t n, hipStream_t stream);
+
 /* dst[i] = src[i] for i < n (Vector3 copy-assignment: NewtonSolver.cpp:12 newtonF = f), non-temporal
  * streams; the buffers must not overlap unless dst == src. */
 int gs_copy(double* dst, const double* src, int64_t n, hipStream_t stream);
