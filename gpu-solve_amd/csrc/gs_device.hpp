@@ -53,6 +53,8 @@ constexpr int WAVE = 64;
 // NEWTON's two forms (include/gpusolve_hip.h): GS_NEWTON reads newtonV as w, GS_NEWTON_B reads the precomputed
 // linearisation factor B = gamma (1 + newtonV) exp(newtonV) (gs_newton_bfac) as w. Both carry a w operand.
 constexpr bool newtonish(int m) { return m == GS_NEWTON || m == GS_NEWTON_B; }
+// GS_NEWTON_G (the first Newton iteration: B = gamma everywhere) launches the GS_NEWTON_B kernels with Coef::bconst
+constexpr int base_mode(int m) { return m == GS_NEWTON_G ? GS_NEWTON_B : m; }
 
 // compile-time / run-time booleans for code specialised per wave (BoolC) or selected per use (RtBool)
 template <bool B>
@@ -79,6 +81,8 @@ struct Coef {
     int zq;        // every s[i] finite and hh a positive normal number: the stencil sum of an identically zero
                    // iterate over hh is exactly +0 (each s[i] * 0 is a signed zero, +0 plus a signed zero is
                    // +0, +0 / hh is +0), so zero-iterate sweeps take q = +0 without evaluating it
+    int bconst;     // GS_NEWTON_B with B = gamma at every point (the first Newton iteration's factor): the pair and
+                    // k_rr2 take k.gamma instead of loading w (which still holds gamma for every other kernel)
     int64_t off[7]; // generic kernel: linear element offsets of the 7 entries
 #ifdef GS_EXP_EFIELD
     int64_t efoff;
@@ -157,7 +161,7 @@ const Knobs kKnobs;
 int64_t gs_exp_efoff = 0; // set by gs_exp_set_efoff (gs_kernels.hip, this build only)
 #endif
 
-Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamma)
+Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamma, int bconst = 0)
 {
     Coef k;
     for (int i = 0; i < 7; i++) {
@@ -175,6 +179,7 @@ Coef make_coef(const gs_stencil* S, const gs_level* L, double omega, double gamm
     k.swz = kKnobs.xhSwizzle;
     k.zq = kKnobs.zeroQ && std::isnormal(k.hh) && k.hh > 0.0;
     for (int i = 0; i < 7; i++) k.zq = k.zq && std::isfinite(S->s[i]);
+    k.bconst = bconst;
 #ifdef GS_EXP_EFIELD
     k.efoff = gs_exp_efoff;
 #endif
@@ -1151,7 +1156,10 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             VB[s][j] = uv ? ld2s<true>(at(v, j + 1, p + 2)) : ld2(at(v, j + 1, p + 2));
             F0[s][j] = uf ? ld2s<true>(at(f, j + 1, p)) : ld2(at(f, j + 1, p));
             F1[s][j] = uf ? ld2s<true>(at(f, j + 1, p + 1)) : ld2(at(f, j + 1, p + 1));
-            if (newtonish(MODE)) {
+            if (MODE == GS_NEWTON_B && k.bconst) {
+                W0[s][j] = make_double2(k.gamma, k.gamma);
+                W1[s][j] = W0[s][j];
+            } else if (newtonish(MODE)) {
                 W0[s][j] = uf ? ld2s<true>(at(w, j + 1, p)) : ld2(at(w, j + 1, p));
                 W1[s][j] = uf ? ld2s<true>(at(w, j + 1, p + 1)) : ld2(at(w, j + 1, p + 1));
             }
@@ -1237,7 +1245,9 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
             Vq[j] = ld2(at(v, j + 1, p));
             V0[j] = ld2(at(v, j + 1, p + 1));
             Fq[j] = ld2(at(f, j + 1, p));
-            Wq[j] = newtonish(MODE) ? ld2(at(w, j + 1, p)) : make_double2(0.0, 0.0);
+            Wq[j] = (MODE == GS_NEWTON_B && k.bconst) ? make_double2(k.gamma, k.gamma)
+                    : newtonish(MODE)                  ? ld2(at(w, j + 1, p))
+                                                       : make_double2(0.0, 0.0);
         }
         Hq[0] = ld2(at(v, 0, p));
         Hq[1] = ld2(at(v, RR + 1, p));
@@ -2189,7 +2199,11 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // 0.986-0.990 ms per 512^3 launch with the LDS state, profiles/r05/r05g_newton_b_norecomp_touch_ab.txt)
     constexpr bool RECOMP = newtonish(MODE) && ((PRO != 0 && MODE == GS_NEWTON) || XH);
     constexpr bool ELDS = RECOMP && MODE == GS_NEWTON; // E in LDS (GS_NEWTON_B: E = 1, A = B from wprev_l)
+#ifdef GS_EXP_LPRO2
+    constexpr bool WLDS = PRO != 0 && (newtonish(MODE) || PFD == 2);
+#else
     constexpr bool WLDS = newtonish(MODE) && PRO != 0; // the coarse X-pass rows in LDS (prolongation pairs)
+#endif
     // (Wprev, Fprev: sweep 2's newtonV / f rows at z-1, in LDS like the coarse rows below)
     __shared__ double2 wprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
     __shared__ double2 fprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
@@ -2241,8 +2255,10 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         if (pfld <= 2) {
             if constexpr (PRO != 0) val = psr[((int64_t)(zz + 1) * 4 + dx) * (ny + 2)];
             else if constexpr (!ZV) val = v[(xe + dx) + proff + (int64_t)zz * ldz];
-        } else if (pfld <= 4) {
-            val = (pfld == 3 ? f : w)[xe + proff + (int64_t)z * ldz];
+        } else if (pfld == 3) {
+            val = f[xe + proff + (int64_t)z * ldz];
+        } else if (pfld == 4) {
+            val = (MODE == GS_NEWTON_B && k.bconst) ? k.gamma : w[xe + proff + (int64_t)z * ldz];
         }
         EPS[s] = val;
     };
@@ -2253,7 +2269,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
         for (int j = 0; j < NV; j++) {
             VL[s][j] = ldv2<ZV>(at(v, j, zv));
             FL[s][j] = ld2s<NTF>(at(f, j, z));
-            if (newtonish(MODE)) WL[s][j] = ld2(at(w, j, z));
+            if (MODE == GS_NEWTON_B && k.bconst) WL[s][j] = make_double2(k.gamma, k.gamma);
+            else if (newtonish(MODE)) WL[s][j] = ld2(at(w, j, z));
 #ifdef GS_EXP_EFIELD
             if (MODE == GS_NEWTON) XL[s][j] = ld2(at(w, j, z) + k.efoff);
 #endif
@@ -2891,6 +2908,7 @@ int launch_pass(const gs_stencil* S, const gs_level* L, int mode, double omega, 
 {
     // v == NULL: the zero iterate (sweeps only, not in NONLINEAR mode, whose coarse iterates are
     // restrictions, never zero)
+    mode = base_mode(mode); // (GS_NEWTON_G: the one-point passes read the factor field, which holds gamma)
     if (!S || bad_level(L) || !valid_stencil(S) || (!v && (KIND != 0 || mode == GS_NONLINEAR))) return GS_EINVAL;
     if (mode < GS_LINEAR || mode > GS_NEWTON_B || (KIND == 2 && mode != GS_NONLINEAR)) return GS_EINVAL;
     if (L->nx == 0 || L->ny == 0 || L->nz == 0) return 0;

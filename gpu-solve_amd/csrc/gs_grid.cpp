@@ -177,6 +177,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         sw.newtonFusedUpdate = !on("GS_NO_NEWTON_FUSED_UPDATE");
         sw.newtonB = !on("GS_NO_NEWTON_B");
         if (const char* e = std::getenv("GS_NEWTON_B_FUSED")) sw.newtonBFused = std::atoi(e) != 0;
+        sw.newtonG = !on("GS_NO_NEWTON_G");
         if (const char* e = std::getenv("GS_NEWTON_PRO_POINTS")) sw.newtonProPoints = std::strtoll(e, nullptr, 10);
         if (const char* e = std::getenv("GS_TILE_POINTS")) sw.tilePoints = std::strtoll(e, nullptr, 10);
         if (const char* e = std::getenv("GS_HALO_ORDER")) sw.haloOrder = std::atoi(e);
@@ -1334,6 +1335,7 @@ bool NewtonSolver::findError(HipGridData& grid)
             else check(gs_newton_bfac(&L.geom, grid.gamma, L.newtonV.data(), L.bfac.data(), grid.stream()), "gs_newton_bfac");
         }
         grid.newtonB_ = true;
+        grid.bconst_ = zeroW && grid.sw.newtonG; // B = gamma everywhere: GS_NEWTON_G
     }
     grid.bfacFresh_ = 0;
 
@@ -1348,10 +1350,10 @@ bool NewtonSolver::findError(HipGridData& grid)
     try {
         HipSolver::solve(grid);
     } catch (...) {
-        grid.newtonB_ = false;
+        grid.newtonB_ = grid.bconst_ = false;
         throw;
     }
-    grid.newtonB_ = false; // newtonV changes next (newtonV += v): the factors are stale from here on
+    grid.newtonB_ = grid.bconst_ = false; // newtonV changes next (newtonV += v): the factors are stale from here on
     HipSolver::history = keep;
     grid.printProgress = keepPrint;
     grid.maxiter = origIter;

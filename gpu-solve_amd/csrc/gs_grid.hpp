@@ -155,6 +155,8 @@ public:
                              // precomputed factor B (GS_NEWTON_B: exp(newtonV) once per point and Newton iteration)
         bool newtonBFused = true; // GS_NEWTON_B_FUSED=0: level 0's factor from its own gs_newton_bfac pass instead
                                   // of the compF update pass (bit-identical)
+        bool newtonG = true; // GS_NO_NEWTON_G: the first Newton iteration's inner solve reads its factor fields (all
+                             // gamma) instead of taking gamma in the pairs and k_rr2 (GS_NEWTON_G; bit-identical)
         int64_t tilePoints = (int64_t)1 << 18; // GS_TILE_POINTS: levels of at most this many points (replicated,
                                                // LINEAR) run the tiled one-launch down/up-leg steps; 0 = off
         int64_t newtonProPoints = (int64_t)1 << 24; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
@@ -186,7 +188,7 @@ public:
 
     // the mode and the w operand the V-cycle's kernels take: GS_NEWTON_B and B while findError's inner solve runs
     // with the factor fields current (newtonB_), else the grid's mode and newtonV (reference expressions)
-    int kmode() const { return newtonB_ ? GS_NEWTON_B : (int)mode; }
+    int kmode() const { return newtonB_ ? (bconst_ ? GS_NEWTON_G : GS_NEWTON_B) : (int)mode; }
     const double* wOf(const LevelData& L) const
     {
         return newtonB_ ? L.bfac.data() : (L.newtonV ? L.newtonV.data() : nullptr);
@@ -230,6 +232,7 @@ private:
     friend class NewtonSolver;
     bool newtonR1_ = false;    // level 1's newtonVNext holds R(level 0's newtonV) (gs_newton_F_update_restrict)
     bool newtonB_ = false;     // every level's bfac holds B of its current newtonV (set for the inner solve)
+    bool bconst_ = false;      // ... and that B is gamma everywhere (newtonV = 0, the first iteration): GS_NEWTON_G
     unsigned bfacFresh_ = 0;   // bit l: level l's bfac already holds B of the newtonV the next findError uses
     bool newtonVZero_ = false; // every level's newtonV is still the zero of grid creation (the first findError)
     double haloCurMs_ = 0.0;   // host ms spent on that exchange so far

@@ -40,6 +40,7 @@ int gs_jacobi_sweep_norm(const gs_stencil* S, const gs_level* L, int mode, doubl
                          const double* v_in, double* v_out, const double* f, const double* w, double* partials,
                          hipStream_t st)
 {
+    mode = base_mode(mode);
     if (!v_out || !f || v_in == v_out || (newtonish(mode) && !w)) return GS_EINVAL;
     if (partials && L && (L->nx == 0 || L->ny == 0 || L->nz == 0))
         return (int)hipMemsetAsync(partials, 0, sizeof(double), st);
@@ -50,6 +51,7 @@ int gs_jacobi_sweep2_supported_mode(const gs_stencil* S, const gs_level* L, int 
 {
     int zc;
     dim3 g, b;
+    mode = base_mode(mode);
     if (mode < GS_LINEAR || mode > GS_NEWTON_B) return 0;
     return (!bad_level(L) && valid_stencil(S)) ? tb2_plan(S, L, &zc, &g, &b, nullptr, mode) : 0;
 }
@@ -76,6 +78,7 @@ const char* gs_jacobi_sweep2_kernel(const gs_stencil* S, const gs_level* L, int 
     int zc;
     dim3 g, b;
     bool y2 = false, xh = false;
+    mode = base_mode(mode);
     if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh)) return "";
     if (y2) return "k_tb2y: 4x2 waves, 2 rows per wave, LDS halo-row exchange, per-wave-row code";
     if (xh) return "k_tb2y XH: 512-point column blocks of 4x2 waves, edge columns computed lane-parallel";
@@ -86,6 +89,7 @@ int64_t gs_jacobi_sweep2_num_partials(const gs_stencil* S, const gs_level* L, in
 {
     int zc;
     dim3 g, b;
+    mode = base_mode(mode);
     if (bad_level(L) || !valid_stencil(S) || !tb2_plan(S, L, &zc, &g, &b, nullptr, mode)) return 0;
     return (int64_t)g.x * g.y;
 }
@@ -97,11 +101,14 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
     int zc;
     dim3 g, b;
     bool y2 = false, xh = false;
+    // GS_NEWTON_G: the GS_NEWTON_B kernels take gamma for the factor instead of loading it (Coef::bconst)
+    const int bconst = mode == GS_NEWTON_G;
+    mode = base_mode(mode);
     if (!S || bad_level(L) || !valid_stencil(S) || !v_out || !f || v_in == v_out || (!v_in && mode == GS_NONLINEAR) ||
         (newtonish(mode) && !w) || mode < GS_LINEAR || mode > GS_NEWTON_B ||
         !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh))
         return GS_EINVAL;
-    const Coef k = make_coef(S, L, omega, gamma);
+    const Coef k = make_coef(S, L, omega, gamma, bconst);
     const int nx = (int)L->nx, ny = (int)L->ny, nz = (int)L->nz;
 #define GS_TB(M, Z) hipLaunchKernelGGL((k_tb2<M, TB_RY_B, TB_WX_B, true, false, Z>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr)
     // LINEAR zero-iterate pairs (the first sweep of a coarse level, v = 0: the lightest variant, three
@@ -164,6 +171,7 @@ int gs_jacobi_sweep2_prolong_supported(const gs_stencil* S, const gs_level* L, i
     int zc;
     dim3 g, b;
     bool y2 = false, xh = false;
+    mode = base_mode(mode);
     // LINEAR and NEWTON (NONLINEAR carries restV too). Rows of more than 512 points (column blocks, XH,
     // NEWTON too since r04) with the workspace of gs_jacobi_sweep2_prolong_ws_elems (the corrected edge
     // columns). The fine planes' parities must be the global ones (even z0): they select each plane's
@@ -177,6 +185,7 @@ int64_t gs_jacobi_sweep2_prolong_ws_elems(const gs_stencil* S, const gs_level* L
     int zc;
     dim3 g, b;
     bool y2 = false, xh = false;
+    mode = base_mode(mode);
     if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || !tb2_plan(S, L, &zc, &g, &b, &y2, mode, &xh, true) || !xh)
         return 0;
     const int64_t bw = 2 * WAVE * TBY_WX, nb = (L->nx + bw - 1) / bw - 1; // interior block boundaries
@@ -199,6 +208,8 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     int zc;
     dim3 g, b;
     bool y2 = false, xh = false;
+    const int bconst = mode == GS_NEWTON_G; // (Coef::bconst, as gs_jacobi_sweep2_norm)
+    mode = base_mode(mode);
     // coarse plane of fine local plane z: (z >> 1) + czoff, z0 even (a slab, or a plane range of one)
     const int64_t czoff = cl ? L->z0 / 2 - cl->z0 : 0;
     if (!gs_jacobi_sweep2_prolong_supported(S, L, mode) || bad_level(cl) || czoff < 0 || !v_in || !coarse_v ||
@@ -211,7 +222,7 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     // the kernel indexes the coarse field from the plane under fine local plane 0
     coarse_v += czoff * cl->ldz;
     if (coarse_sub) coarse_sub += czoff * cl->ldz;
-    const Coef k = make_coef(S, L, omega, gamma);
+    const Coef k = make_coef(S, L, omega, gamma, bconst);
     if (xh && need > 0) {
         const int bw = 2 * WAVE * TBY_WX, nb = (int)((L->nx + bw - 1) / bw - 1);
         hipLaunchKernelGGL(k_pro_strip<false>, dim3((unsigned)((L->ny + 2 + 63) / 64), (unsigned)(L->nz + 4), (unsigned)nb),
@@ -220,6 +231,8 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     }
 #define GS_TBP1(M, P, U, X, WM) hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, 1, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
 #define GS_TBP(M, P, X, WM) do { if (k.unit) GS_TBP1(M, P, true, X, WM); else GS_TBP1(M, P, false, X, WM); } while (0)
+#define GS_TBPF1(M, P, U, X, WM, PF) hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, PF, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
+#define GS_TBPF(M, P, X, WM, PF) do { if (k.unit) GS_TBPF1(M, P, true, X, WM, PF); else GS_TBPF1(M, P, false, X, WM, PF); } while (0)
     // NEWTON's variant keeps ~37 KB of state per x-wave in LDS (its RECOMP rows): rows of <= 256 points
     // (two x-waves) take the instance sized for two, so that two blocks share a CU (8 waves, the VGPR
     // limit) instead of one block of 4 waves holding the whole LDS of a four-x-wave instance
@@ -231,15 +244,22 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     else if (mode == GS_NEWTON && b.y <= 2) GS_TBP(GS_NEWTON, 1, false, 2);
     else if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1, false, TBY_WX);
     else if (xh) GS_TBP(GS_LINEAR, 1, true, TBY_WX);
+#ifdef GS_EXP_LPRO2
+    else GS_TBPF(GS_LINEAR, 1, false, TBY_WX, 2);
+#else
     else GS_TBP(GS_LINEAR, 1, false, TBY_WX);
+#endif
 #undef GS_TBP
 #undef GS_TBP1
+#undef GS_TBPF
+#undef GS_TBPF1
     return launch_status();
 }
 
 // the small-level tiled kernels (gs_device.hpp k_tile_*): LINEAR / NEWTON, canonical stencil order, whole levels
 int gs_tiled_supported(const gs_stencil* S, const gs_level* L, int mode)
 {
+    mode = base_mode(mode);
     return S && valid_stencil(S) && canonical_order(S) && (mode == GS_LINEAR || newtonish(mode)) && !bad_level(L) &&
            L->z0 == 0 && L->nx >= 1 && L->ny >= 1 && L->nz >= 1;
 }
@@ -248,6 +268,7 @@ int gs_smooth2_restrict_tiled(const gs_stencil* S, const gs_level* fl, int mode,
                               const double* v_in, double* v_out, const double* f, const double* w, double* coarse_f,
                               const gs_level* cl, hipStream_t st)
 {
+    mode = base_mode(mode); // (the tiled kernels read the factor field, which holds gamma under GS_NEWTON_G)
     if (!gs_tiled_supported(S, fl, mode) || bad_level(cl) || cl->z0 != 0 || !v_out || !f || !coarse_f ||
         v_in == v_out || (newtonish(mode) && !w) || cl->nx != fl->nx / 2 || cl->ny != fl->ny / 2 ||
         cl->nz != fl->nz / 2)
@@ -270,6 +291,7 @@ int gs_prolong_smooth2_tiled(const gs_stencil* S, const gs_level* fl, int mode, 
                              const double* v_in, const double* coarse_v, const gs_level* cl, double* v_out,
                              const double* f, const double* w, hipStream_t st)
 {
+    mode = base_mode(mode);
     if (!gs_tiled_supported(S, fl, mode) || bad_level(cl) || cl->z0 != 0 || !v_in || !coarse_v || !v_out || !f ||
         v_in == v_out || (newtonish(mode) && !w) || (fl->nx + 1) / 2 > cl->nx + 1 || (fl->ny + 1) / 2 > cl->ny + 1 ||
         (fl->nz + 1) / 2 > cl->nz + 1)
@@ -302,6 +324,7 @@ int64_t gs_residual_num_partials(const gs_stencil* S, const gs_level* L)
 int gs_residual(const gs_stencil* S, const gs_level* L, int mode, double gamma, const double* v, const double* f,
                 const double* w, double* r, double* partials, hipStream_t st)
 {
+    mode = base_mode(mode);
     if (!f || (newtonish(mode) && !w)) return GS_EINVAL;
     if (partials && (L && (L->nx == 0 || L->ny == 0 || L->nz == 0)))
         return (int)hipMemsetAsync(partials, 0, sizeof(double), st);
@@ -346,6 +369,8 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
                               const double* f, const double* w, double* ca, double* cb, const gs_level* cl, int zhi,
                               hipStream_t st)
 {
+    const int bconst = mode == GS_NEWTON_G; // (Coef::bconst: k_rr2 takes gamma for the factor)
+    mode = base_mode(mode);
     if (!S || !valid_stencil(S) || !v || !f || !ca || (newtonish(mode) && !w) || mode < GS_LINEAR ||
         mode > GS_NEWTON_B || bad_level(fl) || bad_level(cl))
         return GS_EINVAL;
@@ -356,7 +381,7 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
     if (2 * cl->nx + 1 > fl->nx + 1 || 2 * cl->ny + 1 > fl->ny + 1 || 2 + zoff - 1 < 0 ||
         2 * cl->nz + zoff + 1 > fl->nz + 1)
         return GS_EINVAL;
-    const Coef k = make_coef(S, fl, 0.0, gamma);
+    const Coef k = make_coef(S, fl, 0.0, gamma, bconst);
     const int64_t wxs = ((fl->nx + 1) / 2 + WAVE - 1) / WAVE; // x-waves covering coarse columns 1..(fnx+1)/2
     const bool ldsOnly = kKnobs.rrLds; // A/B switch for tools/ measurements
     const bool rr2 = !ldsOnly && canonical_order(S) && zoff == 0 && wxs <= RR2_WXMAX;
@@ -594,6 +619,7 @@ int gs_coarse_cycle_max_levels(void) { return CC_MAXLEV; }
 int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int mode, double omega, double gamma,
                     int pre, int post, hipStream_t st)
 {
+    mode = base_mode(mode); // (the coarse levels read their factor fields, which hold gamma under GS_NEWTON_G)
     if (!S || !valid_stencil(S) || !lv || n < 1 || n > CC_MAXLEV || mode < GS_LINEAR || mode > GS_NEWTON_B ||
         pre < 0 || post < 0)
         return GS_EINVAL;

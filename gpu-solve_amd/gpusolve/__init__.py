@@ -20,7 +20,7 @@ from typing import List, Tuple
 import numpy as np
 
 from . import _abi
-from ._abi import GS_LINEAR, GS_NEWTON, GS_NEWTON_B, GS_NONLINEAR, gs_level, gs_params, gs_stencil, kernels, driver, diag  # noqa: F401
+from ._abi import GS_LINEAR, GS_NEWTON, GS_NEWTON_B, GS_NEWTON_G, GS_NONLINEAR, gs_level, gs_params, gs_stencil, kernels, driver, diag  # noqa: F401
 
 CANONICAL_OFFSETS = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
 

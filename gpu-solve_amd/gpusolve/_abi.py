@@ -17,6 +17,7 @@ EXECUTABLE = os.path.join(BIN_DIR, "GpuSolve-hip")
 
 GS_LINEAR, GS_NONLINEAR, GS_NEWTON = 0, 1, 2
 GS_NEWTON_B = 3  # NEWTON with the precomputed linearisation factor B (include/gpusolve_hip.h)
+GS_NEWTON_G = 4  # GS_NEWTON_B whose factor field holds gamma everywhere (the first Newton iteration)
 GS_EINVAL = 100001
 
 dptr = C.POINTER(C.c_double)

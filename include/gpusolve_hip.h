@@ -60,6 +60,12 @@ enum { GS_LINEAR = 0, GS_NONLINEAR = 1, GS_NEWTON = 2 }; /* GridParams::Mode, sr
  * vs ocml's exp). The host driver's inner Newton solves run in this mode: exp(newtonV) is evaluated once per
  * point and Newton iteration instead of in every sweep, residual and restriction of the ten inner V-cycles. */
 enum { GS_NEWTON_B = 3 };
+/* GS_NEWTON_B whose factor field holds gamma at every point, the first Newton iteration's B = gamma*(1+0)*exp(0)
+ * (newtonV = 0). Accepted wherever GS_NEWTON_B is; `w` must still point at that field, filled with gamma (gs_fill).
+ * The fused pairs (gs_jacobi_sweep2*, gs_jacobi_sweep2_prolong*) and the register residual + restriction
+ * (gs_residual_restrict*, k_rr2) then take gamma instead of loading w (8 B per point less); every other launcher reads
+ * the field. Same values as GS_NEWTON_B on that field, bit for bit. */
+enum { GS_NEWTON_G = 4 };
 
 /* GridParams::stencil (src/gridParams.h:7-27): values + (x,y,z) offsets, config order. */
 typedef struct {

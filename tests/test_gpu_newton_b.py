@@ -17,7 +17,7 @@ torch = pytest.importorskip("torch")
 import gpusolve as gsv  # noqa: E402
 from gpusolve.devfield import DevField  # noqa: E402
 
-NEWTON, NEWTON_B = gsv.GS_NEWTON, gsv.GS_NEWTON_B
+NEWTON, NEWTON_B, NEWTON_G = gsv.GS_NEWTON, gsv.GS_NEWTON_B, gsv.GS_NEWTON_G
 
 
 def k():
@@ -163,3 +163,85 @@ def test_newton_solve_b_matches_reference_mode(dims, pre, post):
     for n in ("v", "newtonV"):
         a, c = f_b[(0, n)], f_ref[(0, n)]
         assert np.abs(a - c).max() <= 1e-11 * np.abs(c).max(), n
+
+
+@pytest.mark.parametrize("dims,gamma", [((128, 64, 32), 1.0), ((256, 32, 30), 0.7), ((700, 12, 10), 1.3),
+                                        ((1100, 20, 18), 1.0), ((33, 31, 29), 2.0)])
+def test_mode_g_matches_mode_b_on_a_gamma_field(dims, gamma):
+    """GS_NEWTON_G (the first Newton iteration: B = gamma everywhere) against GS_NEWTON_B on a factor field filled
+    with gamma: the pair (loaded and zero iterate, with norm partials), the fused prolongation pair (column blocks
+    on the long rows), residual + restriction, one sweep and the residual — bit for bit. Where the kernel honours
+    the constant (k_tb2y pairs, k_rr2), it must not read the field at all: the same outputs with the field NaN."""
+    S = gsv.Stencil().to_abi()
+    rng = np.random.default_rng(len(dims) + dims[0])
+    h, v, f, _ = level_pair(rng, dims)
+    L = v.level(h)
+    g_field = DevField(*dims, fill=gamma * (1 + 0.0) * np.exp(0.0))
+    nan_field = DevField(*dims, fill=np.nan)
+    cd = tuple(d // 2 for d in dims)
+
+    def same(a, b):
+        torch.cuda.synchronize()
+        assert a.zyx_ext.cpu().numpy().tobytes() == b.zyx_ext.cpu().numpy().tobytes()
+
+    outs = {}
+    for tag, mode, wf in (("b", NEWTON_B, g_field), ("g", NEWTON_G, g_field), ("gnan", NEWTON_G, nan_field)):
+        o = outs[tag] = {}
+        o["sweep"] = DevField(*dims, fill=0.0)
+        if tag != "gnan":  # one sweep / the residual read the field (k_rb)
+            ok(k().gs_jacobi_sweep(C.byref(S), C.byref(L), mode, 0.8, gamma, v.ptr, o["sweep"].ptr, f.ptr, wf.ptr,
+                                   st()))
+            o["res"] = DevField(*dims, fill=0.0)
+            ok(k().gs_residual(C.byref(S), C.byref(L), mode, gamma, v.ptr, f.ptr, wf.ptr, o["res"].ptr, None, st()))
+        kname = k().gs_jacobi_sweep2_kernel(C.byref(S), C.byref(L), NEWTON_B).decode()
+        if k().gs_jacobi_sweep2_supported_mode(C.byref(S), C.byref(L), NEWTON_B) and \
+                (tag != "gnan" or kname.startswith("k_tb2y")):
+            npart = k().gs_jacobi_sweep2_num_partials(C.byref(S), C.byref(L), NEWTON_B)
+            for i, vin in enumerate((v.ptr, None)):
+                o[f"pair{i}"] = DevField(*dims, fill=0.0)
+                o[f"part{i}"] = torch.zeros(max(1, npart), dtype=torch.float64, device="cuda")
+                ok(k().gs_jacobi_sweep2_norm(C.byref(S), C.byref(L), mode, 0.8, gamma, vin, o[f"pair{i}"].ptr, f.ptr,
+                                             wf.ptr, 0, 0, o[f"part{i}"].data_ptr(), st()))
+        if all(c >= 1 for c in cd):
+            Lc = DevField(*cd).level(1.0 / (cd[1] + 1))
+            o["rr"] = DevField(*cd, fill=0.0)
+            if tag != "gnan" or k().gs_residual_restrict_slab_supported(C.byref(S), C.byref(L)):
+                ok(k().gs_residual_restrict(C.byref(S), C.byref(L), mode, gamma, v.ptr, f.ptr, wf.ptr, o["rr"].ptr,
+                                            None, C.byref(Lc), st()))
+            if k().gs_jacobi_sweep2_prolong_supported(C.byref(S), C.byref(L), NEWTON_B):
+                cv = DevField(*cd).from_xyz(np.random.default_rng(3).uniform(-0.1, 0.1, tuple(c + 2 for c in cd)))
+                wsn = k().gs_jacobi_sweep2_prolong_ws_elems(C.byref(S), C.byref(L), mode)
+                ws = torch.empty(max(1, wsn), dtype=torch.float64, device="cuda")
+                o["pro"] = DevField(*dims, fill=0.0)
+                ok(k().gs_jacobi_sweep2_prolong_ws(C.byref(S), C.byref(L), mode, 0.8, gamma, v.ptr, cv.ptr, None,
+                                                   C.byref(Lc), o["pro"].ptr, f.ptr, wf.ptr, 0, 0, ws.data_ptr(), wsn,
+                                                   st()))
+    assert set(outs["g"]) == set(outs["b"])
+    for key in outs["b"]:
+        a, b = outs["g"][key], outs["b"][key]
+        if isinstance(a, torch.Tensor):
+            torch.cuda.synchronize()
+            assert torch.equal(a, b), key
+        else:
+            same(a, b)
+    for key, a in outs["gnan"].items():
+        if key in ("sweep",) or (key == "rr" and not k().gs_residual_restrict_slab_supported(C.byref(S), C.byref(L))):
+            continue
+        b = outs["b"][key]
+        if isinstance(a, torch.Tensor):
+            torch.cuda.synchronize()
+            assert torch.equal(a, b), key
+        else:
+            same(a, b)
+
+
+@pytest.mark.parametrize("dims", [(127, 127, 127), (130, 66, 34), (1100, 20, 18)])
+def test_newton_solve_g_bit_identical(dims):
+    """Whole Newton solves: the first iteration's inner solve in GS_NEWTON_G (default) against GS_NO_NEWTON_G
+    (GS_NEWTON_B on the gamma-filled factor fields): histories and every level's fields bit for bit."""
+    p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=NEWTON, preSmoothing=2, postSmoothing=2)
+    h_b, f_b = solve(p, GS_NO_NEWTON_G=1)
+    h_g, f_g = solve(p)
+    assert h_g == h_b
+    for key in f_b:
+        assert f_g[key].tobytes() == f_b[key].tobytes(), key

@@ -19,7 +19,8 @@ SWITCHES = ["GS_COARSE_POINTS", "GS_NEWTON_PRO_POINTS", "GS_RR_NR", "GS_RR_LDS",
             "GS_TBX_PFD", "GS_PAIR_BIG_CHUNKS", "GS_NO_UNIT_STENCIL", "GS_PAIR_MIN_BLOCKS", "GS_FIT_ROUNDS",
             "GS_NO_PIPELINE", "GS_NO_NEWTON_FUSED_UPDATE", "GS_RR_NTU", "GS_PAIR_ONE_ROUND", "GS_SLAB_ZC", "GS_PAIR_ZC",
             "GS_RR_REVERSE", "GS_HALO_ORDER", "GS_NO_ZERO_Q", "GS_XH_SWIZZLE",
-            "GS_MID_ZC", "GS_RR_ZC", "GS_NEWTON_XH", "GS_SPEC_CACHED", "GS_RR_ZC_BIG", "GS_PAIR_ONE_ROUND_MID", "GS_RB_ZC", "GS_RR_NG", "GS_NEWTON_B_FUSED"]
+            "GS_MID_ZC", "GS_RR_ZC", "GS_NEWTON_XH", "GS_SPEC_CACHED", "GS_RR_ZC_BIG", "GS_PAIR_ONE_ROUND_MID", "GS_RB_ZC", "GS_RR_NG", "GS_NEWTON_B_FUSED",
+            "GS_NO_NEWTON_G"]
 
 # (case, solve args) -> the switches whose paths that problem exercises
 CASES = {
@@ -40,8 +41,11 @@ CASES = {
     "newton127": ((2, 127, 127, 127, 2), [("GS_NEWTON_PRO_POINTS", "0"), ("GS_NO_FUSED_PROLONG", "1"),
                                           ("GS_NO_PIPELINE", "1"), ("GS_NO_NEWTON_FUSED_UPDATE", "1"),
                                           ("GS_RR_REVERSE", "0"), ("GS_NO_ZERO_Q", "1")]),
-    "newton_rows700": ((2, 700, 12, 10, 2), [("GS_NEWTON_XH", "0")]),
-    "newton255": ((2, 255, 127, 127, 2), [("GS_RB_ZC", "10"), ("GS_RR_NG", "2"), ("GS_NEWTON_B_FUSED", "0")]),
+    # two loopback slabs in NEWTON mode: GS_NEWTON_G's pairs on slab plane ranges (ghost planes of the factor)
+    "newton_slabs": ((2, 130, 66, 128, 2, 2, 2, 2), [("GS_NO_NEWTON_G", "1")]),
+    "newton_rows700": ((2, 700, 12, 10, 2), [("GS_NEWTON_XH", "0"), ("GS_NO_NEWTON_G", "1")]),
+    "newton255": ((2, 255, 127, 127, 2), [("GS_RB_ZC", "10"), ("GS_RR_NG", "2"), ("GS_NEWTON_B_FUSED", "0"),
+                                          ("GS_NO_NEWTON_G", "1")]),
 }
 PARAMS = [(case, sw, val) for case, (_, sws) in CASES.items() for sw, val in sws]
 _default = {}
