@@ -2199,11 +2199,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // 0.986-0.990 ms per 512^3 launch with the LDS state, profiles/r05/r05g_newton_b_norecomp_touch_ab.txt)
     constexpr bool RECOMP = newtonish(MODE) && ((PRO != 0 && MODE == GS_NEWTON) || XH);
     constexpr bool ELDS = RECOMP && MODE == GS_NEWTON; // E in LDS (GS_NEWTON_B: E = 1, A = B from wprev_l)
-#ifdef GS_EXP_LPRO2
-    constexpr bool WLDS = PRO != 0 && (newtonish(MODE) || PFD == 2);
-#else
     constexpr bool WLDS = newtonish(MODE) && PRO != 0; // the coarse X-pass rows in LDS (prolongation pairs)
-#endif
     // (Wprev, Fprev: sweep 2's newtonV / f rows at z-1, in LDS like the coarse rows below)
     __shared__ double2 wprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];
     __shared__ double2 fprev_l[RECOMP ? RY : 1][RECOMP ? 2 * WXMAX : 1][RECOMP ? WAVE : 1];

@@ -231,8 +231,6 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     }
 #define GS_TBP1(M, P, U, X, WM) hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, 1, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
 #define GS_TBP(M, P, X, WM) do { if (k.unit) GS_TBP1(M, P, true, X, WM); else GS_TBP1(M, P, false, X, WM); } while (0)
-#define GS_TBPF1(M, P, U, X, WM, PF) hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, PF, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
-#define GS_TBPF(M, P, X, WM, PF) do { if (k.unit) GS_TBPF1(M, P, true, X, WM, PF); else GS_TBPF1(M, P, false, X, WM, PF); } while (0)
     // NEWTON's variant keeps ~37 KB of state per x-wave in LDS (its RECOMP rows): rows of <= 256 points
     // (two x-waves) take the instance sized for two, so that two blocks share a CU (8 waves, the VGPR
     // limit) instead of one block of 4 waves holding the whole LDS of a four-x-wave instance
@@ -244,15 +242,9 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     else if (mode == GS_NEWTON && b.y <= 2) GS_TBP(GS_NEWTON, 1, false, 2);
     else if (mode == GS_NEWTON) GS_TBP(GS_NEWTON, 1, false, TBY_WX);
     else if (xh) GS_TBP(GS_LINEAR, 1, true, TBY_WX);
-#ifdef GS_EXP_LPRO2
-    else GS_TBPF(GS_LINEAR, 1, false, TBY_WX, 2);
-#else
     else GS_TBP(GS_LINEAR, 1, false, TBY_WX);
-#endif
 #undef GS_TBP
 #undef GS_TBP1
-#undef GS_TBPF
-#undef GS_TBPF1
     return launch_status();
 }
 
