@@ -316,12 +316,32 @@ __device__ __forceinline__ double op_value(const Coef& k, double c, double xp, d
     return op_finish<MODE>(k, s, c, w);
 }
 
+// GS_NEWTON_B's Jacobi quotient r / den (den = preFac + B, the reference's denominator bit for bit): r times den's
+// reciprocal refined by two Newton steps (the reciprocal the IEEE division sequence forms, see div_hh), without the
+// division's final correction, scaling and fix-up: 7 FP64 operations instead of ~11, branch-free, and within 1 ulp
+// of r / den (tests/test_gpu_newton_b.py::test_nb_quotient_ulps: 26 % of the quotients differ, by one ulp). NEWTON's
+// parity is a tolerance — 1e-6 relative on the residual norms (north_star), 1e-9 / 1e-10 in the tests — and its exp
+// already differs by an ulp between ocml and glibc. A denominator above 2^1000 (inf included) is clamped there so the
+// reciprocal stays normal: r / inf comes out below |r| 2^-999 instead of 0; NaN stays NaN, den = 0 gives NaN where the
+// IEEE quotient is inf — both non-finite. Per 512^3 launch: pair 0.871-0.873 vs 0.897-0.914 ms, prolongation pair
+// 0.960-0.965 vs 0.989-0.997 ms; Newton iteration -0.5 ms (r05p, profiles/r05/r05p_newton_b_quotient_ab.txt; one
+// Newton step only: 18 ulp, 1 % faster; a range branch around it: r05o). GS_EXP_NB_IEEE: the IEEE division (A/B).
+__device__ __forceinline__ double nb_quot(double r, double den)
+{
+#ifdef GS_EXP_NB_IEEE
+    return r / den;
+#else
+    const double d = den > 0x1p1000 ? 0x1p1000 : den;
+    return r * hh_recip(d);
+#endif
+}
+
 // Jacobi point update from the old value and its residual — CpuSolver.cpp:157-171
 template <int MODE>
 __device__ __forceinline__ double jacobi_update(const Coef& k, double v, double r, double w)
 {
     if (MODE == GS_LINEAR) return v + k.omega * (k.alpha * r);
-    if (MODE == GS_NEWTON_B) return v + k.omega * (r / (k.preFac + w)); // preFac + B: the reference's den, bit for bit
+    if (MODE == GS_NEWTON_B) return v + k.omega * nb_quot(r, k.preFac + w); // preFac + B: the reference's den
     const double u = (MODE == GS_NONLINEAR) ? v : w;
     const double eu = exp(u);
     const double den = k.preFac + k.gamma * (1 + u) * eu;
@@ -333,9 +353,11 @@ __device__ __forceinline__ double jacobi_update(const Coef& k, double v, double 
 // op_finish / jacobi_update, whose reference expressions evaluate gamma * (1 + w) first and multiply
 // by exp(w) last (CpuSolver.cpp:63-66, :157-171).
 __device__ __forceinline__ double newton_op(double q, double c, double A, double E) { return q + A * c * E; }
+template <int MODE>
 __device__ __forceinline__ double newton_update(const Coef& k, double v, double r, double A, double E)
 {
     const double den = k.preFac + A * E;
+    if constexpr (MODE == GS_NEWTON_B) return v + k.omega * nb_quot(r, den); // (E = 1: den = preFac + B exactly)
 #ifdef GS_EXP_NODIV
     return v + k.omega * (r * den);
 #else
@@ -583,8 +605,8 @@ __global__ __launch_bounds__(WAVE* W) void k_rb(Coef k, const double* __restrict
                 }
                 double o0, o1;
                 if (NS) {
-                    o0 = newton_update(k, c.x, r0, Ax, Ex);
-                    o1 = newton_update(k, c.y, r1, Ay, Ey);
+                    o0 = newton_update<MODE>(k, c.x, r0, Ax, Ex);
+                    o1 = newton_update<MODE>(k, c.y, r1, Ay, Ey);
                 } else if (KIND == 0) {
                     o0 = jacobi_update<MODE>(k, c.x, r0, wx);
                     o1 = jacobi_update<MODE>(k, c.y, r1, wy);
@@ -2496,7 +2518,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         if constexpr (newtonish(MODE)) { // the interior rows' NEWTON expressions, exp once
                             const double we = efld(cs, 4), A = newton_A<MODE>(k, we), E = newton_E<MODE>(we);
                             const double a = newton_op(qe(), c, A, E);
-                            nv = newton_update(k, c, efld(cs, 3) - a, A, E);
+                            nv = newton_update<MODE>(k, c, efld(cs, 3) - a, A, E);
                         } else {
                             const double a = op_finish<MODE>(k, qe(), c, 0.0);
                             nv = jacobi_update<MODE>(k, c, EF[cs] - a, 0.0);
@@ -2545,8 +2567,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                         if (ELDS && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
                         a0 = newton_op(q[0], c.x, A.x, E.x);
                         a1 = newton_op(q[1], c.y, A.y, E.y);
-                        n0 = newton_update(k, c.x, FL[cs][j].x - a0, A.x, E.x);
-                        n1 = newton_update(k, c.y, FL[cs][j].y - a1, A.y, E.y);
+                        n0 = newton_update<MODE>(k, c.x, FL[cs][j].x - a0, A.x, E.x);
+                        n1 = newton_update<MODE>(k, c.y, FL[cs][j].y - a1, A.y, E.y);
                     } else {
                         a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                         a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
@@ -2589,8 +2611,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                             const double a0 = newton_op(q[0], c.x, A.x, E.x);
                             const double a1 = newton_op(q[1], c.y, A.y, E.y);
                             const double2 fp = RECOMP ? fprev_l[j - 1][wx + WX * wy][lane] : Fprev[j - 1];
-                            o0 = newton_update(k, c.x, fp.x - a0, A.x, E.x);
-                            o1 = newton_update(k, c.y, fp.y - a1, A.y, E.y);
+                            o0 = newton_update<MODE>(k, c.x, fp.x - a0, A.x, E.x);
+                            o1 = newton_update<MODE>(k, c.y, fp.y - a1, A.y, E.y);
                         } else {
                             const double a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                             const double a1 = op_finish<MODE>(k, q[1], c.y, 0.0);

@@ -388,6 +388,14 @@ __global__ __launch_bounds__(256) void k_div_check(const double* __restrict__ a,
     ref[i] = a[i] / k.hh;
 }
 
+// GS_NEWTON_B's Jacobi quotient (nb_quot) of r[i] / den[i] (tests: ulp distance to the IEEE quotient)
+__global__ __launch_bounds__(256) void k_nb_quot(const double* __restrict__ r, const double* __restrict__ den, int64_t n,
+                                                 double* __restrict__ q)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) q[i] = nb_quot(r[i], den[i]);
+}
+
 __global__ __launch_bounds__(256) void k_triad(double* __restrict__ out, const double* __restrict__ a,
                                                const double* __restrict__ b, int64_t n2)
 {
@@ -630,6 +638,14 @@ int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, doub
     k.hh = hh;
     k.fastdiv = hh >= 0x1p-120 && hh <= 1.0;
     hipLaunchKernelGGL(k_div_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, n, k, fast, ref);
+    return launch_status();
+}
+
+int gs_debug_nb_quot(const double* r, const double* den, int64_t n, double* q, hipStream_t st)
+{
+    if (!r || !den || !q || n < 0) return GS_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_nb_quot, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, r, den, n, q);
     return launch_status();
 }
 

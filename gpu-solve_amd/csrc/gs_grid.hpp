@@ -188,7 +188,7 @@ public:
 
     // the mode and the w operand the V-cycle's kernels take: GS_NEWTON_B and B while findError's inner solve runs
     // with the factor fields current (newtonB_), else the grid's mode and newtonV (reference expressions)
-    int kmode() const { return newtonB_ ? (bconst_ ? GS_NEWTON_G : GS_NEWTON_B) : (int)mode; }
+    int kmode() const { return newtonB_ ? (bconst_ ? (int)GS_NEWTON_G : (int)GS_NEWTON_B) : (int)mode; }
     const double* wOf(const LevelData& L) const
     {
         return newtonB_ ? L.bfac.data() : (L.newtonV ? L.newtonV.data() : nullptr);

@@ -177,6 +177,7 @@ DIAG_API = {
     "gs_debug_sweep_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double,
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_debug_div_check": (C.c_int, [C.c_void_p, i64, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gs_debug_nb_quot": (C.c_int, [C.c_void_p, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
     "gs_debug_num_pair_variants": (C.c_int, []),
     "gs_debug_pair_variant_name": (C.c_char_p, [C.c_int]),
     "gs_debug_pair_timestamps": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,

@@ -46,6 +46,8 @@ int gs_debug_sweep_variant(int variant, const gs_stencil* S, const gs_level* L, 
                            double* v_out, const double* f, hipStream_t stream);
 /* fast[i] = the kernels' a[i] / hh (3-operation path where it applies), ref[i] = plain division. */
 int gs_debug_div_check(const double* a, int64_t n, double hh, double* fast, double* ref, hipStream_t stream);
+/* q[i] = the GS_NEWTON_B kernels' Jacobi quotient r[i] / den[i] (nb_quot: den's one-step refined reciprocal). */
+int gs_debug_nb_quot(const double* r, const double* den, int64_t n, double* q, hipStream_t stream);
 /* Fused-pair shape variants (LINEAR, level boundaries on both z sides; zc = 0: default chunk). */
 int gs_debug_num_pair_variants(void);
 const char* gs_debug_pair_variant_name(int variant);

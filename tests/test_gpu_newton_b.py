@@ -2,7 +2,8 @@
 B = gamma (1 + newtonV) exp(newtonV) (gs_newton_bfac, once per level and Newton iteration) instead of evaluating
 exp(newtonV) in every sweep, residual and restriction. The Jacobi denominator preFac + B is the reference's
 bit for bit; the operator term B * v re-associates the reference's (gamma (1 + w) v) exp(w), so the mode-3
-kernels agree with the mode-2 ones to a few ulps, and whole Newton solves with GS_NO_NEWTON_B (mode 2 inside)
+kernels agree with the mode-2 ones to a few ulps (and their Jacobi quotient r / (preFac + B) is formed through the
+denominator's one-step refined reciprocal, within 1 ulp of the IEEE quotient: test_nb_quotient_ulps), and whole Newton solves with GS_NO_NEWTON_B (mode 2 inside)
 to far below the 1e-10 field / 1e-9 history tolerances the oracle comparisons use (test_gpu_solver.py,
 test_gpu_zslab.py pin the default path to the reference itself)."""
 import ctypes as C
@@ -18,6 +19,7 @@ import gpusolve as gsv  # noqa: E402
 from gpusolve.devfield import DevField  # noqa: E402
 
 NEWTON, NEWTON_B, NEWTON_G = gsv.GS_NEWTON, gsv.GS_NEWTON_B, gsv.GS_NEWTON_G
+NB_QUOT_ULPS = 1  # the quotient's bound (gs_device.hpp nb_quot: measured max 1 ulp over these draws, r05p)
 
 
 def k():
@@ -245,3 +247,40 @@ def test_newton_solve_g_bit_identical(dims):
     assert h_g == h_b
     for key in f_b:
         assert f_g[key].tobytes() == f_b[key].tobytes(), key
+
+
+def test_nb_quotient_ulps():
+    """The GS_NEWTON_B Jacobi quotient (nb_quot: r times the refined reciprocal of den clamped at 2^1000) against the
+    IEEE quotient: within 1 ulp over the denominators the solver forms (preFac + B, from the coarsest level's ~24
+    up to 2^40) and numerators of every magnitude; the non-finite cases stay non-finite where the IEEE quotient is
+    (NaN in, NaN out; den = 0), and den = inf gives a quotient below |r| 2^-999 (the IEEE one is 0)."""
+    rng = np.random.default_rng(11)
+    n = 400_000
+    den = np.exp(rng.uniform(np.log(20.0), np.log(2.0 ** 40), n))
+    r = rng.normal(0, 1, n) * np.exp(rng.uniform(-200, 200, n))
+    edge_r = np.array([1.0, -2.0, 0.0, 1e300, -1e-300])
+    edge_den = np.array([np.inf, np.nan, 0.0])
+    den = np.concatenate([den, np.repeat(edge_den, edge_r.size), np.full(3, 1e6)])
+    r = np.concatenate([r, np.tile(edge_r, edge_den.size), [np.nan, np.inf, -np.inf]])
+    dr, dd = torch.from_numpy(r).cuda(), torch.from_numpy(den).cuda()
+    q = torch.empty_like(dr)
+    assert gsv.diag().gs_debug_nb_quot(dr.data_ptr(), dd.data_ptr(), dr.numel(), q.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    got = q.cpu().numpy()
+    with np.errstate(all="ignore"):
+        want = r / den
+    body = slice(0, n)
+    fin = np.isfinite(want[body]) & (np.abs(want[body]) >= np.finfo(float).tiny)
+    ulp = np.spacing(np.abs(want[body][fin]))
+    worst = np.max(np.abs(got[body][fin] - want[body][fin]) / ulp)
+    print(f"nb_quot: max {worst} ulp, {np.mean(got[body][fin] != want[body][fin]):.4f} of the quotients differ from r / den")
+    assert worst <= NB_QUOT_ULPS, worst
+    e = slice(n, n + 3 * edge_r.size)
+    ge, de, re_ = got[e], den[e], r[e]
+    inf_d = np.isinf(de)
+    assert np.all(np.abs(ge[inf_d]) <= np.abs(re_[inf_d]) * 2.0 ** -999)
+    assert np.all(np.isnan(ge[np.isnan(de)]))
+    assert not np.any(np.isfinite(ge[(de == 0) & (re_ != 0)]))
+    tail = got[n + 3 * edge_r.size:]
+    assert np.isnan(tail[0]) and np.isinf(tail[1]) and np.isinf(tail[2])
