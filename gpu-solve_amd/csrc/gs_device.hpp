@@ -245,12 +245,13 @@ __device__ __forceinline__ void div_hh_n(const Coef& k, double (&s)[N])
     }
 }
 
-// one row's two points: batched, except in NEWTON mode whose kernels run at the VGPR limit (the batch
-// keeps both sums live across the branch)
+// one row's two points: batched, except in GS_NEWTON mode whose kernels run at the VGPR limit (the batch
+// keeps both sums live across the branch). GS_NEWTON_B's pairs have the room since r05: batched, NEWTON_B pair
+// 0.840-0.853 vs 0.872-0.885 ms, prolongation pair 0.924-0.930 vs 0.964-0.975 ms, Newton iteration -0.8 ms (r05r)
 template <int MODE>
 __device__ __forceinline__ void div_hh_row(const Coef& k, double (&q)[2])
 {
-    if (newtonish(MODE)) {
+    if (MODE == GS_NEWTON) {
         q[0] = div_hh(k, q[0]);
         q[1] = div_hh(k, q[1]);
     } else {
@@ -326,13 +327,17 @@ __device__ __forceinline__ double op_value(const Coef& k, double c, double xp, d
 // IEEE quotient is inf — both non-finite. Per 512^3 launch: pair 0.871-0.873 vs 0.897-0.914 ms, prolongation pair
 // 0.960-0.965 vs 0.989-0.997 ms; Newton iteration -0.5 ms (r05p, profiles/r05/r05p_newton_b_quotient_ab.txt; one
 // Newton step only: 18 ulp, 1 % faster; a range branch around it: r05o). GS_EXP_NB_IEEE: the IEEE division (A/B).
+__device__ __forceinline__ double nb_recip(double den)
+{
+    const double d = den > 0x1p1000 ? 0x1p1000 : den;
+    return hh_recip(d);
+}
 __device__ __forceinline__ double nb_quot(double r, double den)
 {
 #ifdef GS_EXP_NB_IEEE
     return r / den;
 #else
-    const double d = den > 0x1p1000 ? 0x1p1000 : den;
-    return r * hh_recip(d);
+    return r * nb_recip(den);
 #endif
 }
 
@@ -2211,6 +2216,16 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     constexpr int NS = PFD == 2 ? 4 : 2, UNR = PFD == 2 ? 4 : 2;
     double2 Vp[NV], Vc[NV], VL[NS][NV], FL[NS][NV], WL[NS][NV], HL[NS];
     double2 V1p[RY], V1c[NV], Fprev[RY], Aprev[RY], Eprev[RY]; // Aprev, Eprev: NEWTON terms at z-1
+    // YSH (GS_NEWTON_B plain pairs): the E slots (E = 1 there) carry the point's Jacobi reciprocal nb_recip(preFac + B),
+    // formed in sweep 1 and reused by sweep 2 one plane step later — the same value, so bit-identical to nb_quot at
+    // both sweeps (232-238 VGPRs, no spill): pair 0.806-0.829 vs 0.829-0.840 ms, Newton iteration 27.74-28.07 vs
+    // 28.21-28.48 ms (r05t; in the prolongation pairs too: the same Newton time, 255 VGPRs, and the two-x-wave
+    // instance falls to one wave per SIMD, r05s)
+#ifdef GS_EXP_YSH_NOZV
+    constexpr bool YSH = MODE == GS_NEWTON_B && !XH && PRO == 0 && !ZV;
+#else
+    constexpr bool YSH = MODE == GS_NEWTON_B && !XH && PRO == 0;
+#endif
 #ifdef GS_EXP_EFIELD
     double2 XL[NS][NV];
 #endif
@@ -2558,17 +2573,25 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
 #ifdef GS_EXP_EFIELD
                         const double2 E = XL[cs][j];
 #else
-                        const double2 E = make_double2(newton_E<MODE>(wv.x), newton_E<MODE>(wv.y));
+                        const double2 E = YSH ? make_double2(nb_recip(k.preFac + A.x), nb_recip(k.preFac + A.y))
+                                              : make_double2(newton_E<MODE>(wv.x), newton_E<MODE>(wv.y));
 #endif
                         if (!RECOMP && j >= 1) {
                             Acur[j - 1] = A;
                             Ecur[j - 1] = E;
                         }
                         if (ELDS && j >= 1) eprev_l[ph][j - 1][wx + WX * wy][lane] = E;
-                        a0 = newton_op(q[0], c.x, A.x, E.x);
-                        a1 = newton_op(q[1], c.y, A.y, E.y);
-                        n0 = newton_update<MODE>(k, c.x, FL[cs][j].x - a0, A.x, E.x);
-                        n1 = newton_update<MODE>(k, c.y, FL[cs][j].y - a1, A.y, E.y);
+                        if constexpr (YSH) {
+                            a0 = newton_op(q[0], c.x, A.x, 1.0);
+                            a1 = newton_op(q[1], c.y, A.y, 1.0);
+                            n0 = c.x + k.omega * ((FL[cs][j].x - a0) * E.x);
+                            n1 = c.y + k.omega * ((FL[cs][j].y - a1) * E.y);
+                        } else {
+                            a0 = newton_op(q[0], c.x, A.x, E.x);
+                            a1 = newton_op(q[1], c.y, A.y, E.y);
+                            n0 = newton_update<MODE>(k, c.x, FL[cs][j].x - a0, A.x, E.x);
+                            n1 = newton_update<MODE>(k, c.y, FL[cs][j].y - a1, A.y, E.y);
+                        }
                     } else {
                         a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                         a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
@@ -2608,11 +2631,16 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
                                 A = Aprev[j - 1];
                                 E = Eprev[j - 1];
                             }
-                            const double a0 = newton_op(q[0], c.x, A.x, E.x);
-                            const double a1 = newton_op(q[1], c.y, A.y, E.y);
+                            const double a0 = newton_op(q[0], c.x, A.x, YSH ? 1.0 : E.x);
+                            const double a1 = newton_op(q[1], c.y, A.y, YSH ? 1.0 : E.y);
                             const double2 fp = RECOMP ? fprev_l[j - 1][wx + WX * wy][lane] : Fprev[j - 1];
-                            o0 = newton_update<MODE>(k, c.x, fp.x - a0, A.x, E.x);
-                            o1 = newton_update<MODE>(k, c.y, fp.y - a1, A.y, E.y);
+                            if constexpr (YSH) {
+                                o0 = c.x + k.omega * ((fp.x - a0) * E.x);
+                                o1 = c.y + k.omega * ((fp.y - a1) * E.y);
+                            } else {
+                                o0 = newton_update<MODE>(k, c.x, fp.x - a0, A.x, E.x);
+                                o1 = newton_update<MODE>(k, c.y, fp.y - a1, A.y, E.y);
+                            }
                         } else {
                             const double a0 = op_finish<MODE>(k, q[0], c.x, 0.0);
                             const double a1 = op_finish<MODE>(k, q[1], c.y, 0.0);
