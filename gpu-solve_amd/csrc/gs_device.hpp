@@ -2221,11 +2221,9 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // both sweeps (232-238 VGPRs, no spill): pair 0.806-0.829 vs 0.829-0.840 ms, Newton iteration 27.74-28.07 vs
     // 28.21-28.48 ms (r05t; in the prolongation pairs too: the same Newton time, 255 VGPRs, and the two-x-wave
     // instance falls to one wave per SIMD, r05s)
-#ifdef GS_EXP_YSH_NOZV
-    constexpr bool YSH = MODE == GS_NEWTON_B && !XH && PRO == 0 && !ZV;
-#else
+    // (the zero-iterate pairs too, though it costs them their third wave per SIMD: 166 -> 177 VGPRs; without them
+    // 28.54-28.81 vs 28.08-28.43 ms per Newton iteration, r05u)
     constexpr bool YSH = MODE == GS_NEWTON_B && !XH && PRO == 0;
-#endif
 #ifdef GS_EXP_EFIELD
     double2 XL[NS][NV];
 #endif
