@@ -121,7 +121,7 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_PAIR_ONE_ROUND=0  no one-round / four-round chunking on >= 2^26-point levels
 //   GS_RR_LDS            residual + restriction through the LDS kernel (k_resrestrict) only
 //   GS_RR_NR=1|2         coarse rows per k_rr2 block (default: 2 on LINEAR levels of >= 2^26 points)
-//   GS_RR_NTU=0|2        k_rr2 non-temporal loads never / always (default: two-row blocks only)
+//   GS_RR_NTU=0|1        k_rr2 non-temporal loads never / on two-row blocks only (default 2: every block, r05w)
 //   GS_RR_REVERSE=0|1    k_rr2 z-chunks in ascending (0) or descending (1, default: r04e, -1% on 512^3) order
 //   GS_NO_ZERO_Q         zero-iterate sweeps evaluate the stencil of their zeros instead of taking q = +0
 //   GS_XH_SWIZZLE=0|1    column-block pairs: the mirrored row's x-waves rotated by two (1, default) or not (0)
@@ -150,7 +150,7 @@ struct Knobs {
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
           newtonXh(num("GS_NEWTON_XH", 1) != 0), specCached(num("GS_SPEC_CACHED", 0) != 0),
           xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), oneRoundMid(num("GS_PAIR_ONE_ROUND_MID", 0)), rbZc(num("GS_RB_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
-          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 1)), rrReverse(num("GS_RR_REVERSE", 1)), rrNg(num("GS_RR_NG", 0)),
+          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 2)), rrReverse(num("GS_RR_REVERSE", 1)), rrNg(num("GS_RR_NG", 0)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
     }

@@ -407,7 +407,9 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
         // one operand slot (154 VGPRs, 3 waves per SIMD) measured 1.5 % (level 0) to 9 % (level 1) faster
         // than the two-slot prefetch ring (228 VGPRs, 2 waves per SIMD): tools/ab_session.sh, ab5
         // two-row blocks: the rows no neighbouring block reads are non-temporal loads (0.490 vs 0.505 ms at
-        // 512^3, r02 tools/rr_ab_session.sh rrntu); GS_RR_NTU=0 keeps them cached (A/B)
+        // 512^3, r02 tools/rr_ab_session.sh rrntu); since r05 one-row blocks too (their middle row's f and w: NEWTON_B
+        // level 0 and the LINEAR levels below 2^26 points; Newton iteration 27.73-27.76 vs 27.86-27.97 ms, V-cycle
+        // 2.097-2.100 vs 2.101-2.108 ms, r05w); GS_RR_NTU=0 keeps them cached, =1 restores the two-row-only rule (A/B)
         const int ntu_env = kKnobs.rrNtu;
         const bool ntu = ntu_env == 2 || (ntu_env == 1 && nr == 2);
 #define GS_RR2G(M, N, U, T, G) hipLaunchKernelGGL((k_rr2<M, false, N, U, T, G>), g, b, 0, st, k, v, f, w, ca, cb, (int)fl->nx, (int)fl->ny, (int)fl->nz, fl->ldy, fl->ldz, (int)cl->nx, (int)cl->ny, (int)cl->nz, cl->ldy, cl->ldz, (int)zc, zhi ? 1 : 0, kKnobs.rrReverse)

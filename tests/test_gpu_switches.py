@@ -24,7 +24,7 @@ SWITCHES = ["GS_COARSE_POINTS", "GS_NEWTON_PRO_POINTS", "GS_RR_NR", "GS_RR_LDS",
 
 # (case, solve args) -> the switches whose paths that problem exercises
 CASES = {
-    "linear256": ((0, 256, 256, 256, 3), [("GS_NO_FUSED_SWEEPS", "1"), ("GS_NO_FUSED_RR", "1"),
+    "linear256": ((0, 256, 256, 256, 3), [("GS_RR_NTU", "1"), ("GS_NO_FUSED_SWEEPS", "1"), ("GS_NO_FUSED_RR", "1"),
                                           ("GS_NO_FUSED_PROLONG", "1"), ("GS_NO_SPECULATION", "1"),
                                           ("GS_NO_ZERO_GUESS", "1"), ("GS_NO_PIPELINE", "1"), ("GS_RR_LDS", "1"),
                                           ("GS_RR_NR", "2"), ("GS_NO_UNIT_STENCIL", "1"),
