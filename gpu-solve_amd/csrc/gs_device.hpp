@@ -33,6 +33,8 @@
 //   GS_EXP_NODIV  NEWTON's r / den replaced by a multiplication (what the divisions cost)
 //   GS_EXP_EFIELD k_tb2y's NEWTON sweep-1 rows load E = exp(w) from a second field instead of evaluating it
 //                 (the field lies gs_exp_set_efoff(n) elements past newtonV; tools/newton_kprobe.py sets it)
+// Alternative-arithmetic builds (A/B only; correct results, not the product's choice):
+//   GS_EXP_NB_IEEE   GS_NEWTON_B's Jacobi quotient as the IEEE division instead of nb_quot (r05p)
 #ifdef GS_EXP_NOEXP
 #define exp(x) ((x) * 1.0000001)
 #endif
@@ -2223,7 +2225,10 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* 
     // instance falls to one wave per SIMD, r05s)
     // (the zero-iterate pairs too, though it costs them their third wave per SIMD: 166 -> 177 VGPRs; without them
     // 28.54-28.81 vs 28.08-28.43 ms per Newton iteration, r05u)
-    constexpr bool YSH = MODE == GS_NEWTON_B && !XH && PRO == 0;
+    // (and the four-x-wave prolongation pair, 255 VGPRs, no spill: 0.906-0.918 vs 0.935-0.943 ms per 512^3 launch,
+    // Newton iteration 27.74-28.04 vs 27.99-28.25 ms, r05z; the two-x-wave instance of 256-point rows keeps
+    // recomputing: at 255 VGPRs it would fall to one wave per SIMD, r05s)
+    constexpr bool YSH = MODE == GS_NEWTON_B && !XH && (PRO == 0 || WXMAX > 2);
 #ifdef GS_EXP_EFIELD
     double2 XL[NS][NV];
 #endif
