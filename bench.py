@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-vcycles", type=int, default=2, help="cpu_baseline V-cycles after one warm-up cycle (0: skip)")
     ap.add_argument("--config5", type=int, default=1,
                     help="N=1: also time config #5's 1024^3 grid on this GPU (the strong-scaling denominator)")
+    ap.add_argument("--config2", type=int, default=1,
+                    help="N=1: also time BASELINE config #2 (128^3 linear 2+2, 10 V-cycles)")
     ap.add_argument("--newton-iters", type=int, default=2,
                     help="timed Newton iterations of BASELINE config #4 (512^3 Newton 2+2) at N=1 (0: skip)")
     ap.add_argument("--cta-ab", default="16,64",
@@ -277,15 +279,20 @@ def slab_local_pair_ms(grid, rank, world, k):
     return e0.elapsed_time(e1) / k
 
 
-CEILING_KINDS = {"read": (0, 8.0), "copy": (2, 16.0), "triad": (3, 24.0)}  # gs_debug_bw kind, bytes per element
+# gs_debug_bw kind, bytes per element
+CEILING_KINDS = {"read": (0, 8.0), "copy": (2, 16.0), "triad": (3, 24.0), "write": (1, 8.0)}
+# (blocks, unroll) shapes: grid-stride loops over 1024 / 2048 / 4096 blocks with 1 or 4 dwordx4 in flight per lane,
+# and (r06) blocks = 0: the guide's float4-copy shape, a grid covering the array once (no loop), 1 / 2 / 4 dwordx4
+# per thread
+CEILING_SHAPES = [(b, u) for b in (1024, 2048, 4096) for u in (1, 4)] + [(0, u) for u in (1, 2, 4)]
 
 
 def stream_ceilings(n):
     """This GPU's streaming ceilings on arrays of the level's size, measured in this run beside the kernels
     they bound: the triad (2 streamed reads + 1 streamed write, 24 B per element: the smoother's byte mix),
-    a copy (1 read + 1 write) and a read-only stream, each 16 B per lane (dwordx4) in a grid-stride loop
-    (gs_debug_bw), the best over 1024 / 2048 / 4096 blocks x 1 / 4 loads in flight per lane x default /
-    non-temporal policy. Boxes differ by up to ~25 %, so the kernel's fraction of these is reported next
+    a copy (1 read + 1 write), a read-only and a store-only stream, each 16 B per lane (dwordx4), the best
+    over CEILING_SHAPES x default / non-temporal policy (gs_debug_bw); per kind also the best of each shape
+    family (grid-stride / flat). Boxes differ by up to ~25 %, so the kernel's fraction of these is reported next
     to the fraction of the 8 TB/s datasheet peak."""
     kl = gsv.diag()  # the streaming probes live in the diagnostics library
     A = torch.rand(n, dtype=torch.float64, device="cuda")
@@ -295,29 +302,38 @@ def stream_ceilings(n):
     st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     out = {}
+    def shape_name(blocks, unroll, nt):
+        s = (f"{blocks} blocks, grid-stride, {unroll} dwordx4 in flight per lane" if blocks > 0 else
+             f"flat grid covering the array, {unroll} dwordx4 per thread, no loop")
+        return s + (", nt" if nt else ", default policy")
+
     for name, (kind, bpe) in CEILING_KINDS.items():
-        best = None
-        for blocks in (1024, 2048, 4096):
-            for unroll in (1, 4):
-                for nt in (1, 0):
-                    def run():
-                        rc = kl.gs_debug_bw(kind, unroll, nt, blocks, O.data_ptr(), A.data_ptr(), B.data_ptr(), n,
-                                            sink.data_ptr(), st.cuda_stream)
-                        assert rc == 0, rc
-                    for _ in range(2):
-                        run()
-                    e0.record(st)
-                    for _ in range(8):
-                        run()
-                    e1.record(st)
-                    torch.cuda.synchronize()
-                    ms = e0.elapsed_time(e1) / 8
-                    if best is None or ms < best[0]:
-                        best = (ms, blocks, unroll, nt)
+        best, fam = None, {}
+        for blocks, unroll in CEILING_SHAPES:
+            for nt in (1, 0):
+                def run():
+                    rc = kl.gs_debug_bw(kind, unroll, nt, blocks, O.data_ptr(), A.data_ptr(), B.data_ptr(), n,
+                                        sink.data_ptr(), st.cuda_stream)
+                    assert rc == 0, rc
+                for _ in range(2):
+                    run()
+                e0.record(st)
+                for _ in range(8):
+                    run()
+                e1.record(st)
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / 8
+                if best is None or ms < best[0]:
+                    best = (ms, blocks, unroll, nt)
+                f = "flat" if blocks <= 0 else "grid_stride"
+                if f not in fam or ms < fam[f][0]:
+                    fam[f] = (ms, blocks, unroll, nt)
         ms, blocks, unroll, nt = best
-        out[name] = {"kernel": (f"streaming {name}, {int(bpe)} B per element, 16 B per lane, {blocks} blocks, "
-                                f"{unroll} load(s) in flight per lane, {'nt' if nt else 'default policy'}"),
-                     "elements": n, "ms": round(ms, 4), "gbps": round(bpe * n / (ms * 1e-3) / 1e9, 1)}
+        out[name] = {"kernel": f"streaming {name}, {int(bpe)} B per element, 16 B per lane, " +
+                               shape_name(blocks, unroll, nt),
+                     "elements": n, "ms": round(ms, 4), "gbps": round(bpe * n / (ms * 1e-3) / 1e9, 1),
+                     "by_shape": {f: {"gbps": round(bpe * n / (v[0] * 1e-3) / 1e9, 1), "shape": shape_name(*v[1:])}
+                                  for f, v in fam.items()}}
     del A, B, O
     return out
 
@@ -347,6 +363,98 @@ def newton_timing(n, iters):
     if iters > 1:
         out["ms_per_later_iteration"] = round((ms - ms1) / (iters - 1), 2)
     return out
+
+
+KERNEL_OPS = {"pair", "sweep", "pro", "residual", "resrestrict", "restrict", "prolongadd", "applyadd", "coarse",
+              "tiledpre", "tiledpro", "norm", "copy", "newtonF", "axpy", "bfac", "newtonFupdate"}
+
+
+def launches_per_cycle(p):
+    """Kernel launches one more V-cycle adds to the solve's schedule, counted on the driver's own schedule trace
+    (gs_zslab_schedule, one rank: no device touched): solves of maxiter 2 and 3 differ by one steady-state cycle."""
+    import ctypes as C
+    d = gsv.driver()
+
+    def count(maxiter):
+        q = gsv.GridParams(maxiter=maxiter, tol=0.0, gridDim=p.gridDim, mode=p.mode, preSmoothing=p.preSmoothing,
+                           postSmoothing=p.postSmoothing).to_abi()
+        n = C.c_int64()
+        assert d.gs_zslab_schedule(C.byref(q), 1, 0, 0, None, 0, C.byref(n)) == 0
+        buf = C.create_string_buffer(n.value + 1)
+        assert d.gs_zslab_schedule(C.byref(q), 1, 0, 0, buf, n.value + 1, C.byref(n)) == 0
+        ops = [l.split()[0] for l in buf.value.decode().splitlines() if l.strip()]
+        return sum(op in KERNEL_OPS for op in ops), ops
+
+    a, _ = count(2)
+    b, ops = count(3)
+    return b - a
+
+
+def config2_timing(n=128, cycles=10):
+    """BASELINE config #2: 128^3 linear 7-point, 2+2 smoothing, 10 V-cycles, fp64 (CpuSolver::solve,
+    src/cpu/CpuSolver.cpp:12-43 with vcycle :85-139). The whole 10-cycle solve as the reference runs it (initial
+    residual, ten V-cycles, every norm read back; host wall clock), after one untimed solve on the same grid; the
+    steady-state cycle (gs_grid_time_vcycles); the launches one cycle takes (the driver's schedule trace); and the
+    device ms per level of one cycle (a second grid with the per-level HIP-event clock, GS_METRICS: that clock turns
+    the norm-wait overlap off, so its cycle is the unpipelined one)."""
+    import ctypes as C
+    drv = gsv.driver()
+    p = gsv.GridParams(maxiter=cycles, tol=0.0, gridDim=(n, n, n), mode=gsv.GS_LINEAR, preSmoothing=2,
+                       postSmoothing=2)
+    out = {"config": f"{n}^3 linear 7-point, 2+2, {cycles} V-cycles, fp64 (BASELINE config #2)"}
+    with gsv.HipGridData(p) as g:
+        gsv.HipSolver.solve(g)  # warm-up: first touch of every level
+        walls = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            hist = gsv.HipSolver.solve(g)
+            walls.append((time.perf_counter() - t0) * 1e3)
+        out["solve_ms"] = round(min(walls), 3)
+        out["solve_ms_runs"] = [round(w, 3) for w in walls]
+        out["ms_per_cycle"] = round(min(walls) / cycles, 4)
+        out["residuals_last_run"] = [hist[0], hist[-1]]
+        ms, last = C.c_double(), C.c_double()
+        if drv.gs_grid_time_vcycles(g.handle, 50, C.byref(ms), C.byref(last)):
+            raise gsv.GpuSolveError(drv.gs_last_error().decode())
+        out["steady_cycle_ms"] = round(ms.value / 50, 4)
+    try:
+        out["launches_per_cycle"] = launches_per_cycle(p)
+    except Exception as e:  # noqa: BLE001 (reported, never required)
+        out["launches_per_cycle"] = {"error": str(e)}
+    out.update(level_split(p))
+    return out
+
+
+def level_split(p):
+    """Device ms per V-cycle by level: a grid of the same params created with the per-level HIP-event clock
+    (GS_METRICS=1, read at grid creation), one solve of p.maxiter cycles. That clock records events around each
+    level's down- and up-leg work and turns the norm-wait overlap off, so its cycle is the unpipelined one."""
+    import ctypes as C
+    drv = gsv.driver()
+    old = os.environ.get("GS_METRICS")
+    os.environ["GS_METRICS"] = "1"
+    try:
+        with gsv.HipGridData(p) as g:
+            gsv.HipSolver.solve(g)
+            nl = g.numLevels()
+            lv = (C.c_double * nl)()
+            line = C.create_string_buffer(4096)
+            if drv.gs_grid_metrics(g.handle, line, 4096, lv, nl):
+                raise gsv.GpuSolveError(drv.gs_last_error().decode())
+            ms = [float(x) for x in lv]
+            return {"level_ms_per_cycle": [round(x, 4) for x in ms],
+                    "levels_ge1_ms_per_cycle": round(sum(ms[1:]), 4),
+                    "level_ms_note": ("device ms per V-cycle by level (HIP events around each level's down- and up-leg "
+                                      "work, unpipelined cycle, GS_METRICS grid; levels of the one-launch coarse end "
+                                      "are booked to the level it starts from)")}
+    except Exception as e:  # noqa: BLE001 (reported, never required)
+        return {"level_ms_per_cycle": {"error": f"{type(e).__name__}: {e}"}}
+    finally:
+        if old is None:
+            os.environ.pop("GS_METRICS", None)
+        else:
+            os.environ["GS_METRICS"] = old
 
 
 CONFIG5_FILE = os.path.join(REPO, "profiles", "config5_single_gpu.json")
@@ -573,8 +681,15 @@ def main():
         rows = [x.tolist() for x in allp]
         fin = lambda x: round(x, 4) if math.isfinite(x) else None  # noqa: E731 (JSON has no NaN)
         gaps = [r[1] - r[2] for r in rows if math.isfinite(r[2])]
+        slab_bytes = BYTES_PER_LUP * float(dims[0]) * dims[1] * dims[2] / world
         multi = {"rank_ms_per_step": [fin(r[0]) for r in rows],
                  "rank_pair_ms": [fin(r[1]) for r in rows],
+                 # per GPU: 24 B x the rank's slab points / its overlapped pair's average launch time, over 8 TB/s
+                 "rank_pair_frac_of_peak": [fin(slab_bytes / (r[1] * 1e-3) / 1e9 / PEAK_GBPS) if r[1] > 0 else None
+                                            for r in rows],
+                 "rank_pair_frac_of_peak_no_exchange": [
+                     fin(slab_bytes / (r[2] * 1e-3) / 1e9 / PEAK_GBPS) if math.isfinite(r[2]) and r[2] > 0 else None
+                     for r in rows],
                  "rank_pair_ms_no_exchange": [fin(r[2]) for r in rows],
                  "exchange_ms_per_pair_max": fin(max(gaps)) if gaps else None,
                  "rank_halo_host_us_per_call": [fin(r[3]) for r in rows],
@@ -633,6 +748,8 @@ def main():
                   "first_residual": res}
             if world == 1:  # the other two level-0 passes of the V-cycle, each alone
                 vc["level0_kernels"] = vcycle_level0_kernels(grid, max(4, min(a.steps, 20)))
+                vc.update(level_split(gsv.GridParams(maxiter=5, tol=0.0, gridDim=dims, mode=gsv.GS_LINEAR,
+                                                     preSmoothing=2, postSmoothing=2)))
 
     cta_ab = None
     if world > 1 and a.cta_ab:
@@ -648,13 +765,19 @@ def main():
                 g2 = None
                 try:
                     g2 = make_grid(params, rank, world, ctas=c)
-                    el, _, kms, _, _ = timed_window(g2, a.warmup, min(a.ramp_ms, 200.0), a.steps)
-                    res = (el, kms)
                 except Exception as e:  # noqa: BLE001 (reported, never required)
                     err = f"{type(e).__name__}: {e}"
-                finally:
-                    if g2 is not None:
-                        g2.close()
+                # every rank has its grid (or none has) before any rank enters the timed window's collectives
+                if not any_rank(err is not None):
+                    try:
+                        el, _, kms, _, _ = timed_window(g2, a.warmup, min(a.ramp_ms, 200.0), a.steps)
+                        res = (el, kms)
+                    except Exception as e:  # noqa: BLE001 (reported, never required)
+                        err = f"{type(e).__name__}: {e}"
+                elif err is None:
+                    err = "grid creation failed on another rank"
+                if g2 is not None:
+                    g2.close()
                 if any_rank(err is not None):
                     cta_ab.setdefault(str(c), []).append({"error": err or "failed on another rank"})
                     continue
@@ -724,10 +847,24 @@ def main():
         else:
             speedup["same_job_error"] = (c5_same_job or {}).get("error", "not measured (--config5 0)")
 
-    cpu = None
-    if rank == 0 and world == 1 and a.cpu_sweeps > 0:
+    c2 = None
+    if world == 1 and a.config2:
         try:
-            cpu = cpu_baseline(n, a.cpu_sweeps, a.cpu_vcycles)
+            c2 = config2_timing()
+        except Exception as e:  # noqa: BLE001 (reported, never required)
+            c2 = {"error": f"{type(e).__name__}: {e}"}
+
+    cpu = None
+    if rank == 0 and a.cpu_sweeps > 0:
+        # north_star: the CPU reference "timed on the same box's host cores ... in the same run" at every N: rank 0
+        # runs it after every GPU leg of this job (the other ranks are done); N > 1 takes a reduced sample
+        try:
+            if world == 1:
+                cpu = cpu_baseline(n, a.cpu_sweeps, a.cpu_vcycles)
+            else:
+                cpu = cpu_baseline(n, max(2, a.cpu_sweeps // 3), 0)
+                cpu["note"] = (f"rank 0 of {world}, after every GPU leg of this job, reduced sample; the GPU line's value "
+                               f"is the whole job's ({world} GPUs)")
         except Exception as e:  # the baseline is reported, never required
             cpu = {"error": str(e)}
 
@@ -769,9 +906,14 @@ def main():
                          "frac_of_measured_ceiling": round(achieved / ceiling["gbps"], 4) if ceiling else None,
                          "frac_of_best_ceiling": (round(achieved / max(c["gbps"] for c in ceilings.values()), 4)
                                                   if ceilings else None),
+                         "frac_of_best_store_ceiling": (
+                             round(achieved / max(ceilings[k]["gbps"] for k in ("copy", "triad", "write")), 4)
+                             if ceilings else None),
                          "ceiling_note": ("frac_of_measured_ceiling: of the streaming triad (the smoother's 2 reads + "
-                                          "1 write), frac_of_best_ceiling: of the fastest of the triad, copy and "
-                                          "read-only streams measured in this run (measured_ceilings)"),
+                                          "1 write), frac_of_best_store_ceiling: of the fastest stream that stores "
+                                          "(triad, copy, store-only), frac_of_best_ceiling: of the fastest of those "
+                                          "and the read-only stream, all measured in this run in two shapes "
+                                          "(measured_ceilings)"),
                          "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
                          "kernel": (pair_kernel + ": two fused sweeps per launch (24 B per point per launch)"
                                     if fused else "k_rb: one sweep per launch (24 B per point per launch)"),
@@ -793,6 +935,7 @@ def main():
             "vcycle": vc,
             "newton": newton,
             "config5_single_gpu": c5,
+            "config2": c2,
             "speedup_vs_1gpu_same_grid": speedup,
             "cpu_baseline": cpu,
             "kernel_build": gsv.build_info(),

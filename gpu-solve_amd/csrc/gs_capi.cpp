@@ -193,7 +193,10 @@ int gs_grid_level(void* grid, int level, gs_level* out)
     return 0;
 }
 
-double* gs_grid_field(void* grid, int level, int field)
+// `writable`: the caller may write through the pointer (gs_grid_field, uploads), so the driver stops assuming
+// anything about newtonV it derived earlier; reads (downloads, dumps) leave that state alone, so a rank that only
+// reads its newtonV schedules exactly what the others do
+static double* field_ptr(void* grid, int level, int field, bool writable)
 {
     auto& g = G(grid);
     if (level < 0 || level >= (int)g.numLevels()) return nullptr;
@@ -201,8 +204,8 @@ double* gs_grid_field(void* grid, int level, int field)
     switch (field) {
     case 0: return L.v ? L.v.data() : nullptr;
     case 1: return L.restV ? L.restV.data() : nullptr;
-    case 2: // (a caller may write through the pointer: the driver no longer assumes newtonV = 0)
-        g.newtonVTouched();
+    case 2:
+        if (writable) g.newtonVTouched();
         return L.newtonV ? L.newtonV.data() : nullptr;
     case 3: return L.f ? L.f.data() : nullptr;
     case 4: return L.r ? L.r.data() : nullptr;
@@ -211,12 +214,14 @@ double* gs_grid_field(void* grid, int level, int field)
     }
 }
 
+double* gs_grid_field(void* grid, int level, int field) { return field_ptr(grid, level, field, true); }
+
 hipStream_t gs_grid_stream(void* grid) { return G(grid).stream(); }
 
 static int copy_field(void* grid, int level, int field, double* host, const double* src_host)
 {
     return guarded([&] {
-        double* d = gs_grid_field(grid, level, field);
+        double* d = field_ptr(grid, level, field, host == nullptr);
         if (!d) throw gs::Error("no such field on this level");
         const gs_level& L = G(grid).getLevel(level).geom;
         const size_t w = sizeof(double) * (size_t)(L.nx + 2), rows = (size_t)((L.ny + 2) * (L.nz + 2));
@@ -523,12 +528,17 @@ int gs_zslab_loopback_run(const gs_params* p, int nranks, int64_t min_points, in
     std::vector<std::string> errs(nranks);
     std::vector<double> h0;
     const gs::GridParams params = toParams(p);
+    // test hook: GS_LOOPBACK_TOUCH_NEWTONV=r marks rank r's newtonV as handed out before the solve (what
+    // gs_grid_field does), so that rank alone loses the zero-newtonV shortcut unless the solver agrees on it
+    const char* touchEnv = std::getenv("GS_LOOPBACK_TOUCH_NEWTONV");
+    const int touchRank = touchEnv && *touchEnv ? std::atoi(touchEnv) : -1;
     auto body = [&](int r) {
         try {
             gs::check((int)hipSetDevice(dev), "hipSetDevice");
             auto comm = gs::makeLoopbackComm(hub, r);
             gs::HipGridData g(params, comm.get(), min_points);
             gs::HipSolver::jacobi(g, 0, (std::size_t)sweeps);
+            if (r == touchRank) g.newtonVTouched();
             if (solve) {
                 g.printProgress = false;
                 std::vector<double> h;

@@ -329,9 +329,13 @@ __device__ __forceinline__ double op_value(const Coef& k, double c, double xp, d
 // IEEE quotient is inf — both non-finite. Per 512^3 launch: pair 0.871-0.873 vs 0.897-0.914 ms, prolongation pair
 // 0.960-0.965 vs 0.989-0.997 ms; Newton iteration -0.5 ms (r05p, profiles/r05/r05p_newton_b_quotient_ab.txt; one
 // Newton step only: 18 ulp, 1 % faster; a range branch around it: r05o). GS_EXP_NB_IEEE: the IEEE division (A/B).
+// The clamp is symmetric (r06): B = gamma (1 + w) e^w is negative for w < -1, so preFac + B can be negative; a
+// denominator of magnitude above 2^1000 (-inf included) keeps its sign. Denominators of magnitude 2^-1000 .. 2^1000
+// of either sign stay within the 1 ulp (test_nb_quotient_ulps); below that the reciprocal overflows to inf, where the
+// IEEE quotient may still be finite (a point whose denominator cancels to ~1e-301 has left the contract anyway).
 __device__ __forceinline__ double nb_recip(double den)
 {
-    const double d = den > 0x1p1000 ? 0x1p1000 : den;
+    const double d = __builtin_fabs(den) > 0x1p1000 ? __builtin_copysign(0x1p1000, den) : den;
     return hh_recip(d);
 }
 __device__ __forceinline__ double nb_quot(double r, double den)

@@ -352,6 +352,36 @@ __global__ __launch_bounds__(256) void k_bw(double* __restrict__ out, const doub
     if (KIND == 0 && acc == -1.2345e300) *sink = acc; // keeps the loads alive
 }
 
+// The same streams in the guide's shape (MI355X_MICROARCH.md: "6.29 TB/s measured, float4 copy"): no grid-stride
+// loop, a grid that covers the array once, each thread UNROLL dwordx4 at stride 256 inside its block's contiguous
+// run of UNROLL x 4 KB (every wave-instruction 1 KB contiguous); KIND as k_bw.
+template <int KIND, int UNROLL, bool NT>
+__global__ __launch_bounds__(256) void k_bwflat(double* __restrict__ out, const double* __restrict__ a,
+                                                const double* __restrict__ b, int64_t n2, double* __restrict__ sink)
+{
+    const int64_t i0 = (int64_t)blockIdx.x * (256 * UNROLL) + threadIdx.x;
+    double2 va[UNROLL], vb[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+        const int64_t i = i0 + 256 * u;
+        if (i < n2) {
+            if (KIND != 1) va[u] = ld2s<NT>(a + 2 * i);
+            if (KIND == 3) vb[u] = ld2s<NT>(b + 2 * i);
+        }
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+        const int64_t i = i0 + 256 * u;
+        if (i >= n2) continue;
+        if (KIND == 0) acc += va[u].x + va[u].y;
+        else if (KIND == 1) st2s<NT>(out + 2 * i, 1.0, 2.0);
+        else if (KIND == 2) st2s<NT>(out + 2 * i, va[u].x, va[u].y);
+        else st2s<NT>(out + 2 * i, va[u].x + 0.8 * vb[u].x, va[u].y + 0.8 * vb[u].y);
+    }
+    if (KIND == 0 && acc == -1.2345e300) *sink = acc; // keeps the loads alive
+}
+
 // A copy with the resource footprint of RCCL's gfx950 transport kernels (ncclDevKernel_Generic: 256
 // VGPRs, 37664 B of LDS per 256-thread workgroup): the clobber of v255 makes the allocator reserve
 // every VGPR. Stands in for the ghost exchange in tools/exchange_probe.py (when does a workgroup
@@ -614,12 +644,25 @@ int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const dou
         hipLaunchKernelGGL(k_sleep, dim3(1), dim3(64), 0, st, n);
         return launch_status();
     }
-    if (n < 0 || (n & 1) || kind < 0 || kind > 4 || blocks <= 0) return GS_EINVAL;
+    if (n < 0 || (n & 1) || kind < 0 || kind > 4 || (kind == 4 && blocks <= 0)) return GS_EINVAL;
     if (kind == 4) { // copy at RCCL's transport-kernel footprint (k_fatcopy)
         hipLaunchKernelGGL(k_fatcopy, dim3(blocks), dim3(256), 0, st, out, a, n / 2);
         return launch_status();
     }
     using K = void (*)(double*, const double*, const double*, int64_t, double*);
+    if (blocks <= 0) { // the flat grid (k_bwflat): unroll 1, 2 or 4 dwordx4 per thread
+        static const K flat[4][3][2] = {
+#define GS_BWF(KD) {{k_bwflat<KD, 1, false>, k_bwflat<KD, 1, true>}, {k_bwflat<KD, 2, false>, k_bwflat<KD, 2, true>}, \
+                    {k_bwflat<KD, 4, false>, k_bwflat<KD, 4, true>}}
+            GS_BWF(0), GS_BWF(1), GS_BWF(2), GS_BWF(3)
+#undef GS_BWF
+        };
+        const int u = unroll >= 4 ? 2 : (unroll >= 2 ? 1 : 0);
+        const int64_t per = 256LL << u, nb = (n / 2 + per - 1) / per;
+        if (nb <= 0 || nb > 0x7fffffff) return nb <= 0 ? 0 : GS_EINVAL;
+        hipLaunchKernelGGL(flat[kind][u][nt != 0], dim3((unsigned)nb), dim3(256), 0, st, out, a, b, n / 2, sink);
+        return launch_status();
+    }
     static const K tab[4][2][2] = {
         {{k_bw<0, 1, false>, k_bw<0, 1, true>}, {k_bw<0, 4, false>, k_bw<0, 4, true>}},
         {{k_bw<1, 1, false>, k_bw<1, 1, true>}, {k_bw<1, 4, false>, k_bw<1, 4, true>}},

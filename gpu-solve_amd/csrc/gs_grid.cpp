@@ -56,6 +56,21 @@ DeviceField& DeviceField::operator=(DeviceField&& o) noexcept
     return *this;
 }
 
+bool HipGridData::allRanks(bool flag)
+{
+    if (trace || !comm_ || comm_->size() <= 1) return flag;
+    const hipStream_t s = stream();
+    const double on = flag ? 1.0 : 0.0;
+    std::vector<double> all((std::size_t)comm_->size(), 0.0);
+    check((int)hipMemcpyAsync(dNorm_, &on, sizeof(double), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+    comm_->allgather1(dNorm_, dRankSums_, s);
+    check((int)hipMemcpyAsync(all.data(), dRankSums_, sizeof(double) * all.size(), hipMemcpyDeviceToHost, s),
+          "hipMemcpyAsync");
+    comm_->sync(s);
+    for (const double a : all) flag = flag && a != 0.0;
+    return flag;
+}
+
 void DeviceField::zero(hipStream_t s)
 {
     if (base_) check((int)hipMemsetAsync(base_, 0, sizeof(double) * alloc_, s), "hipMemsetAsync");
@@ -220,7 +235,7 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
         if (l + 1 < nlev) L.r = DeviceField(nx, ny, nz, s, dry); // restriction source
         if (mode == NONLINEAR && l > 0) L.restV = DeviceField(nx, ny, nz, s, dry);
         if (mode == NEWTON) L.newtonV = DeviceField(nx, ny, nz, s, dry);
-        if (mode == NEWTON && sw.newtonB) L.bfac = DeviceField(nx, ny, nz, s, dry);
+        if (mode == NEWTON && sw.newtonB && dry) L.bfac = DeviceField(nx, ny, nz, s, dry); // (else: below)
         if (mode == NEWTON && l == 1 && nlev >= 3 && !L.distributed) L.newtonVNext = DeviceField(nx, ny, nz, s, dry);
         L.geom = gs_level{nx, ny, nz, L.v.ldy(), L.v.ldz(), L.lo - 1, L.h};
         maxParts = std::max(maxParts, gs_residual_num_partials(&stencilAbi, &L.geom));
@@ -287,15 +302,22 @@ HipGridData::HipGridData(const GridParams& grid, Comm* comm, int64_t agglomerate
     // GS_METRICS is read by each process, but the per-level clock changes the collective schedule (no
     // pipelined cycles; the last closing norm is kept): a distributed grid runs it only if EVERY rank has it
     // on, so that all ranks issue the same exchanges and collectives
-    if (comm_ && comm_->size() > 1) {
-        const double on = clock.on ? 1.0 : 0.0;
-        std::vector<double> all((std::size_t)comm_->size(), 0.0);
-        check((int)hipMemcpyAsync(dNorm_, &on, sizeof(double), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
-        comm_->allgather1(dNorm_, dRankSums_, s);
-        check((int)hipMemcpyAsync(all.data(), dRankSums_, sizeof(double) * all.size(), hipMemcpyDeviceToHost, s),
-              "hipMemcpyAsync");
-        comm_->sync(s);
-        for (const double a : all) clock.on = clock.on && a != 0.0;
+    clock.on = allRanks(clock.on);
+    // GS_NEWTON_B's factor fields: one more level-sized array per NEWTON level (~8.6 GB at 1023^3). If they do not
+    // fit, the grid runs the reference-expression inner solves (mode 2, GS_NO_NEWTON_B) instead of failing; the
+    // choice is agreed across ranks (it changes which kernels run, never the exchanges, but stays uniform)
+    if (mode == NEWTON && sw.newtonB) {
+        bool ok = true;
+        try {
+            for (auto& L : levels_) L.bfac = DeviceField(L.geom.nx, L.geom.ny, L.geom.nz, s, dry);
+        } catch (const Error&) {
+            ok = false;
+            (void)hipGetLastError(); // (the failed hipMalloc's sticky error)
+        }
+        if (!allRanks(ok)) {
+            sw.newtonB = false;
+            for (auto& L : levels_) L.bfac = DeviceField();
+        }
     }
     // the fused prolongation pair's edge-column workspaces (column-block rows), one per stream, at their
     // largest size now: proPlanes never reallocates them
@@ -1211,7 +1233,12 @@ void NewtonSolver::solve(HipGridData& grid)
     else
         check(gs_copy(grid.newtonF.data(), L0.f.data(), L0.f.span(), s), "gs_copy");
     const double initialResidual = compF(grid);
-    grid.newtonR1_ = false; // (the first findError restricts level 1 itself: fields may have been set since)
+    // fields may have been set since the last solve: the first findError restricts level 1 and forms level 0's factor
+    // itself, and skips the restrictions of a zero newtonV only if EVERY rank still has it (a rank that handed its
+    // newtonV pointer out would restrict, and restrictions exchange ghost planes on distributed levels)
+    grid.newtonR1_ = false;
+    grid.bfacFresh_ = 0;
+    grid.newtonVZero_ = grid.allRanks(grid.newtonVZero_);
     if (history) history->push_back(initialResidual);
     if (print) std::cout << "Inital newton residual: " << initialResidual << '\n';
 

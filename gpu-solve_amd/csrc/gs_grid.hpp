@@ -193,8 +193,18 @@ public:
     {
         return newtonB_ ? L.bfac.data() : (L.newtonV ? L.newtonV.data() : nullptr);
     }
-    // newtonV may have been written from outside the solvers (the C ABI's field pointer): see newtonVZero_
-    void newtonVTouched() { newtonVZero_ = false; }
+    // newtonV may have been written from outside the solvers (the C ABI's writable field pointer or an upload):
+    // nothing derived from it may be reused — not the zero-field shortcut (newtonVZero_), nor level 1's restriction
+    // (newtonR1_) or level 0's factor (bfacFresh_) that the last update pass wrote
+    void newtonVTouched()
+    {
+        newtonVZero_ = false;
+        newtonR1_ = false;
+        bfacFresh_ = 0;
+    }
+    // AND of `flag` over every rank of a distributed grid (an allgather of one word; the flag itself elsewhere), so
+    // that a schedule decision taken from per-process state issues the same collectives on every rank
+    bool allRanks(bool flag);
     // ghost planes of a distributed level's field (no-op otherwise); depth 2 where possible for
     // iterate fields (the fused pair reads two ghost planes of v)
     void halo(LevelData& L, DeviceField& fld, hipStream_t s, int depth = 1);

@@ -55,7 +55,8 @@ int gs_debug_pair_variant(int variant, const gs_stencil* S, const gs_level* L, d
                           double* v_out, const double* f, int zc, hipStream_t stream);
 int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t n, hipStream_t stream);
 /* Streaming ceilings: kind 0 read a, 1 write out, 2 copy, 3 triad; unroll 1 or 4 dwordx4 per thread,
- * nt = non-temporal, `blocks` workgroups of 256 threads (grid-stride). Kind 4: a non-temporal copy
+ * nt = non-temporal, `blocks` workgroups of 256 threads (grid-stride); blocks <= 0 (kinds 0-3): a grid that
+ * covers the array once, no grid-stride loop, unroll 1, 2 or 4 dwordx4 per thread. Kind 4: a non-temporal copy
  * at the resource footprint of RCCL's transport kernels (256 VGPRs, 37 KB of LDS per workgroup;
  * unroll / nt ignored), the stand-in exchange of tools/exchange_probe.py. Kind 5: one wave that sleeps n x
  * s_sleep(127) (~3.4 us each), touching no memory (out / a / b / blocks ignored). */

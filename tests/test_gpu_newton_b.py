@@ -249,6 +249,38 @@ def test_newton_solve_g_bit_identical(dims):
         assert f_g[key].tobytes() == f_b[key].tobytes(), key
 
 
+@pytest.mark.parametrize("dims", [(63, 63, 63), (130, 66, 34)])
+def test_solve_upload_newtonv_solve(dims):
+    """A solve, then newtonV replaced through the C ABI (gs_grid_upload), then a second solve on the same grid: the
+    second solve must linearise at the uploaded newtonV on every level — level 0's factor the first solve's last update
+    pass left behind (bfacFresh_) and its level-1 restriction (newtonR1_) are stale — so it equals the same sequence
+    with level 0's factor formed by its own pass (GS_NEWTON_B_FUSED=0), bit for bit. A download of newtonV between
+    the solves (read-only: no state dropped) leaves the second solve unchanged too."""
+    p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=NEWTON, preSmoothing=2, postSmoothing=2)
+    x = rand_field(np.random.default_rng(5), dims, -0.2, 0.2)
+
+    def run(upload, **e):
+        with env(**e):
+            with gsv.HipGridData(p) as g:
+                gsv.NewtonSolver.solve(g)
+                g.field(0, "newtonV")  # read-only
+                if upload:
+                    g.set_field(0, "newtonV", x)
+                hist = gsv.NewtonSolver.solve(g)
+                return hist, {n: g.field(0, n) for n in ("v", "newtonV")}
+
+    h_fused, f_fused = run(True)
+    h_sep, f_sep = run(True, GS_NEWTON_B_FUSED=0)
+    assert np.all(np.isfinite(h_sep)), h_sep
+    assert h_fused == h_sep
+    for n in f_sep:
+        assert f_fused[n].tobytes() == f_sep[n].tobytes(), n
+    h_plain, _ = run(False)
+    h_plain_sep, _ = run(False, GS_NEWTON_B_FUSED=0)
+    assert h_plain == h_plain_sep
+    assert h_plain != h_fused  # (the upload did change the linearisation point)
+
+
 def test_nb_quotient_ulps():
     """The GS_NEWTON_B Jacobi quotient (nb_quot: r times the refined reciprocal of den clamped at 2^1000) against the
     IEEE quotient: within 1 ulp over the denominators the solver forms (preFac + B, from the coarsest level's ~24
@@ -256,10 +288,15 @@ def test_nb_quotient_ulps():
     (NaN in, NaN out; den = 0), and den = inf gives a quotient below |r| 2^-999 (the IEEE one is 0)."""
     rng = np.random.default_rng(11)
     n = 400_000
-    den = np.exp(rng.uniform(np.log(20.0), np.log(2.0 ** 40), n))
+    # the solver's range (preFac + B from ~24 up), then (r06) negative denominators — B < 0 where w < -1 — and
+    # small magnitudes of either sign down to 2^-990, where the reciprocal is still normal
+    m = n // 2
+    den = np.exp(rng.uniform(np.log(20.0), np.log(2.0 ** 40), m))
+    mag = np.exp2(rng.uniform(-990.0, 40.0, n - m))
+    den = np.concatenate([den, np.where(rng.random(n - m) < 0.5, -mag, mag)])
     r = rng.normal(0, 1, n) * np.exp(rng.uniform(-200, 200, n))
     edge_r = np.array([1.0, -2.0, 0.0, 1e300, -1e-300])
-    edge_den = np.array([np.inf, np.nan, 0.0])
+    edge_den = np.array([np.inf, -np.inf, np.nan, 0.0])
     den = np.concatenate([den, np.repeat(edge_den, edge_r.size), np.full(3, 1e6)])
     r = np.concatenate([r, np.tile(edge_r, edge_den.size), [np.nan, np.inf, -np.inf]])
     dr, dd = torch.from_numpy(r).cuda(), torch.from_numpy(den).cuda()
@@ -276,11 +313,14 @@ def test_nb_quotient_ulps():
     worst = np.max(np.abs(got[body][fin] - want[body][fin]) / ulp)
     print(f"nb_quot: max {worst} ulp, {np.mean(got[body][fin] != want[body][fin]):.4f} of the quotients differ from r / den")
     assert worst <= NB_QUOT_ULPS, worst
-    e = slice(n, n + 3 * edge_r.size)
+    ne = edge_den.size * edge_r.size
+    e = slice(n, n + ne)
     ge, de, re_ = got[e], den[e], r[e]
     inf_d = np.isinf(de)
     assert np.all(np.abs(ge[inf_d]) <= np.abs(re_[inf_d]) * 2.0 ** -999)
+    nz = inf_d & (re_ != 0)  # the clamp keeps the denominator's sign: r / -inf is -r 2^-1000 (or -0), not +
+    assert np.all(np.signbit(ge[nz]) == (np.signbit(re_[nz]) ^ np.signbit(de[nz])))
     assert np.all(np.isnan(ge[np.isnan(de)]))
     assert not np.any(np.isfinite(ge[(de == 0) & (re_ != 0)]))
-    tail = got[n + 3 * edge_r.size:]
+    tail = got[n + ne:]
     assert np.isnan(tail[0]) and np.isinf(tail[1]) and np.isinf(tail[2])

@@ -177,3 +177,18 @@ def test_newton_fused_update_on_slabs(monkeypatch, dims, nranks):
         assert a == b and rel(a, c) < 1e-12, (a, b, c)
     np.testing.assert_array_equal(v[:, :, 1:-1], v2[:, :, 1:-1])
     np.testing.assert_array_equal(v[:, :, 1:-1], ref_v[:, :, 1:-1])
+
+
+@pytest.mark.parametrize("dims,nranks,touch", [((127, 63, 64), 2, 0), ((127, 63, 96), 3, 2)])
+def test_newton_zero_shortcut_agreed_across_ranks(monkeypatch, dims, nranks, touch):
+    """The first findError skips the restrictions of a still-zero newtonV, and restrictions exchange ghost planes on
+    distributed levels: when ONE rank has handed its newtonV out (gs_grid_field, here the loopback runner's test hook)
+    the ranks must agree before deciding, or that rank issues exchanges nobody answers. With the agreement every rank
+    restricts (zeros), and the solve is bit-identical to the untouched one."""
+    p = gsv.GridParams(maxiter=2, tol=0.0, gridDim=dims, mode=2)
+    h, v = loopback(p, nranks, 0, 0, True)
+    monkeypatch.setenv("GS_LOOPBACK_TOUCH_NEWTONV", str(touch))
+    h2, v2 = loopback(p, nranks, 0, 0, True)
+    assert all(math.isfinite(a) for a in h), h
+    assert h == h2
+    np.testing.assert_array_equal(v[:, :, 1:-1], v2[:, :, 1:-1])
