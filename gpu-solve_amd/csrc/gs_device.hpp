@@ -138,7 +138,7 @@ bool valid_stencil(const gs_stencil* S)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh, specCached;
     int xhSwizzle, midZc, rrZc, rrZcBig, oneRoundMid, rbZc;
-    int slabZc, pairZc, rrNr, rrNtu, rrReverse, rrNg;
+    int slabZc, pairZc, rrNr, rrNtu, rrReverse, rrNg, rrDma, ccLds;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
     {
@@ -152,7 +152,7 @@ struct Knobs {
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
           newtonXh(num("GS_NEWTON_XH", 1) != 0), specCached(num("GS_SPEC_CACHED", 0) != 0),
           xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), oneRoundMid(num("GS_PAIR_ONE_ROUND_MID", 0)), rbZc(num("GS_RB_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
-          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 2)), rrReverse(num("GS_RR_REVERSE", 1)), rrNg(num("GS_RR_NG", 0)),
+          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 2)), rrReverse(num("GS_RR_REVERSE", 1)), rrNg(num("GS_RR_NG", 0)), rrDma(num("GS_RR_DMA", 0)), ccLds(num("GS_CC_LDS", 1)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
     }
@@ -1343,6 +1343,266 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
 }
 
 // ---------------------------------------------------------------------------------------------
+// Residual + full weighting with an LDS-DMA operand ring ("rr2d", r06; verdict r05 item 1). Same arithmetic,
+// term order and outputs as k_rr2 (bit-identical), built for the case k_rr2 handles worst: its operands of a plane
+// step are loaded at the top of the step and waited for at once (no register room for a prefetch ring: PF = false),
+// so at two waves per SIMD the loads are exposed every step (PMC wait_inst 0.43-0.46 of wave cycles).
+// Here the operands never occupy VGPRs while in flight: every wave streams ITS OWN columns of the operand rows of
+// fine plane p + 2 straight into an LDS ring (global_load_lds_dwordx4, one instruction per row and wave, inline asm:
+// M0 is written in the statement that reads it) while it computes plane p, and waits for plane p's with a hand-
+// counted s_waitcnt vmcnt before the step's one barrier. A ring slot holds what the residual of fine plane p adds to
+// the register window (v of planes p-1, p): v of plane p+1 on the computed rows, the two halo rows of plane p, f
+// (and NEWTON's w) of plane p, RR + 2 + RR (+ RR) rows of the block's width; three slots (plane p read, p+1 and p+2
+// in flight). The wave-edge columns x-1 / x+2 of every v row are read straight from the neighbouring waves' columns
+// of the slot (LDS broadcast reads, one plane early), so only r's wave-edge column still goes through an exchange.
+// One fine plane per step; the restriction of coarse plane Z runs at step 2Z+2, once r of plane 2Z+1 has crossed
+// the wave edges with that step's barrier.
+// The counted wait is exact because every VMEM operation of the loop is accounted for: RROWS DMA instructions per
+// step and 2 NR coarse stores at every even step, stores that never branch away (an invalid point writes to a sink
+// word instead); so before the wait of step p exactly one plane's DMA group and one store group are younger than
+// plane p's DMA group (the prologue issues one group of sink stores to make step p0 look the same).
+// LDS: 3 slots x RROWS rows x WX KB (512-point rows: 144 KB LINEAR NR = 2, 132 KB NEWTON NR = 1): one block per CU.
+constexpr int RR2D_WXMAX = 4, RR2D_SLOTS = 3;
+__device__ double gs_rr2d_sink[2 * WAVE]; // where the unconditional stores of invalid points go
+
+template <int MODE, int NR, bool WR>
+constexpr int rr2d_rows()
+{
+    return (2 * NR + 1) * (WR ? 3 : 2) + 2;
+}
+
+template <int N>
+__device__ __forceinline__ void rr2d_wait()
+{
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+// 16 B per lane from gsrc into LDS at byte address lds_dst + 16 lane (lds_dst wave-uniform)
+__device__ __forceinline__ void rr2d_dma(const double* gsrc, unsigned lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+template <int MODE, int NR, bool UN, bool WR>
+__global__ __launch_bounds__(WAVE* RR2D_WXMAX) void k_rr2d(Coef k, const double* __restrict__ v,
+                                                           const double* __restrict__ f, const double* __restrict__ w,
+                                                           double* __restrict__ ca, double* __restrict__ cb, int fnx,
+                                                           int fny, int fnz, int64_t fldy, int64_t fldz, int cnx,
+                                                           int cny, int cnz, int64_t cldy, int64_t cldz, int ZC, int zhi)
+{
+    constexpr int RR = 2 * NR + 1;                   // computed fine rows; v rows 0 .. RR+1 (0, RR+1: halo rows)
+    constexpr int RROWS = rr2d_rows<MODE, NR, WR>(); // ring rows per slot (= DMA instructions per wave and step)
+    constexpr int RV = 0, RH = RR, RF = RR + 2, RW = 2 * RR + 2; // first row of each operand in a slot
+    constexpr int NSTORE = 2 * NR;                               // coarse stores per wave at an even step
+    constexpr int NWAIT = RROWS + NSTORE;                        // VMEM operations younger than the awaited plane's
+    static_assert(NWAIT <= 63, "vmcnt field");
+    extern __shared__ double ring[]; // [slot][row][WX * 128 doubles]; then re, ve
+    const int lane = threadIdx.x;
+    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int WX = blockDim.y;
+    const int RS = WX * 2 * WAVE; // doubles per ring row
+    double* re = ring + RR2D_SLOTS * RROWS * RS; // r(2X+1) edges: [parity][1 + wave][row]
+    double* ve = re + 2 * (RR2D_WXMAX + 2) * RR;  // prologue v edges: [1 + wave][side][row]
+    const int tid = lane + WAVE * wx;
+    for (int i = tid; i < 2 * (RR2D_WXMAX + 2) * RR + (RR2D_WXMAX + 2) * 2 * RR; i += WAVE * WX) re[i] = 0.0;
+    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+    const int Y = 1 + NR * (int)(tile % gridDim.x);
+    const int Zb = 1 + (int)(tile / gridDim.x) * ZC, Ze = min(Zb + ZC - 1, cnz);
+    const int X = 1 + wx * WAVE + lane;
+    const int x = 2 * X - 1, xl = min(x, fnx + 1);
+    const bool okx0 = x <= fnx, okx1 = x + 1 <= fnx;
+    int64_t roff[RR + 2];
+    bool rowc[RR + 2];
+#pragma unroll
+    for (int j = 0; j < RR + 2; j++) {
+        const int y = 2 * Y - 2 + j;
+        roff[j] = (int64_t)min(max(y, 0), fny + 1) * fldy;
+        rowc[j] = y >= 1 && y <= fny;
+    }
+    auto at = [&](const double* b, int j, int p) {
+        return b + xl + roff[j] + (int64_t)min(max(p, 0), fnz + 1 + zhi) * fldz;
+    };
+    typedef __attribute__((address_space(3))) double* lds_dp;
+    const unsigned lbase = (unsigned)(uintptr_t)(lds_dp)ring;
+    // this wave's 1 KB of ring row r of slot s, as an LDS byte address (wave-uniform)
+    auto dst = [&](int s, int r) {
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)(lbase + 8u * (unsigned)((s * RROWS + r) * RS + wx * 2 * WAVE)));
+    };
+    // the operand rows of fine plane p into slot s
+    auto dma_plane = [&](int s, int p) {
+#pragma unroll
+        for (int j = 0; j < RR; j++) rr2d_dma(at(v, j + 1, p + 1), dst(s, RV + j));
+        rr2d_dma(at(v, 0, p), dst(s, RH));
+        rr2d_dma(at(v, RR + 1, p), dst(s, RH + 1));
+#pragma unroll
+        for (int j = 0; j < RR; j++) rr2d_dma(at(f, j + 1, p), dst(s, RF + j));
+        if constexpr (WR) {
+#pragma unroll
+            for (int j = 0; j < RR; j++) rr2d_dma(at(w, j + 1, p), dst(s, RW + j));
+        }
+    };
+    auto row_at = [&](int s, int r) { return ring + (s * RROWS + r) * RS; };
+    auto lds2 = [&](int s, int r) { return *reinterpret_cast<const double2*>(row_at(s, r) + wx * 2 * WAVE + 2 * lane); };
+    double* sink = gs_rr2d_sink;
+
+    // r = f - A v on fine plane p (k_rr2's resid: same expression, same term order; 0 outside the interior), with the
+    // plane's 2 RR divisions by h^2 batched behind one range branch (div_hh_n: the same quotients bit for bit) — at
+    // one wave per SIMD a branch per point would expose every point's latency
+    auto resid = [&](const double2 (&Vm)[RR], const double2 (&Vc)[RR], const double2 (&H)[2], const double2 (&Vp)[RR],
+                     const double2 (&F)[RR], const double2 (&W)[RR], const double (&CL)[RR], const double (&CR)[RR], int p,
+                     double2 (&R)[RR]) {
+        const bool pin = p >= 1 && (p <= fnz || (zhi && p == fnz + 1));
+        double q[2 * RR];
+#pragma unroll
+        for (int j = 0; j < RR; j++) {
+            const double2 c = Vc[j];
+            const double2 ym = j == 0 ? H[0] : Vc[j - 1], yp = j == RR - 1 ? H[1] : Vc[j + 1];
+            const double xm0 = lane_from_left<true>(c.y, CL[j]);
+            const double xp1 = lane_from_right<true>(c.x, CR[j]);
+            q[2 * j] = stencil_sum<UN>(k, c.x, c.y, xm0, yp.x, ym.x, Vp[j].x, Vm[j].x);
+            q[2 * j + 1] = stencil_sum<UN>(k, c.y, xp1, c.x, yp.y, ym.y, Vp[j].y, Vm[j].y);
+        }
+        div_hh_n(k, q);
+#pragma unroll
+        for (int j = 0; j < RR; j++) {
+            const double w0 = newtonish(MODE) ? W[j].x : 0.0, w1 = newtonish(MODE) ? W[j].y : 0.0;
+            const double a0 = op_finish<MODE>(k, q[2 * j], Vc[j].x, w0);
+            const double a1 = op_finish<MODE>(k, q[2 * j + 1], Vc[j].y, w1);
+            const bool ok = pin && rowc[j + 1];
+            R[j] = make_double2((ok && okx0) ? F[j].x - a0 : 0.0, (ok && okx1) ? F[j].y - a1 : 0.0);
+        }
+    };
+
+    // prologue: the window v(p0 - 1), v(p0) (p0 = 2Zb - 1) by ordinary loads, v(p0)'s wave-edge columns through LDS
+    const int p0 = 2 * Zb - 1;
+    double2 Vm[RR], V0[RR];
+    double CL0[RR], CR0[RR];
+#pragma unroll
+    for (int j = 0; j < RR; j++) {
+        Vm[j] = ld2(at(v, j + 1, p0 - 1));
+        V0[j] = ld2(at(v, j + 1, p0));
+    }
+    __syncthreads(); // (the zeroed re / ve)
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < RR; j++) ve[((wx + 1) * 2 + 0) * RR + j] = V0[j].x;
+    }
+    if (lane == WAVE - 1) {
+#pragma unroll
+        for (int j = 0; j < RR; j++) ve[((wx + 1) * 2 + 1) * RR + j] = V0[j].y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RR; j++) {
+        CL0[j] = uniform_d(ve[(wx * 2 + 1) * RR + j]);
+        CR0[j] = uniform_d(ve[((wx + 2) * 2 + 0) * RR + j]);
+    }
+    // (every ordinary load above is complete: the ve writes needed them)
+    dma_plane(p0 % RR2D_SLOTS, p0);
+    dma_plane((p0 + 1) % RR2D_SLOTS, p0 + 1);
+#pragma unroll
+    for (int i = 0; i < NSTORE; i++) // the store group step p0's count expects (volatile: never merged or dropped)
+        *reinterpret_cast<volatile double*>(sink + (i & 1) * WAVE + lane) = 0.0;
+
+    double2 Ra[RR], Rb[RR], Rc[RR]; // r of planes p-3, p-2, p-1 entering step p
+    double Na[RR], Nb[RR];          // r(2X+1) of planes p-3, p-2
+#pragma unroll
+    for (int j = 0; j < RR; j++) {
+        Ra[j] = Rb[j] = Rc[j] = make_double2(0.0, 0.0);
+        Na[j] = Nb[j] = 0.0;
+    }
+    const int pe = 2 * Ze + 2;
+    auto step = [&](const int p, const bool even) {
+        const int s = p % RR2D_SLOTS;
+        rr2d_wait<NWAIT>();                              // plane p landed (every wave), slot p-1 read by every wave
+        dma_plane((p + 2) % RR2D_SLOTS, p + 2);          // into the slot plane p-1 used
+        double2 Vn[RR], H[2], F[RR], W[RR];
+        double CLn[RR], CRn[RR], En[RR];
+        // every LDS read of the step first, none under a branch (one wait for all of them): v(p+1)'s wave-edge
+        // columns for the next step (from clamped columns, zero beyond the level's x-boundaries), r(2X+1) of plane
+        // p-1 (its edge word written last step, visible past this step's barrier)
+        const int cl = wx > 0 ? wx * 2 * WAVE - 1 : 0, cr = wx + 1 < WX ? (wx + 1) * 2 * WAVE : 0;
+        const double* rprev = re + ((p - 1) & 1) * (RR2D_WXMAX + 2) * RR + (wx + 2) * RR;
+#pragma unroll
+        for (int j = 0; j < RR; j++) {
+            Vn[j] = lds2(s, RV + j);
+            F[j] = lds2(s, RF + j);
+            if constexpr (WR) W[j] = lds2(s, RW + j);
+            else if constexpr (MODE == GS_NEWTON_B) W[j] = make_double2(k.gamma, k.gamma); // (GS_NEWTON_G)
+            else W[j] = make_double2(0.0, 0.0);
+            CLn[j] = row_at(s, RV + j)[cl];
+            CRn[j] = row_at(s, RV + j)[cr];
+            En[j] = rprev[j];
+        }
+        H[0] = lds2(s, RH);
+        H[1] = lds2(s, RH + 1);
+#pragma unroll
+        for (int j = 0; j < RR; j++) {
+            CLn[j] = wx > 0 ? uniform_d(CLn[j]) : 0.0;
+            CRn[j] = wx + 1 < WX ? uniform_d(CRn[j]) : 0.0;
+        }
+        double2 R[RR];
+        resid(Vm, V0, H, Vn, F, W, CL0, CR0, p, R);
+        double Nc[RR];
+#pragma unroll
+        for (int j = 0; j < RR; j++) Nc[j] = lane_from_right<true>(Rc[j].x, uniform_d(En[j]));
+        // plane p's edge word, for the next step
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < RR; j++) re[(p & 1) * (RR2D_WXMAX + 2) * RR + (wx + 1) * RR + j] = R[j].x;
+        }
+        if (even) { // restriction of coarse plane Z = p / 2 - 1 from r of planes 2Z-1 .. 2Z+1 = p-3 .. p-1
+            const int Z = p / 2 - 1;
+#pragma unroll
+            for (int i = 0; i < NR; i++) {
+                double acc = 0.0;
+#pragma unroll
+                for (int a = -1; a <= 1; a++)
+#pragma unroll
+                    for (int b = -1; b <= 1; b++)
+#pragma unroll
+                        for (int c = -1; c <= 1; c++) {
+                            const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
+                                               ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                            const int j = 2 * i + b + 1;
+                            const double2 rp = c < 0 ? Ra[j] : (c == 0 ? Rb[j] : Rc[j]);
+                            const double rn = c < 0 ? Na[j] : (c == 0 ? Nb[j] : Nc[j]);
+                            acc += wgt * (a < 0 ? rp.x : (a == 0 ? rp.y : rn));
+                        }
+                const bool ok = Z >= Zb && Z <= Ze && X <= cnx && Y + i <= cny;
+                const int64_t q = X + (Y + i) * cldy + (int64_t)Z * cldz;
+                double* pa = ok ? ca + q : sink + lane;
+                double* pb = (ok && cb) ? cb + q : sink + WAVE + lane;
+                *pa = acc;
+                *pb = acc;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RR; j++) {
+            Vm[j] = V0[j];
+            V0[j] = Vn[j];
+            CL0[j] = CLn[j];
+            CR0[j] = CRn[j];
+            Ra[j] = Rb[j];
+            Rb[j] = Rc[j];
+            Rc[j] = R[j];
+            Na[j] = Nb[j];
+            Nb[j] = Nc[j];
+        }
+    };
+    for (int p = p0; p <= pe; p += 2) {
+        step(p, false);
+        step(p + 1, true);
+    }
+    // drain: the last DMAs must land before the block's LDS can be reused by another block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------------------
 // Trilinear prolongation, closed form per fine point (the reference's inject + X, Y, Z passes,
 // CpuSolver.cpp:240-290, combined in the same X -> Y -> Z order). Fine index P-1 is never written by
 // the reference (stays 0) and coarse index Pc-1 is the zero boundary, so along each axis:
@@ -1905,6 +2165,178 @@ __global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
         __syncthreads();
         smooth(l - 1, P.post);
     }
+}
+
+// The same coarse cycle with every field of its levels in LDS (r06, verdict r05 item 5: config #2's 128^3 cycle is
+// launch- and latency-bound, and this one launch was ~28 us of its ~120). k_coarse_cycle spends ~1.2 us per
+// operator phase on a dependent chain: two integer divisions to index the point, L2 loads (~0.5 us), the store's
+// drain before the barrier. Here a level's points are indexed once per thread (one point per thread: levels of
+// <= CCL_T points), the fields are copied into LDS once (compact padded layout, boundaries included), every phase
+// reads and writes LDS only, and every field the global kernel writes is copied back at the end — so the fields
+// after the launch are bit for bit k_coarse_cycle's (same expressions; the stencil offsets and the restriction /
+// prolongation strides are the LDS layout's).
+constexpr int CCL_T = 512, CCL_LDS_DOUBLES = 8 * 1024; // threads; LDS budget (64 KB)
+struct CclLevel {
+    int v, va, f, r, rv, w; // LDS offsets (doubles) of the level's fields, -1: absent
+    int ldy, ldz, n;        // LDS strides, padded size
+    int nx, ny, nz, vz;
+    Coef k; // stencil offsets of the LDS layout
+};
+struct CclGlobal { // a level's global fields (as k_coarse_cycle's CcLevel) and strides
+    double *v, *va, *f, *r, *rv, *w;
+    int64_t ldy, ldz;
+};
+struct CclPlan {
+    CclGlobal G[CC_MAXLEV];
+    CclLevel L[CC_MAXLEV];
+    int n, pre, post, total;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(CCL_T) void k_coarse_cycle_lds(CclPlan P)
+{
+    extern __shared__ double lds[];
+    const int tid = threadIdx.x;
+    // this thread's point on every level (x fastest), computed once
+    int px[CC_MAXLEV], py[CC_MAXLEV], pz[CC_MAXLEV];
+    bool pok[CC_MAXLEV];
+#pragma unroll
+    for (int l = 0; l < CC_MAXLEV; l++) {
+        const CclLevel& L = P.L[l < P.n ? l : 0];
+        const int n = L.nx * L.ny * L.nz;
+        pok[l] = l < P.n && tid < n;
+        const int ii = pok[l] ? tid : 0;
+        const int t = ii / L.nx, z = t / L.ny;
+        px[l] = 1 + ii - t * L.nx;
+        py[l] = 1 + t - z * L.ny;
+        pz[l] = 1 + z;
+    }
+    // copy a padded global field into LDS (gfield: element (0,0,0) of the padded array)
+    auto stage = [&](const double* g, const CclGlobal& G, const CclLevel& L, int off, bool in) {
+        const int sx = L.nx + 2, sxy = sx * (L.ny + 2);
+        for (int i = tid; i < L.n; i += CCL_T) {
+            const int z = i / sxy, rem = i - z * sxy, y = rem / sx, x = rem - y * sx;
+            const int64_t q = x + y * G.ldy + (int64_t)z * G.ldz;
+            if (in) lds[off + i] = g[q];
+            else const_cast<double*>(g)[q] = lds[off + i];
+        }
+    };
+    auto fields = [&](int l, bool in, auto&& fn) { // (global pointer, LDS offset) of every field of level l
+        const CclGlobal& G = P.G[l];
+        const CclLevel& L = P.L[l];
+        fn(G.v, L.v);
+        fn(G.va, L.va);
+        fn(G.f, L.f);
+        if (L.r >= 0) fn(G.r, L.r);
+        if (L.rv >= 0) fn(G.rv, L.rv);
+        if (L.w >= 0 && in) fn(G.w, L.w); // (read only)
+    };
+    for (int l = 0; l < P.n; l++)
+        fields(l, true, [&](const double* g, int off) { stage(g, P.G[l], P.L[l], off, true); });
+    __syncthreads();
+
+    unsigned alt = 0, zero = 0;
+    for (int l = 0; l < P.n; l++)
+        if (P.L[l].vz) zero |= 1u << l;
+    auto cur = [&](int l) { return lds + (((alt >> l) & 1) ? P.L[l].va : P.L[l].v); };
+    // dst[p] (dst2[p]) = fn(x, y, z, p) at this thread's point of level l (cc_map, one point per thread)
+    auto map = [&](int l, double* dst, double* dst2, auto&& fn) {
+        const CclLevel& L = P.L[l];
+        const int p = px[l] + py[l] * L.ldy + pz[l] * L.ldz;
+        const double val = fn(px[l], py[l], pz[l], (int64_t)p);
+        if (pok[l]) {
+            dst[p] = val;
+            if (dst2) dst2[p] = val;
+        }
+    };
+    auto materialize = [&](int l) {
+        if (!((zero >> l) & 1)) return;
+        map(l, cur(l), nullptr, [&](int, int, int, int64_t) { return 0.0; });
+        __syncthreads();
+        zero &= ~(1u << l);
+    };
+    auto smooth = [&](int l, int sweeps) {
+        const CclLevel& L = P.L[l];
+        if (sweeps == 0) materialize(l);
+        for (int s = 0; s < sweeps; s++) {
+            const bool uz = (zero >> l) & 1;
+            const double* in = cur(l);
+            double* out = lds + (((alt >> l) & 1) ? L.v : L.va);
+            const double* w = L.w >= 0 ? lds + L.w : nullptr;
+            const double* f = lds + L.f;
+            map(l, out, nullptr, [&](int, int, int, int64_t p) {
+                double c, wv;
+                const double a = cc_op<MODE>(L.k, in, uz, w, p, c, wv);
+                const double r = f[p] - a;
+                return jacobi_update<MODE>(L.k, c, r, wv);
+            });
+            __syncthreads();
+            alt ^= 1u << l;
+            zero &= ~(1u << l);
+        }
+    };
+    auto restrict_to = [&](const double* src, const CclLevel& F, double* ca, double* cb, int lc) {
+        map(lc, ca, cb, [&](int x, int y, int z, int64_t) {
+            const double* c0 = src + 2 * x + (2 * y) * F.ldy + (2 * z) * F.ldz;
+            double acc = 0.0;
+#pragma unroll
+            for (int a = -1; a <= 1; a++)
+#pragma unroll
+                for (int b = -1; b <= 1; b++)
+#pragma unroll
+                    for (int c = -1; c <= 1; c++) {
+                        const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
+                                           ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
+                        acc += wgt * c0[a + b * F.ldy + c * F.ldz];
+                    }
+            return acc;
+        });
+    };
+
+    for (int l = 0; l + 1 < P.n; l++) {
+        const CclLevel &F = P.L[l], &C = P.L[l + 1];
+        smooth(l, P.pre);
+        const double* u = cur(l);
+        const double* fw = F.w >= 0 ? lds + F.w : nullptr;
+        const double* ff = lds + F.f;
+        map(l, lds + F.r, nullptr, [&](int, int, int, int64_t p) {
+            double c, wv;
+            const double a = cc_op<MODE>(F.k, u, false, fw, p, c, wv);
+            return ff[p] - a;
+        });
+        __syncthreads();
+        restrict_to(lds + F.r, F, lds + C.f, nullptr, l + 1);
+        if (MODE == GS_NONLINEAR) restrict_to(u, F, lds + C.rv, cur(l + 1), l + 1);
+        __syncthreads();
+        if (MODE == GS_NONLINEAR) {
+            const double* crv = lds + C.rv;
+            double* cf = lds + C.f;
+            map(l + 1, cf, nullptr, [&](int, int, int, int64_t p) {
+                double c, wv;
+                const double a = cc_op<GS_NONLINEAR>(C.k, crv, false, nullptr, p, c, wv);
+                return cf[p] + a;
+            });
+            __syncthreads();
+        }
+    }
+    smooth(P.n - 1, P.pre + P.post);
+    for (int l = P.n - 1; l > 0; l--) {
+        const CclLevel& C = P.L[l];
+        materialize(l);
+        const double* cv = cur(l);
+        double* fv = cur(l - 1);
+        const double* crv = C.rv >= 0 ? lds + C.rv : nullptr;
+        map(l - 1, fv, nullptr, [&](int x, int y, int z, int64_t p) {
+            const double e = MODE == GS_NONLINEAR ? prolong_value<true>(cv, crv, x, y, z, C.ldy, C.ldz, 0)
+                                                  : prolong_value<false>(cv, nullptr, x, y, z, C.ldy, C.ldz, 0);
+            return fv[p] + e;
+        });
+        __syncthreads();
+        smooth(l - 1, P.post);
+    }
+    // every field back: k_coarse_cycle leaves all of them written (the host reads the iterates)
+    for (int l = 0; l < P.n; l++)
+        fields(l, false, [&](const double* g, int off) { stage(g, P.G[l], P.L[l], off, false); });
 }
 
 int launch_status()

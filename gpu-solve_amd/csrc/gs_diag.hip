@@ -382,6 +382,86 @@ __global__ __launch_bounds__(256) void k_bwflat(double* __restrict__ out, const 
     if (KIND == 0 && acc == -1.2345e300) *sink = acc; // keeps the loads alive
 }
 
+// The LINEAR pair's memory skeleton without its arithmetic (r06 probe, verdict r05 item 2: where does the pair lose
+// against the flat triad?): k_tb2y's tiles (4 x-waves x 2 mirrored y-waves, RY = 2 rows per wave, one 4-row x 512-
+// column tile per block, XCD-aware tile order), its z-march over chunks of ZC planes, its loads per plane step (v rows
+// -1..RY, f rows 0..RY, dwordx4 per lane) with PFD steps in flight, and its stores (the wave's RY rows, one plane per
+// step) — but each output is a pointwise mix of the loaded values, no stencil, no LDS. BAR: the pair's per-step
+// workgroup barrier. 24 B per point like the pair.
+// SYNC > 0: bounded drift — before plane step i a block's leader lane waits (bounded spin) until every block has
+// finished step i - SYNC (a relaxed agent-scope counter, one add per block and step), so the blocks march the
+// planes together (the concurrent address footprint stays a few planes wide)
+template <int PFD, bool BAR, bool NTS, bool NTF, bool LEAN = false, int SYNC = 0, int RYT = 2>
+__global__ __launch_bounds__(512) void k_march(const double* __restrict__ v, const double* __restrict__ f,
+                                               double* __restrict__ out, int nx, int ny, int nz, int64_t ldy,
+                                               int64_t ldz, int ZC, unsigned* __restrict__ cnt = nullptr)
+{
+    constexpr int RY = RYT, NV = RY + 1, NS = PFD == 2 ? 4 : 2;
+    const int lane = threadIdx.x;
+    const int wx = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int wy = __builtin_amdgcn_readfirstlane(threadIdx.z);
+    const int64_t tile = xcd_tile(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+    const int y0 = 1 + (int)(tile % gridDim.x) * (2 * RY);
+    const int zb = 1 + (int)(tile / gridDim.x) * ZC, ze = min(zb + ZC - 1, nz);
+    const int x = 1 + wx * (2 * WAVE) + 2 * lane, xl = min(x, nx + 1);
+    const bool okx = x + 1 <= nx;
+    int64_t roff[RY + 2];
+    bool rowc[RY + 2];
+#pragma unroll
+    for (int j = -1; j <= RY; j++) {
+        const int y = wy ? y0 + 2 * RY - j : y0 - 1 + j;
+        roff[j + 1] = (int64_t)min(max(y, 0), ny + 1) * ldy;
+        rowc[j + 1] = y >= 1 && y <= ny;
+    }
+    auto at = [&](const double* b, int j, int z) { return b + xl + roff[j + 1] + (int64_t)min(z, nz + 1) * ldz; };
+    double2 VL[NS][NV], FL[NS][NV], HL[NS];
+    // LEAN: only the rows the wave stores (v and f rows 1..RY: 16 B per point of L2 requests, the triad's), the
+    // others taken as zero
+    auto load_slot = [&](int s, int z) {
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            VL[s][j] = (LEAN && j == 0) ? make_double2(0.0, 0.0) : ld2(at(v, j, z));
+            FL[s][j] = (LEAN && j == 0) ? make_double2(0.0, 0.0) : ld2s<NTF>(at(f, j, z));
+        }
+        HL[s] = LEAN ? make_double2(0.0, 0.0) : ld2(at(v, -1, z));
+    };
+#pragma unroll
+    for (int p = 0; p < PFD; p++) load_slot(p, zb + p);
+    const bool leader = lane == 0 && wx == 0 && wy == 0;
+    const unsigned nblk = gridDim.x * gridDim.y;
+    for (int z0 = zb; z0 <= ze; z0 += NS) {
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            const int z = z0 + u;
+            if (SYNC > 0) {
+                const int i = z - zb;
+                if (leader && i >= SYNC) {
+                    const unsigned need = nblk * (unsigned)(i - SYNC + 1);
+                    for (int spin = 0; spin < 2000; spin++) {
+                        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
+                __builtin_amdgcn_s_barrier();
+            }
+            load_slot((u + PFD) % NS, z + PFD);
+            if (BAR) __builtin_amdgcn_s_barrier();
+            if (SYNC > 0 && leader && z <= ze)
+                __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (z <= ze) {
+#pragma unroll
+                for (int j = 1; j <= RY; j++) {
+                    const double2 a = VL[u][j], b = j == 1 ? VL[u][0] : VL[u][j - 1], c = FL[u][j];
+                    const double2 h = j == 1 ? HL[u] : FL[u][0];
+                    const double o0 = a.x + 0.25 * b.x + 0.8 * c.x + 1e-300 * h.x;
+                    const double o1 = a.y + 0.25 * b.y + 0.8 * c.y + 1e-300 * h.y;
+                    if (rowc[j + 1] && okx) st2s<NTS>(out + xl + roff[j + 1] + (int64_t)z * ldz, o0, o1);
+                }
+            }
+        }
+    }
+}
+
 // A copy with the resource footprint of RCCL's gfx950 transport kernels (ncclDevKernel_Generic: 256
 // VGPRs, 37664 B of LDS per 256-thread workgroup): the clobber of v255 makes the allocator reserve
 // every VGPR. Stands in for the ghost exchange in tools/exchange_probe.py (when does a workgroup
@@ -670,6 +750,54 @@ int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const dou
         {{k_bw<3, 1, false>, k_bw<3, 1, true>}, {k_bw<3, 4, false>, k_bw<3, 4, true>}},
     };
     hipLaunchKernelGGL(tab[kind][unroll > 1][nt != 0], dim3(blocks), dim3(256), 0, st, out, a, b, n / 2, sink);
+    return launch_status();
+}
+
+int gs_debug_march(int pfd, int bar, int nts, int ntf, int zc, const gs_level* L, const double* v, const double* f,
+                   double* out, hipStream_t st)
+{
+    if (!L || bad_level(L) || !v || !f || !out || zc < 1 || (pfd != 1 && pfd != 2) || L->nx > 512 || L->ny % 4)
+        return GS_EINVAL;
+    if (ntf >= 6) { // (ntf 6 / 7: RY = 1 / 4 rows per wave, 2 / 8-row tiles; pfd 2, barrier, nt stores)
+        const int ry = ntf == 6 ? 1 : 4;
+        if (L->ny % (2 * ry)) return GS_EINVAL;
+        const dim3 g((unsigned)(L->ny / (2 * ry)), (unsigned)((L->nz + zc - 1) / zc)), b(WAVE, 4, 2);
+        if (ry == 1) hipLaunchKernelGGL((k_march<2, true, true, false, false, 0, 1>), g, b, 0, st, v, f, out,
+                                        (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, nullptr);
+        else hipLaunchKernelGGL((k_march<1, true, true, false, false, 0, 4>), g, b, 0, st, v, f, out, (int)L->nx,
+                                (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, nullptr);
+        return launch_status();
+    }
+    if (ntf >= 3) { // (ntf 3 / 4 / 5: bounded drift of 2 / 4 / 8 plane steps, pfd 2, barrier, nt stores; the counter
+                    // lives in out's plane -1, zeroed here)
+        const dim3 g((unsigned)(L->ny / 4), (unsigned)((L->nz + zc - 1) / zc)), b(WAVE, 4, 2);
+        if ((int64_t)g.x * g.y > 256) return GS_EINVAL; // (every block must be resident: one per CU)
+        unsigned* cnt = reinterpret_cast<unsigned*>(out - L->ldz); // (plane -1 of the padded layout)
+        if (hipMemsetAsync(cnt, 0, 16, st) != hipSuccess) return GS_EINVAL;
+#define GS_MS(D) hipLaunchKernelGGL((k_march<2, true, true, false, false, D>), g, b, 0, st, v, f, out, (int)L->nx, \
+                                    (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, cnt)
+        if (ntf == 3) GS_MS(2); else if (ntf == 4) GS_MS(4); else GS_MS(8);
+#undef GS_MS
+        return launch_status();
+    }
+    if (ntf >= 2) { // (ntf 2: LEAN loads, pfd 2, nt stores)
+        const dim3 g((unsigned)(L->ny / 4), (unsigned)((L->nz + zc - 1) / zc)), b(WAVE, 4, 2);
+        if (bar) hipLaunchKernelGGL((k_march<2, true, true, false, true>), g, b, 0, st, v, f, out, (int)L->nx,
+                                    (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, nullptr);
+        else hipLaunchKernelGGL((k_march<2, false, true, false, true>), g, b, 0, st, v, f, out, (int)L->nx,
+                                (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, nullptr);
+        return launch_status();
+    }
+    using K = void (*)(const double*, const double*, double*, int, int, int, int64_t, int64_t, int, unsigned*);
+    static const K tab[2][2][2][2] = {
+#define GS_MF(P, B) {{k_march<P, B, false, false>, k_march<P, B, false, true>}, \
+                     {k_march<P, B, true, false>, k_march<P, B, true, true>}}
+        {GS_MF(1, false), GS_MF(1, true)}, {GS_MF(2, false), GS_MF(2, true)}
+#undef GS_MF
+    };
+    const dim3 g((unsigned)(L->ny / 4), (unsigned)((L->nz + zc - 1) / zc)), b(WAVE, 4, 2);
+    hipLaunchKernelGGL(tab[pfd - 1][bar != 0][nts != 0][ntf != 0], g, b, 0, st, v, f, out, (int)L->nx, (int)L->ny,
+                       (int)L->nz, L->ldy, L->ldz, zc, nullptr);
     return launch_status();
 }
 

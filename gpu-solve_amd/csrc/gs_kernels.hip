@@ -378,6 +378,77 @@ int gs_residual_restrict_slab(const gs_stencil* S, const gs_level* fl, int mode,
     const bool ldsOnly = kKnobs.rrLds; // A/B switch for tools/ measurements
     const bool rr2 = !ldsOnly && canonical_order(S) && zoff == 0 && wxs <= RR2_WXMAX;
     if (zhi && !rr2) return GS_EINVAL; // the slab form exists for the register kernel only
+    // the LDS-DMA ring form (k_rr2d): rows of up to 4 x-waves (fine rows <= 512 points) whose lanes never clamp a
+    // column (every lane's dwordx4 lies inside the padded row). GS_RR_DMA: 0 never (default), 1 the factor-loading
+    // GS_NEWTON_B launches only, 2 every eligible launch (A/B). Measured slower where it matters (r06):
+    // alone, 512^3 LINEAR 0.533-0.540 vs 0.459 ms, NEWTON_B 0.710-0.712 vs 0.726 ms, GS_NEWTON_G 0.576 vs 0.494 ms;
+    // in the Newton cycle (GS_RR_DMA=1) 29.26 / 29.40 vs 28.58 / 28.55 ms per iteration. One block per CU (the ring
+    // takes 132-144 KB) and LDS-DMA's landing rate, ~25-32 GB/s per CU measured here (MI355X_MICROARCH.md
+    // 'ldsdma-fill': ~25 GB/s per CU), cap it below what two register-loading blocks per CU reach
+    const bool dmaMode = kKnobs.rrDma >= 2 || (kKnobs.rrDma == 1 && mode == GS_NEWTON_B && !bconst);
+    const bool dma = rr2 && dmaMode && wxs <= RR2D_WXMAX && 2 * WAVE * wxs - 1 <= fl->nx + 1;
+    if (dma) {
+        const bool big = fl->nx * fl->ny * fl->nz >= ((int64_t)1 << RR2_NR2_LOG2_POINTS);
+        const int nr_env = kKnobs.rrNr;
+        const int nr = mode == GS_LINEAR && (nr_env == 2 || (nr_env == 0 && big)) ? 2 : 1;
+        const bool wr = newtonish(mode) && !bconst;
+        const int rr = 2 * nr + 1;
+        const int rrows = rr * (wr ? 3 : 2) + 2;
+        const size_t lds = sizeof(double) * ((size_t)RR2D_SLOTS * rrows * wxs * 2 * WAVE +
+                                             (size_t)3 * (RR2D_WXMAX + 2) * rr * 2);
+        const int64_t rows = (cl->ny + nr - 1) / nr;
+        const void* fn = nullptr;
+#define GS_RR2D_FN(M, N, U, W) fn = (const void*)&k_rr2d<M, N, U, W>
+#define GS_RR2D_U(M, N, W) do { if (k.unit) GS_RR2D_FN(M, N, true, W); else GS_RR2D_FN(M, N, false, W); } while (0)
+        if (mode == GS_LINEAR && nr == 2) GS_RR2D_U(GS_LINEAR, 2, false);
+        else if (mode == GS_LINEAR) GS_RR2D_U(GS_LINEAR, 1, false);
+        else if (mode == GS_NEWTON_B && wr) GS_RR2D_U(GS_NEWTON_B, 1, true);
+        else if (mode == GS_NEWTON_B) GS_RR2D_U(GS_NEWTON_B, 1, false);
+        else if (mode == GS_NONLINEAR) GS_RR2D_U(GS_NONLINEAR, 1, false);
+        else GS_RR2D_U(GS_NEWTON, 1, true);
+#undef GS_RR2D_U
+#undef GS_RR2D_FN
+        static std::mutex m;
+        static std::map<std::pair<const void*, size_t>, int64_t> cap;
+        int64_t resident = 0;
+        {
+            std::lock_guard<std::mutex> lk(m);
+            const auto key = std::make_pair(fn, lds);
+            auto it = cap.find(key);
+            if (it == cap.end()) {
+                int per = 0;
+                if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, (int)(WAVE * wxs), lds) != hipSuccess)
+                    per = 0;
+                (void)hipGetLastError();
+                it = cap.emplace(key, per * device_cus()).first;
+            }
+            resident = it->second;
+        }
+        if (resident > 0) {
+            // one round of resident blocks: z-chunks so that rows x chunks ~ the blocks the GPU holds at once
+            const int64_t chunks = std::max<int64_t>(1, resident / rows);
+            int64_t zc = (cl->nz + chunks - 1) / chunks;
+            zc = zc < 1 ? 1 : zc;
+            if (kKnobs.rrZcBig > 0 && big) zc = kKnobs.rrZcBig;
+            if (kKnobs.rrZc > 0 && !big) zc = kKnobs.rrZc;
+            const dim3 g((unsigned)rows, (unsigned)((cl->nz + zc - 1) / zc)), b(WAVE, (unsigned)wxs);
+            Coef ka = k;
+            const double *va = v, *fa = f, *wa = w;
+            double *caa = ca, *cba = cb;
+            int fnx = (int)fl->nx, fny = (int)fl->ny, fnz = (int)fl->nz, cnx = (int)cl->nx, cny = (int)cl->ny,
+                cnz = (int)cl->nz, zca = (int)zc, zha = zhi ? 1 : 0;
+            int64_t fldy = fl->ldy, fldz = fl->ldz, cldy = cl->ldy, cldz = cl->ldz;
+            void* args[] = {&ka, &va, &fa, &wa, &caa, &cba, &fnx, &fny, &fnz, &fldy, &fldz,
+                            &cnx, &cny, &cnz, &cldy, &cldz, &zca, &zha};
+            const hipError_t e = hipLaunchKernel(fn, g, b, args, lds, st);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                return (int)e;
+            }
+            return launch_status();
+        }
+    }
     if (rr2) {
         // >= 2048 blocks of one coarse row where the level has them (chunks of <= 32 coarse planes)
         // LINEAR levels of >= 2^26 points: two coarse rows per block (231 VGPRs, 2 waves per SIMD): 0.507 vs
@@ -647,6 +718,54 @@ int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int m
         L.nz = (int)g->nz;
         L.vz = a.v_zero != 0;
         L.k = make_coef(S, g, omega, gamma);
+    }
+    // the LDS form (k_coarse_cycle_lds) where every level has at most CCL_T points and all fields fit the LDS
+    // budget; GS_CC_LDS=0 keeps the L2 form (A/B)
+    if (kKnobs.ccLds) {
+        CclPlan Q{};
+        Q.n = n;
+        Q.pre = pre;
+        Q.post = post;
+        int total = 0;
+        bool fits = true;
+        for (int l = 0; l < n && fits; l++) {
+            const CcLevel& G = P.L[l];
+            CclLevel& L = Q.L[l];
+            Q.G[l] = CclGlobal{G.v, G.va, G.f, G.r, G.rv, G.w, G.ldy, G.ldz};
+            L.nx = G.nx;
+            L.ny = G.ny;
+            L.nz = G.nz;
+            L.vz = G.vz;
+            L.ldy = G.nx + 2;
+            L.ldz = (G.nx + 2) * (G.ny + 2);
+            L.n = L.ldz * (G.nz + 2);
+            fits = (int64_t)G.nx * G.ny * G.nz <= CCL_T;
+            auto take = [&](const double* g) {
+                if (!g) return -1;
+                const int o = total;
+                total += L.n;
+                return o;
+            };
+            L.v = take(G.v);
+            L.va = take(G.va);
+            L.f = take(G.f);
+            L.r = l + 1 < n ? take(G.r) : -1;
+            L.rv = mode == GS_NONLINEAR && l > 0 ? take(G.rv) : -1;
+            L.w = newtonish(mode) ? take(G.w) : -1;
+            const gs_level lg{G.nx, G.ny, G.nz, L.ldy, L.ldz, 0, lv[l].geom.h};
+            L.k = make_coef(S, &lg, omega, gamma);
+        }
+        Q.total = total;
+        if (fits && total <= CCL_LDS_DOUBLES) {
+            const size_t bytes = sizeof(double) * (size_t)total;
+            if (mode == GS_LINEAR) hipLaunchKernelGGL(k_coarse_cycle_lds<GS_LINEAR>, dim3(1), dim3(CCL_T), bytes, st, Q);
+            else if (mode == GS_NONLINEAR)
+                hipLaunchKernelGGL(k_coarse_cycle_lds<GS_NONLINEAR>, dim3(1), dim3(CCL_T), bytes, st, Q);
+            else if (mode == GS_NEWTON_B)
+                hipLaunchKernelGGL(k_coarse_cycle_lds<GS_NEWTON_B>, dim3(1), dim3(CCL_T), bytes, st, Q);
+            else hipLaunchKernelGGL(k_coarse_cycle_lds<GS_NEWTON>, dim3(1), dim3(CCL_T), bytes, st, Q);
+            return launch_status();
+        }
     }
     if (mode == GS_LINEAR) hipLaunchKernelGGL(k_coarse_cycle<GS_LINEAR>, dim3(1), dim3(CC_T), 0, st, P);
     else if (mode == GS_NONLINEAR) hipLaunchKernelGGL(k_coarse_cycle<GS_NONLINEAR>, dim3(1), dim3(CC_T), 0, st, P);

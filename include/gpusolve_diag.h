@@ -62,6 +62,15 @@ int gs_debug_stream_triad(double* out, const double* a, const double* b, int64_t
  * s_sleep(127) (~3.4 us each), touching no memory (out / a / b / blocks ignored). */
 int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const double* a, const double* b, int64_t n,
                 double* sink, hipStream_t stream);
+/* The LINEAR pair's memory skeleton without its arithmetic (k_march): k_tb2y's tiles, z-march over chunks of zc
+ * planes, loads (pfd = 1 or 2 plane steps in flight) and stores, outputs a pointwise mix of the loaded values;
+ * bar: a workgroup barrier per plane step; nts / ntf: non-temporal stores / f loads (ntf 2: only the rows
+ * stored are loaded, pfd 2, nt stores; ntf 3 / 4 / 5: every block at most 2 / 4 / 8 plane steps ahead of the
+ * slowest (a relaxed agent-scope counter in out's plane -1, bounded spins; at most 256 blocks), pfd 2, nt stores;
+ * ntf 6 / 7: 1 / 4 rows per wave (2- / 8-row tiles; pfd 2 / 1), barrier, nt stores). Levels of nx <= 512 points,
+ * ny a multiple of 4. 24 B per point. */
+int gs_debug_march(int pfd, int bar, int nts, int ntf, int zc, const gs_level* L, const double* v, const double* f,
+                   double* out, hipStream_t stream);
 
 /* The production LINEAR pair with per-block timestamps (4 doubles per block in ts: start and end wall
  * clock at 100 MHz, hardware block index, HW_ID); zc > 0 overrides the plan's z-chunk. */
