@@ -138,7 +138,7 @@ bool valid_stencil(const gs_stencil* S)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh, specCached;
     int xhSwizzle, midZc, rrZc, rrZcBig, oneRoundMid, rbZc;
-    int slabZc, pairZc, rrNr, rrNtu, rrReverse, rrNg, rrDma, ccLds;
+    int slabZc, pairZc, rrNr, rrNtu, rrReverse, rrNg, rrDma;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
     {
@@ -152,7 +152,7 @@ struct Knobs {
           rrLds(getenv("GS_RR_LDS") != nullptr), zeroQ(getenv("GS_NO_ZERO_Q") == nullptr),
           newtonXh(num("GS_NEWTON_XH", 1) != 0), specCached(num("GS_SPEC_CACHED", 0) != 0),
           xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), oneRoundMid(num("GS_PAIR_ONE_ROUND_MID", 0)), rbZc(num("GS_RB_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
-          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 2)), rrReverse(num("GS_RR_REVERSE", 1)), rrNg(num("GS_RR_NG", 0)), rrDma(num("GS_RR_DMA", 0)), ccLds(num("GS_CC_LDS", 1)),
+          rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 2)), rrReverse(num("GS_RR_REVERSE", 1)), rrNg(num("GS_RR_NG", 0)), rrDma(num("GS_RR_DMA", 0)),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
     }
@@ -2165,178 +2165,6 @@ __global__ __launch_bounds__(CC_T) void k_coarse_cycle(CcPlan P)
         __syncthreads();
         smooth(l - 1, P.post);
     }
-}
-
-// The same coarse cycle with every field of its levels in LDS (r06, verdict r05 item 5: config #2's 128^3 cycle is
-// launch- and latency-bound, and this one launch was ~28 us of its ~120). k_coarse_cycle spends ~1.2 us per
-// operator phase on a dependent chain: two integer divisions to index the point, L2 loads (~0.5 us), the store's
-// drain before the barrier. Here a level's points are indexed once per thread (one point per thread: levels of
-// <= CCL_T points), the fields are copied into LDS once (compact padded layout, boundaries included), every phase
-// reads and writes LDS only, and every field the global kernel writes is copied back at the end — so the fields
-// after the launch are bit for bit k_coarse_cycle's (same expressions; the stencil offsets and the restriction /
-// prolongation strides are the LDS layout's).
-constexpr int CCL_T = 512, CCL_LDS_DOUBLES = 8 * 1024; // threads; LDS budget (64 KB)
-struct CclLevel {
-    int v, va, f, r, rv, w; // LDS offsets (doubles) of the level's fields, -1: absent
-    int ldy, ldz, n;        // LDS strides, padded size
-    int nx, ny, nz, vz;
-    Coef k; // stencil offsets of the LDS layout
-};
-struct CclGlobal { // a level's global fields (as k_coarse_cycle's CcLevel) and strides
-    double *v, *va, *f, *r, *rv, *w;
-    int64_t ldy, ldz;
-};
-struct CclPlan {
-    CclGlobal G[CC_MAXLEV];
-    CclLevel L[CC_MAXLEV];
-    int n, pre, post, total;
-};
-
-template <int MODE>
-__global__ __launch_bounds__(CCL_T) void k_coarse_cycle_lds(CclPlan P)
-{
-    extern __shared__ double lds[];
-    const int tid = threadIdx.x;
-    // this thread's point on every level (x fastest), computed once
-    int px[CC_MAXLEV], py[CC_MAXLEV], pz[CC_MAXLEV];
-    bool pok[CC_MAXLEV];
-#pragma unroll
-    for (int l = 0; l < CC_MAXLEV; l++) {
-        const CclLevel& L = P.L[l < P.n ? l : 0];
-        const int n = L.nx * L.ny * L.nz;
-        pok[l] = l < P.n && tid < n;
-        const int ii = pok[l] ? tid : 0;
-        const int t = ii / L.nx, z = t / L.ny;
-        px[l] = 1 + ii - t * L.nx;
-        py[l] = 1 + t - z * L.ny;
-        pz[l] = 1 + z;
-    }
-    // copy a padded global field into LDS (gfield: element (0,0,0) of the padded array)
-    auto stage = [&](const double* g, const CclGlobal& G, const CclLevel& L, int off, bool in) {
-        const int sx = L.nx + 2, sxy = sx * (L.ny + 2);
-        for (int i = tid; i < L.n; i += CCL_T) {
-            const int z = i / sxy, rem = i - z * sxy, y = rem / sx, x = rem - y * sx;
-            const int64_t q = x + y * G.ldy + (int64_t)z * G.ldz;
-            if (in) lds[off + i] = g[q];
-            else const_cast<double*>(g)[q] = lds[off + i];
-        }
-    };
-    auto fields = [&](int l, bool in, auto&& fn) { // (global pointer, LDS offset) of every field of level l
-        const CclGlobal& G = P.G[l];
-        const CclLevel& L = P.L[l];
-        fn(G.v, L.v);
-        fn(G.va, L.va);
-        fn(G.f, L.f);
-        if (L.r >= 0) fn(G.r, L.r);
-        if (L.rv >= 0) fn(G.rv, L.rv);
-        if (L.w >= 0 && in) fn(G.w, L.w); // (read only)
-    };
-    for (int l = 0; l < P.n; l++)
-        fields(l, true, [&](const double* g, int off) { stage(g, P.G[l], P.L[l], off, true); });
-    __syncthreads();
-
-    unsigned alt = 0, zero = 0;
-    for (int l = 0; l < P.n; l++)
-        if (P.L[l].vz) zero |= 1u << l;
-    auto cur = [&](int l) { return lds + (((alt >> l) & 1) ? P.L[l].va : P.L[l].v); };
-    // dst[p] (dst2[p]) = fn(x, y, z, p) at this thread's point of level l (cc_map, one point per thread)
-    auto map = [&](int l, double* dst, double* dst2, auto&& fn) {
-        const CclLevel& L = P.L[l];
-        const int p = px[l] + py[l] * L.ldy + pz[l] * L.ldz;
-        const double val = fn(px[l], py[l], pz[l], (int64_t)p);
-        if (pok[l]) {
-            dst[p] = val;
-            if (dst2) dst2[p] = val;
-        }
-    };
-    auto materialize = [&](int l) {
-        if (!((zero >> l) & 1)) return;
-        map(l, cur(l), nullptr, [&](int, int, int, int64_t) { return 0.0; });
-        __syncthreads();
-        zero &= ~(1u << l);
-    };
-    auto smooth = [&](int l, int sweeps) {
-        const CclLevel& L = P.L[l];
-        if (sweeps == 0) materialize(l);
-        for (int s = 0; s < sweeps; s++) {
-            const bool uz = (zero >> l) & 1;
-            const double* in = cur(l);
-            double* out = lds + (((alt >> l) & 1) ? L.v : L.va);
-            const double* w = L.w >= 0 ? lds + L.w : nullptr;
-            const double* f = lds + L.f;
-            map(l, out, nullptr, [&](int, int, int, int64_t p) {
-                double c, wv;
-                const double a = cc_op<MODE>(L.k, in, uz, w, p, c, wv);
-                const double r = f[p] - a;
-                return jacobi_update<MODE>(L.k, c, r, wv);
-            });
-            __syncthreads();
-            alt ^= 1u << l;
-            zero &= ~(1u << l);
-        }
-    };
-    auto restrict_to = [&](const double* src, const CclLevel& F, double* ca, double* cb, int lc) {
-        map(lc, ca, cb, [&](int x, int y, int z, int64_t) {
-            const double* c0 = src + 2 * x + (2 * y) * F.ldy + (2 * z) * F.ldz;
-            double acc = 0.0;
-#pragma unroll
-            for (int a = -1; a <= 1; a++)
-#pragma unroll
-                for (int b = -1; b <= 1; b++)
-#pragma unroll
-                    for (int c = -1; c <= 1; c++) {
-                        const double wgt = 0.125 * ((2.0 - (a < 0 ? -a : a)) / 2.0) *
-                                           ((2.0 - (b < 0 ? -b : b)) / 2.0) * ((2.0 - (c < 0 ? -c : c)) / 2.0);
-                        acc += wgt * c0[a + b * F.ldy + c * F.ldz];
-                    }
-            return acc;
-        });
-    };
-
-    for (int l = 0; l + 1 < P.n; l++) {
-        const CclLevel &F = P.L[l], &C = P.L[l + 1];
-        smooth(l, P.pre);
-        const double* u = cur(l);
-        const double* fw = F.w >= 0 ? lds + F.w : nullptr;
-        const double* ff = lds + F.f;
-        map(l, lds + F.r, nullptr, [&](int, int, int, int64_t p) {
-            double c, wv;
-            const double a = cc_op<MODE>(F.k, u, false, fw, p, c, wv);
-            return ff[p] - a;
-        });
-        __syncthreads();
-        restrict_to(lds + F.r, F, lds + C.f, nullptr, l + 1);
-        if (MODE == GS_NONLINEAR) restrict_to(u, F, lds + C.rv, cur(l + 1), l + 1);
-        __syncthreads();
-        if (MODE == GS_NONLINEAR) {
-            const double* crv = lds + C.rv;
-            double* cf = lds + C.f;
-            map(l + 1, cf, nullptr, [&](int, int, int, int64_t p) {
-                double c, wv;
-                const double a = cc_op<GS_NONLINEAR>(C.k, crv, false, nullptr, p, c, wv);
-                return cf[p] + a;
-            });
-            __syncthreads();
-        }
-    }
-    smooth(P.n - 1, P.pre + P.post);
-    for (int l = P.n - 1; l > 0; l--) {
-        const CclLevel& C = P.L[l];
-        materialize(l);
-        const double* cv = cur(l);
-        double* fv = cur(l - 1);
-        const double* crv = C.rv >= 0 ? lds + C.rv : nullptr;
-        map(l - 1, fv, nullptr, [&](int x, int y, int z, int64_t p) {
-            const double e = MODE == GS_NONLINEAR ? prolong_value<true>(cv, crv, x, y, z, C.ldy, C.ldz, 0)
-                                                  : prolong_value<false>(cv, nullptr, x, y, z, C.ldy, C.ldz, 0);
-            return fv[p] + e;
-        });
-        __syncthreads();
-        smooth(l - 1, P.post);
-    }
-    // every field back: k_coarse_cycle leaves all of them written (the host reads the iterates)
-    for (int l = 0; l < P.n; l++)
-        fields(l, false, [&](const double* g, int off) { stage(g, P.G[l], P.L[l], off, false); });
 }
 
 int launch_status()

@@ -462,6 +462,41 @@ __global__ __launch_bounds__(512) void k_march(const double* __restrict__ v, con
     }
 }
 
+// One workgroup's operator-phase floor (r06, the one-launch coarse cycle's ~1 us per phase): `phases` rounds of
+// [every thread: WORK (0: none, 1: 7 LDS reads + a dependent FP64 chain of ~14 ops, 2: the same from global memory
+// (L2-resident) with a global store) -> store -> barrier]. threads: 512 or 1024.
+template <int WORK>
+__global__ __launch_bounds__(1024) void k_phase_probe(double* __restrict__ g, int phases, double* __restrict__ sink)
+{
+    __shared__ double a[2][1024 + 64];
+    const int t = threadIdx.x;
+    a[0][t] = t * 1e-3;
+    a[1][t] = 0.0;
+    if (t < 64) a[0][1024 + t] = a[1][1024 + t] = 0.0;
+    __syncthreads();
+    double acc = 0.0;
+    for (int ph = 0; ph < phases; ph++) {
+        const int s = ph & 1;
+        double v = 0.0;
+        if (WORK == 1) {
+            const double* x = a[s] + t;
+            double q = 6.0 * x[0] - x[1] - x[2] - x[3] - x[5] - x[9] - x[17];
+            q = q * 0.37 + 1e-3;
+            v = x[0] + 0.8 * (0.1 * (x[0] * 0.5 - q));
+        } else if (WORK == 2) {
+            const double* x = g + (s ? 4096 : 0) + t;
+            double q = 6.0 * x[0] - x[1] - x[2] - x[3] - x[5] - x[9] - x[17];
+            q = q * 0.37 + 1e-3;
+            v = x[0] + 0.8 * (0.1 * (x[0] * 0.5 - q));
+            g[(s ? 0 : 4096) + t] = v;
+        }
+        a[s ^ 1][t] = v;
+        acc += v;
+        __syncthreads();
+    }
+    if (acc == -1.2345e300) *sink = acc;
+}
+
 // A copy with the resource footprint of RCCL's gfx950 transport kernels (ncclDevKernel_Generic: 256
 // VGPRs, 37664 B of LDS per 256-thread workgroup): the clobber of v255 makes the allocator reserve
 // every VGPR. Stands in for the ghost exchange in tools/exchange_probe.py (when does a workgroup
@@ -798,6 +833,15 @@ int gs_debug_march(int pfd, int bar, int nts, int ntf, int zc, const gs_level* L
     const dim3 g((unsigned)(L->ny / 4), (unsigned)((L->nz + zc - 1) / zc)), b(WAVE, 4, 2);
     hipLaunchKernelGGL(tab[pfd - 1][bar != 0][nts != 0][ntf != 0], g, b, 0, st, v, f, out, (int)L->nx, (int)L->ny,
                        (int)L->nz, L->ldy, L->ldz, zc, nullptr);
+    return launch_status();
+}
+
+int gs_debug_phase_probe(int work, int threads, int phases, double* g, double* sink, hipStream_t st)
+{
+    if ((threads != 512 && threads != 1024) || phases < 0 || work < 0 || work > 2 || !g || !sink) return GS_EINVAL;
+    if (work == 0) hipLaunchKernelGGL(k_phase_probe<0>, dim3(1), dim3(threads), 0, st, g, phases, sink);
+    else if (work == 1) hipLaunchKernelGGL(k_phase_probe<1>, dim3(1), dim3(threads), 0, st, g, phases, sink);
+    else hipLaunchKernelGGL(k_phase_probe<2>, dim3(1), dim3(threads), 0, st, g, phases, sink);
     return launch_status();
 }
 

@@ -719,54 +719,6 @@ int gs_coarse_cycle(const gs_stencil* S, const gs_coarse_level* lv, int n, int m
         L.vz = a.v_zero != 0;
         L.k = make_coef(S, g, omega, gamma);
     }
-    // the LDS form (k_coarse_cycle_lds) where every level has at most CCL_T points and all fields fit the LDS
-    // budget; GS_CC_LDS=0 keeps the L2 form (A/B)
-    if (kKnobs.ccLds) {
-        CclPlan Q{};
-        Q.n = n;
-        Q.pre = pre;
-        Q.post = post;
-        int total = 0;
-        bool fits = true;
-        for (int l = 0; l < n && fits; l++) {
-            const CcLevel& G = P.L[l];
-            CclLevel& L = Q.L[l];
-            Q.G[l] = CclGlobal{G.v, G.va, G.f, G.r, G.rv, G.w, G.ldy, G.ldz};
-            L.nx = G.nx;
-            L.ny = G.ny;
-            L.nz = G.nz;
-            L.vz = G.vz;
-            L.ldy = G.nx + 2;
-            L.ldz = (G.nx + 2) * (G.ny + 2);
-            L.n = L.ldz * (G.nz + 2);
-            fits = (int64_t)G.nx * G.ny * G.nz <= CCL_T;
-            auto take = [&](const double* g) {
-                if (!g) return -1;
-                const int o = total;
-                total += L.n;
-                return o;
-            };
-            L.v = take(G.v);
-            L.va = take(G.va);
-            L.f = take(G.f);
-            L.r = l + 1 < n ? take(G.r) : -1;
-            L.rv = mode == GS_NONLINEAR && l > 0 ? take(G.rv) : -1;
-            L.w = newtonish(mode) ? take(G.w) : -1;
-            const gs_level lg{G.nx, G.ny, G.nz, L.ldy, L.ldz, 0, lv[l].geom.h};
-            L.k = make_coef(S, &lg, omega, gamma);
-        }
-        Q.total = total;
-        if (fits && total <= CCL_LDS_DOUBLES) {
-            const size_t bytes = sizeof(double) * (size_t)total;
-            if (mode == GS_LINEAR) hipLaunchKernelGGL(k_coarse_cycle_lds<GS_LINEAR>, dim3(1), dim3(CCL_T), bytes, st, Q);
-            else if (mode == GS_NONLINEAR)
-                hipLaunchKernelGGL(k_coarse_cycle_lds<GS_NONLINEAR>, dim3(1), dim3(CCL_T), bytes, st, Q);
-            else if (mode == GS_NEWTON_B)
-                hipLaunchKernelGGL(k_coarse_cycle_lds<GS_NEWTON_B>, dim3(1), dim3(CCL_T), bytes, st, Q);
-            else hipLaunchKernelGGL(k_coarse_cycle_lds<GS_NEWTON>, dim3(1), dim3(CCL_T), bytes, st, Q);
-            return launch_status();
-        }
-    }
     if (mode == GS_LINEAR) hipLaunchKernelGGL(k_coarse_cycle<GS_LINEAR>, dim3(1), dim3(CC_T), 0, st, P);
     else if (mode == GS_NONLINEAR) hipLaunchKernelGGL(k_coarse_cycle<GS_NONLINEAR>, dim3(1), dim3(CC_T), 0, st, P);
     else if (mode == GS_NEWTON_B) hipLaunchKernelGGL(k_coarse_cycle<GS_NEWTON_B>, dim3(1), dim3(CC_T), 0, st, P);

@@ -188,6 +188,7 @@ DIAG_API = {
     "gs_debug_pair_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
                                         C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "gs_debug_stream_triad": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p]),
+    "gs_debug_phase_probe": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_debug_march": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(gs_level), C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.c_void_p]),
     "gs_debug_bw": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p,

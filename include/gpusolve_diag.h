@@ -69,6 +69,10 @@ int gs_debug_bw(int kind, int unroll, int nt, int blocks, double* out, const dou
  * slowest (a relaxed agent-scope counter in out's plane -1, bounded spins; at most 256 blocks), pfd 2, nt stores;
  * ntf 6 / 7: 1 / 4 rows per wave (2- / 8-row tiles; pfd 2 / 1), barrier, nt stores). Levels of nx <= 512 points,
  * ny a multiple of 4. 24 B per point. */
+/* One workgroup of `threads` (512 / 1024) running `phases` rounds of [work -> store -> barrier]; work 0: none, 1: a
+ * 7-point LDS stencil and a dependent FP64 chain, 2: the same from global memory g (>= 8192 doubles) with a global
+ * store. The per-phase floor of the one-launch coarse cycle. */
+int gs_debug_phase_probe(int work, int threads, int phases, double* g, double* sink, hipStream_t stream);
 int gs_debug_march(int pfd, int bar, int nts, int ntf, int zc, const gs_level* L, const double* v, const double* f,
                    double* out, hipStream_t stream);
 

@@ -20,11 +20,11 @@ SWITCHES = ["GS_COARSE_POINTS", "GS_NEWTON_PRO_POINTS", "GS_RR_NR", "GS_RR_LDS",
             "GS_NO_PIPELINE", "GS_NO_NEWTON_FUSED_UPDATE", "GS_RR_NTU", "GS_PAIR_ONE_ROUND", "GS_SLAB_ZC", "GS_PAIR_ZC",
             "GS_RR_REVERSE", "GS_HALO_ORDER", "GS_NO_ZERO_Q", "GS_XH_SWIZZLE",
             "GS_MID_ZC", "GS_RR_ZC", "GS_NEWTON_XH", "GS_SPEC_CACHED", "GS_RR_ZC_BIG", "GS_PAIR_ONE_ROUND_MID", "GS_RB_ZC", "GS_RR_NG", "GS_NEWTON_B_FUSED",
-            "GS_NO_NEWTON_G", "GS_RR_DMA", "GS_CC_LDS"]
+            "GS_NO_NEWTON_G", "GS_RR_DMA"]
 
 # (case, solve args) -> the switches whose paths that problem exercises
 CASES = {
-    "linear256": ((0, 256, 256, 256, 3), [("GS_CC_LDS", "0"), ("GS_RR_NTU", "1"), ("GS_NO_FUSED_SWEEPS", "1"), ("GS_NO_FUSED_RR", "1"),
+    "linear256": ((0, 256, 256, 256, 3), [("GS_RR_NTU", "1"), ("GS_NO_FUSED_SWEEPS", "1"), ("GS_NO_FUSED_RR", "1"),
                                           ("GS_NO_FUSED_PROLONG", "1"), ("GS_NO_SPECULATION", "1"),
                                           ("GS_NO_ZERO_GUESS", "1"), ("GS_NO_PIPELINE", "1"), ("GS_RR_LDS", "1"),
                                           ("GS_RR_NR", "2"), ("GS_NO_UNIT_STENCIL", "1"),
@@ -39,7 +39,7 @@ CASES = {
     "linear_rows700": ((0, 700, 64, 64, 3), [("GS_PAIR_XH", "0"), ("GS_TBX_PFD", "1"), ("GS_XH_SWIZZLE", "0")]),
     # two loopback slabs of 512^3: the interior launches of the overlapped sweeps (z0 != 0)
     "slabs512": ((0, 512, 512, 1024, 2, 2, 2, 2), [("GS_SLAB_ZC", "16"), ("GS_HALO_ORDER", "1")]),
-    "newton127": ((2, 127, 127, 127, 2), [("GS_CC_LDS", "0"), ("GS_NEWTON_PRO_POINTS", "0"), ("GS_NO_FUSED_PROLONG", "1"),
+    "newton127": ((2, 127, 127, 127, 2), [("GS_NEWTON_PRO_POINTS", "0"), ("GS_NO_FUSED_PROLONG", "1"),
                                           ("GS_NO_PIPELINE", "1"), ("GS_NO_NEWTON_FUSED_UPDATE", "1"),
                                           ("GS_RR_REVERSE", "0"), ("GS_NO_ZERO_Q", "1")]),
     # two loopback slabs in NEWTON mode: GS_NEWTON_G's pairs on slab plane ranges (ghost planes of the factor)
