@@ -2390,9 +2390,10 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
 // expression, so every output is bit-identical to two gs_jacobi_sweep calls.
 // TS (diagnostics only, gs_debug_pair_timestamps): es is a buffer of 4 doubles per tile that receives the
 // block's start and end wall clock (100 MHz), its hardware block index and its HW_ID register
+// WPE: waves per SIMD the register allocation must allow (0: the default, one; 4: <= 128 VGPRs, two 8-wave blocks per CU)
 template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0,
-          int PFD = 1, bool XH = false, bool UN = false, bool TS = false>
-__global__ __launch_bounds__(WAVE* WXMAX * 2) void k_tb2y(Coef k, const double* __restrict__ v,
+          int PFD = 1, bool XH = false, bool UN = false, bool TS = false, int WPE = 0>
+__global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coef k, const double* __restrict__ v,
                                                            const double* __restrict__ f, const double* __restrict__ w,
                                                            double* __restrict__ out, double* __restrict__ partials,
                                                            int nx, int ny, int nz, int64_t ldy, int64_t ldz, int ZC,

@@ -742,6 +742,36 @@ int gs_debug_pair_reverse(const gs_stencil* S, const gs_level* L, double omega, 
     return launch_status();
 }
 
+// The LINEAR pair (k_tb2y, whole 512-point rows) in other row / prefetch / occupancy shapes (r06, verdict r05 item 2):
+// ry output rows per y-wave (1 or 2), pfd plane steps of prefetch, wpe waves per SIMD the allocation must allow
+// (0: one, the production build; 4: <= 128 VGPRs, so two 8-wave blocks share a CU), zc planes per chunk. Same
+// expressions per point as the production pair, so the output is bit-identical to gs_jacobi_sweep2's.
+int gs_debug_pair_shape(const gs_stencil* S, const gs_level* L, double omega, const double* v_in, double* v_out,
+                        const double* f, int ry, int pfd, int wpe, int zc, hipStream_t st)
+{
+    if (!S || bad_level(L) || !valid_stencil(S) || !canonical_order(S) || !v_in || !v_out || !f || v_in == v_out ||
+        zc < 2 || (zc & 1) || L->nx > 2 * WAVE * TBY_WX || (ry != 1 && ry != 2) || (pfd != 1 && pfd != 2) ||
+        (wpe != 0 && wpe != 3 && wpe != 4))
+        return GS_EINVAL;
+    const Coef k = make_coef(S, L, omega, 0.0);
+    const dim3 g((unsigned)((L->ny + 2 * ry - 1) / (2 * ry)), (unsigned)((L->nz + zc - 1) / zc)),
+        b(WAVE, (unsigned)((L->nx + 2 * WAVE - 1) / (2 * WAVE)), 2);
+    using K = void (*)(Coef, const double*, const double*, const double*, double*, double*, int, int, int, int64_t,
+                       int64_t, int, int, int, const double*, const double*, int, int, int, int64_t, int64_t,
+                       const double*);
+#define GS_PSH(RY, P, W) k_tb2y<GS_LINEAR, RY, TBY_WX, true, false, false, true, 0, P, false, true, false, W>
+    static const K tab[2][2][3] = {{{GS_PSH(1, 1, 0), GS_PSH(1, 1, 3), GS_PSH(1, 1, 4)},
+                                    {GS_PSH(1, 2, 0), GS_PSH(1, 2, 3), GS_PSH(1, 2, 4)}},
+                                   {{GS_PSH(2, 1, 0), GS_PSH(2, 1, 3), GS_PSH(2, 1, 4)},
+                                    {GS_PSH(2, 2, 0), GS_PSH(2, 2, 3), GS_PSH(2, 2, 4)}}};
+#undef GS_PSH
+    if (!k.unit) return GS_EINVAL; // (the unit-stencil sums only: every reference config)
+    hipLaunchKernelGGL(tab[ry - 1][pfd - 1][wpe == 0 ? 0 : (wpe == 3 ? 1 : 2)], g, b, 0, st, k, v_in, f, nullptr, v_out,
+                       nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, 0, 0, nullptr, nullptr, 0, 0,
+                       0, (int64_t)0, (int64_t)0, nullptr);
+    return launch_status();
+}
+
 int64_t gs_debug_pair_blocks(const gs_stencil* S, const gs_level* L, int zc)
 {
     int zcp;

@@ -185,6 +185,8 @@ DIAG_API = {
     "gs_debug_pair_reverse": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
                                         C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "gs_debug_pair_blocks": (i64, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_int]),
+    "gs_debug_pair_shape": (C.c_int, [C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "gs_debug_pair_variant": (C.c_int, [C.c_int, C.POINTER(gs_stencil), C.POINTER(gs_level), C.c_double, C.c_void_p,
                                         C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "gs_debug_stream_triad": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, i64, C.c_void_p]),

@@ -82,6 +82,12 @@ int gs_debug_pair_timestamps(const gs_stencil* S, const gs_level* L, double omeg
                              const double* f, int zc, double* ts, hipStream_t stream);
 int64_t gs_debug_pair_blocks(const gs_stencil* S, const gs_level* L, int zc);
 
+/* The LINEAR pair (k_tb2y, rows of <= 512 points, unit stencils) in another shape: ry output rows per y-wave (1, 2),
+ * pfd plane steps of prefetch (1, 2), wpe waves per SIMD the register allocation allows (0: one, as the product; 3;
+ * 4: two 8-wave blocks per CU), zc planes per chunk (even). Output bit-identical to gs_jacobi_sweep2's. */
+int gs_debug_pair_shape(const gs_stencil* S, const gs_level* L, double omega, const double* v_in, double* v_out,
+                        const double* f, int ry, int pfd, int wpe, int zc, hipStream_t stream);
+
 /* Timing only: the production LINEAR pair with the planes marched in descending order (reverse != 0; the
  * z-terms enter the sum swapped, so the values are not the sweep's). */
 int gs_debug_pair_reverse(const gs_stencil* S, const gs_level* L, double omega, const double* v_in, double* v_out,

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default="")
+    ap.add_argument("--variants", default="", help="pfd,bar,nts,ntf,zc;... (default: the r06e set)")
     a = ap.parse_args()
     n = a.n
     k, kd = gsv.kernels(), gsv.diag()
@@ -53,6 +54,8 @@ def main():
                                                                 sink.data_ptr(), st.cuda_stream)}
     variants = [(2, 1, 1, 0, zc) for zc in (256, 128)] + \
                [(2, 1, 1, 6, zc) for zc in (512, 256, 128)] + [(1, 1, 1, 7, zc) for zc in (256, 128, 64)]
+    if a.variants:
+        variants = [tuple(int(x) for x in v.split(",")) for v in a.variants.split(";")]
     for pfd, bar, nts, ntf, zc in variants:
         tag = {0: "", 1: " nt-f", 2: " LEAN", 3: " sync2", 4: " sync4", 5: " sync8", 6: " RY1", 7: " RY4"}[ntf]
         name = f"march pfd{pfd} bar{bar} {'nt' if nts else 'plain'}-st zc{zc}{tag}"
