@@ -777,8 +777,11 @@ static bool proSlabOk(HipGridData& grid, std::size_t l)
 // 512^3's level 1 and 256^3's level 0 too (Newton iteration 36.5-36.6 against 36.7-36.75 ms at 512^3,
 // 6.32-6.36 against 6.58-6.62 ms at 256^3: profiles/r04/r04e_newton_ab_swizzle_rrreverse.txt,
 // r04f_newton_pro_threshold.txt),
-// so NEWTON levels take it from GS_NEWTON_PRO_POINTS (default 2^24) points per rank on (judged on the
-// thinnest slab: rank-uniform). LINEAR levels always do.
+// so NEWTON levels take it from GS_NEWTON_PRO_POINTS points per rank on (judged on the thinnest slab: rank-uniform).
+// Since r06 the default is 2^21, so 512^3's 128^3 level fuses too: its two-x-wave GS_NEWTON_B prolongation pair
+// (34.7 us) replaces gs_prolong_add (39 us) + the plain pair (22 us), one launch fewer per inner V-cycle; a Newton
+// iteration's kernel time 29.09 vs 29.22 ms, wall 27.63-27.80 vs 27.69-27.84 ms (3 interleaved rounds,
+// profiles/r06/r06p_newton_pro_points_ab.txt). LINEAR levels always do.
 static bool proWorthIt(HipGridData& grid, std::size_t l)
 {
     if (grid.mode != GridParams::NEWTON) return true;

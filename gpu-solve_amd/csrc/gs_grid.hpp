@@ -159,8 +159,9 @@ public:
                              // gamma) instead of taking gamma in the pairs and k_rr2 (GS_NEWTON_G; bit-identical)
         int64_t tilePoints = (int64_t)1 << 18; // GS_TILE_POINTS: levels of at most this many points (replicated,
                                                // LINEAR) run the tiled one-launch down/up-leg steps; 0 = off
-        int64_t newtonProPoints = (int64_t)1 << 24; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
-                                                     // prolongation pair from this many points per rank
+        int64_t newtonProPoints = (int64_t)1 << 21; // GS_NEWTON_PRO_POINTS: NEWTON levels take the fused
+                                                     // prolongation pair from this many points per rank (r06: 2^21,
+                                                     // 128^3 too, was 2^24)
         // GS_HALO_ORDER: in a pipelined Z-slab sweep sequence, interior k goes before boundary k when
         // exchange k-1 has not settled on the host yet (0, adaptive), always (1), or never (2: boundary first)
         int haloOrder = 0;

@@ -1,5 +1,5 @@
 """NEWTON's fused prolongation pair inside whole solves. The driver takes it only on levels of at
-least GS_NEWTON_PRO_POINTS points (default 2^24: below that gs_prolong_add + the plain pair is
+least GS_NEWTON_PRO_POINTS points (default 2^21 since r06, 2^24 before: below that gs_prolong_add + the plain pair is
 faster); forcing it on every level (0) must leave every field and every residual bit-identical to
 the unfused sequence (a threshold no level reaches), on one GPU and on Z-slabs. The unfused
 sequence is itself pinned to the reference (test_gpu_solver.py: src/cpu/NewtonSolver.cpp)."""
