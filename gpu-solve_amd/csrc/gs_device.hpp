@@ -2565,18 +2565,31 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coe
     };
     // field fl of this lane's edge row from packed slot s (a lane permute; every lane of the wave active)
     auto efld = [&](const int s, const int fl) { return __shfl(EPS[s], fl * 8 + (lane & 7), WAVE); };
+    // GRP (LINEAR plain pairs, r06): a step's loads grouped by field and plane, rows ascending — v's halo row and rows
+    // 0..RY, then f's rows — instead of row by row alternating between the two streams: pair 0.5831-0.5998 vs
+    // 0.5935-0.6013 ms per 512^3 launch, 5 of 6 interleaved rounds faster (profiles/r06/r06v_pair_load_order_ab.txt,
+    // r06u); the NEWTON pairs and every prolongation pair measured slower with it (r06u / r06v) and keep the row order
+    constexpr bool GRP = MODE == GS_LINEAR && PRO == 0;
     auto load_slot = [&](const int s, const int z, const int zv) {
+        if constexpr (GRP) {
+            HL[s] = ldv2<ZV>(at(v, -1, z));
 #pragma unroll
-        for (int j = 0; j < NV; j++) {
-            VL[s][j] = ldv2<ZV>(at(v, j, zv));
-            FL[s][j] = ld2s<NTF>(at(f, j, z));
-            if (MODE == GS_NEWTON_B && k.bconst) WL[s][j] = make_double2(k.gamma, k.gamma);
-            else if (newtonish(MODE)) WL[s][j] = ld2(at(w, j, z));
+            for (int j = 0; j < NV; j++) VL[s][j] = ldv2<ZV>(at(v, j, zv));
+#pragma unroll
+            for (int j = 0; j < NV; j++) FL[s][j] = ld2s<NTF>(at(f, j, z));
+        } else {
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                VL[s][j] = ldv2<ZV>(at(v, j, zv));
+                FL[s][j] = ld2s<NTF>(at(f, j, z));
+                if (MODE == GS_NEWTON_B && k.bconst) WL[s][j] = make_double2(k.gamma, k.gamma);
+                else if (newtonish(MODE)) WL[s][j] = ld2(at(w, j, z));
 #ifdef GS_EXP_EFIELD
-            if (MODE == GS_NEWTON) XL[s][j] = ld2(at(w, j, z) + k.efoff);
+                if (MODE == GS_NEWTON) XL[s][j] = ld2(at(w, j, z) + k.efoff);
 #endif
+            }
+            HL[s] = ldv2<ZV>(at(v, -1, z));
         }
-        HL[s] = ldv2<ZV>(at(v, -1, z));
         if constexpr (XH && !EPK) {
             if (edg) load_edge(s, z, zv);
         }
