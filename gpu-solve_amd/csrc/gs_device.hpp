@@ -1180,6 +1180,14 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
     double2 VA[2][RR], VB[2][RR], H0[2][2], H1[2][2], F0[2][RR], F1[2][RR], W0[2][RR], W1[2][RR];
     auto load_slot = [&](const int s, const int Z) {
         const int p = 2 * Z;
+        // the step's halo rows first (the rows the y-neighbour blocks read too), then row by row: k_rr2 0.442-0.443 vs
+        // 0.458-0.459 ms LINEAR, 0.7085-0.7088 vs 0.7254-0.7259 ms NEWTON_B per 512^3 launch (r06x / r06y,
+        // interleaved, profiles/r06/r06x_load_order_ab.txt; f rows first: 0.449 / 0.726-0.740, plane by plane: 0.484-0.485 /
+        // 0.754-0.760, v / f / w grouped: 0.481-0.485 / 0.747-0.750, halos then v then f / w: 0.476-0.478 / 0.751)
+        H0[s][0] = ld2(at(v, 0, p));
+        H0[s][1] = ld2(at(v, RR + 1, p));
+        H1[s][0] = ld2(at(v, 0, p + 1));
+        H1[s][1] = ld2(at(v, RR + 1, p + 1));
 #pragma unroll
         for (int j = 0; j < RR; j++) {
             // NTU: rows no neighbouring block reads (v: 2Y+1 .. 2Y+2NR-3, f: 2Y .. 2Y+2NR-2) bypass L2
@@ -1197,10 +1205,6 @@ __global__ __launch_bounds__(WAVE* RR2_WXMAX) void k_rr2(Coef k, const double* _
                 W1[s][j] = uf ? ld2s<true>(at(w, j + 1, p + 1)) : ld2(at(w, j + 1, p + 1));
             }
         }
-        H0[s][0] = ld2(at(v, 0, p));
-        H0[s][1] = ld2(at(v, RR + 1, p));
-        H1[s][0] = ld2(at(v, 0, p + 1));
-        H1[s][1] = ld2(at(v, RR + 1, p + 1));
     };
     // LDS-only barrier: the outstanding prefetch stays in flight across it
     auto lds_barrier = [] { GS_LDS_BARRIER(); }; // lgkmcnt(0), s_barrier
@@ -2578,6 +2582,37 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coe
 #pragma unroll
             for (int j = 0; j < NV; j++) FL[s][j] = ld2s<NTF>(at(f, j, z));
         } else {
+#if defined(GS_EXP_ORD) // (timing A/B, r06: other load orders for the prolongation / NEWTON pairs)
+            auto ldw = [&](int j) {
+                if (MODE == GS_NEWTON_B && k.bconst) WL[s][j] = make_double2(k.gamma, k.gamma);
+                else if (newtonish(MODE)) WL[s][j] = ld2(at(w, j, z));
+            };
+            if (GS_EXP_ORD == 1) { // f (and w) rows, the halo row, v rows
+#pragma unroll
+                for (int j = 0; j < NV; j++) FL[s][j] = ld2s<NTF>(at(f, j, z));
+#pragma unroll
+                for (int j = 0; j < NV; j++) ldw(j);
+                HL[s] = ldv2<ZV>(at(v, -1, z));
+#pragma unroll
+                for (int j = 0; j < NV; j++) VL[s][j] = ldv2<ZV>(at(v, j, zv));
+            } else if (GS_EXP_ORD == 2) { // w rows, v rows, f rows, the halo row
+#pragma unroll
+                for (int j = 0; j < NV; j++) ldw(j);
+#pragma unroll
+                for (int j = 0; j < NV; j++) VL[s][j] = ldv2<ZV>(at(v, j, zv));
+#pragma unroll
+                for (int j = 0; j < NV; j++) FL[s][j] = ld2s<NTF>(at(f, j, z));
+                HL[s] = ldv2<ZV>(at(v, -1, z));
+            } else { // the halo row first, then row by row
+                HL[s] = ldv2<ZV>(at(v, -1, z));
+#pragma unroll
+                for (int j = 0; j < NV; j++) {
+                    VL[s][j] = ldv2<ZV>(at(v, j, zv));
+                    FL[s][j] = ld2s<NTF>(at(f, j, z));
+                    ldw(j);
+                }
+            }
+#else
 #pragma unroll
             for (int j = 0; j < NV; j++) {
                 VL[s][j] = ldv2<ZV>(at(v, j, zv));
@@ -2589,6 +2624,7 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coe
 #endif
             }
             HL[s] = ldv2<ZV>(at(v, -1, z));
+#endif
         }
         if constexpr (XH && !EPK) {
             if (edg) load_edge(s, z, zv);
