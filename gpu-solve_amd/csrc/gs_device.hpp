@@ -2582,37 +2582,6 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coe
 #pragma unroll
             for (int j = 0; j < NV; j++) FL[s][j] = ld2s<NTF>(at(f, j, z));
         } else {
-#if defined(GS_EXP_ORD) // (timing A/B, r06: other load orders for the prolongation / NEWTON pairs)
-            auto ldw = [&](int j) {
-                if (MODE == GS_NEWTON_B && k.bconst) WL[s][j] = make_double2(k.gamma, k.gamma);
-                else if (newtonish(MODE)) WL[s][j] = ld2(at(w, j, z));
-            };
-            if (GS_EXP_ORD == 1) { // f (and w) rows, the halo row, v rows
-#pragma unroll
-                for (int j = 0; j < NV; j++) FL[s][j] = ld2s<NTF>(at(f, j, z));
-#pragma unroll
-                for (int j = 0; j < NV; j++) ldw(j);
-                HL[s] = ldv2<ZV>(at(v, -1, z));
-#pragma unroll
-                for (int j = 0; j < NV; j++) VL[s][j] = ldv2<ZV>(at(v, j, zv));
-            } else if (GS_EXP_ORD == 2) { // w rows, v rows, f rows, the halo row
-#pragma unroll
-                for (int j = 0; j < NV; j++) ldw(j);
-#pragma unroll
-                for (int j = 0; j < NV; j++) VL[s][j] = ldv2<ZV>(at(v, j, zv));
-#pragma unroll
-                for (int j = 0; j < NV; j++) FL[s][j] = ld2s<NTF>(at(f, j, z));
-                HL[s] = ldv2<ZV>(at(v, -1, z));
-            } else { // the halo row first, then row by row
-                HL[s] = ldv2<ZV>(at(v, -1, z));
-#pragma unroll
-                for (int j = 0; j < NV; j++) {
-                    VL[s][j] = ldv2<ZV>(at(v, j, zv));
-                    FL[s][j] = ld2s<NTF>(at(f, j, z));
-                    ldw(j);
-                }
-            }
-#else
 #pragma unroll
             for (int j = 0; j < NV; j++) {
                 VL[s][j] = ldv2<ZV>(at(v, j, zv));
@@ -2624,7 +2593,6 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coe
 #endif
             }
             HL[s] = ldv2<ZV>(at(v, -1, z));
-#endif
         }
         if constexpr (XH && !EPK) {
             if (edg) load_edge(s, z, zv);
