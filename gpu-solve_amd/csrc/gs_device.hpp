@@ -135,10 +135,12 @@ bool valid_stencil(const gs_stencil* S)
 //   GS_NEWTON_XH=0       NEWTON plain pairs on rows of 513-1024 points through k_tb2 instead of column blocks (A/B)
 //   GS_SPEC_CACHED=1     pairs with norm partials store through the caches, not non-temporally (A/B)
 //   GS_RR_NG=2           k_rr2 with two groups of coarse rows per block (default 1: measured faster, r05b)
+//   GS_PAIR_FX=0         LINEAR plain pairs always through the instance with per-lane range selects (A/B, r06)
 struct Knobs {
     bool unitStencil, tbxPfd2, pairXh, fitRounds, bigChunks, oneRound, rrLds, zeroQ, newtonXh, specCached;
     int xhSwizzle, midZc, rrZc, rrZcBig, oneRoundMid, rbZc;
     int slabZc, pairZc, rrNr, rrNtu, rrReverse, rrNg, rrDma;
+    bool pairFx;
     int64_t pairMinBlocks;
     static int num(const char* name, int dflt)
     {
@@ -153,6 +155,7 @@ struct Knobs {
           newtonXh(num("GS_NEWTON_XH", 1) != 0), specCached(num("GS_SPEC_CACHED", 0) != 0),
           xhSwizzle(num("GS_XH_SWIZZLE", 1)), midZc(num("GS_MID_ZC", 0)), rrZc(num("GS_RR_ZC", 0)), rrZcBig(num("GS_RR_ZC_BIG", 0)), oneRoundMid(num("GS_PAIR_ONE_ROUND_MID", 0)), rbZc(num("GS_RB_ZC", 0)), slabZc(num("GS_SLAB_ZC", 0)), pairZc(num("GS_PAIR_ZC", 0)),
           rrNr(num("GS_RR_NR", 0)), rrNtu(num("GS_RR_NTU", 2)), rrReverse(num("GS_RR_REVERSE", 1)), rrNg(num("GS_RR_NG", 0)), rrDma(num("GS_RR_DMA", 0)),
+          pairFx(num("GS_PAIR_FX", 1) != 0),
           pairMinBlocks(num("GS_PAIR_MIN_BLOCKS", 128))
     {
     }
@@ -2395,8 +2398,11 @@ __global__ __launch_bounds__(WAVE* WXMAX) void k_tb2(Coef k, const double* __res
 // TS (diagnostics only, gs_debug_pair_timestamps): es is a buffer of 4 doubles per tile that receives the
 // block's start and end wall clock (100 MHz), its hardware block index and its HW_ID register
 // WPE: waves per SIMD the register allocation must allow (0: the default, one; 4: <= 128 VGPRs, two 8-wave blocks per CU)
+// FX (r06): every lane's two points lie inside the row (the host launches it where nx is a whole number of 128-point
+// waves, 512-point column blocks for XH): the per-lane range selects of the new values, the norm partials and the stores
+// fold away — the same values from fewer VALU instructions per step
 template <int MODE, int RY, int WXMAX, bool NT, bool NTF = false, bool ZV = false, bool SPEC = false, int PRO = 0,
-          int PFD = 1, bool XH = false, bool UN = false, bool TS = false, int WPE = 0>
+          int PFD = 1, bool XH = false, bool UN = false, bool TS = false, int WPE = 0, bool FX = false>
 __global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coef k, const double* __restrict__ v,
                                                            const double* __restrict__ f, const double* __restrict__ w,
                                                            double* __restrict__ out, double* __restrict__ partials,
@@ -2439,8 +2445,8 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coe
     const int x0 = xb + wx * (2 * WAVE);
     const int x = x0 + 2 * lane;
     const int xl = min(x, nx + 1);
-    const bool bx0 = x > nx, bx1 = x + 1 > nx;
-    const bool okx0 = x <= nx, okx1 = x + 1 <= nx;
+    const bool bx0 = !FX && x > nx, bx1 = !FX && x + 1 > nx;
+    const bool okx0 = FX || x <= nx, okx1 = FX || x + 1 <= nx;
     const int y0 = 1 + (int)((tile % gridDim.x) / nh) * (2 * RY);
     const int zb = 1 + (int)(tile / gridDim.x) * ZC;
     const int ze = min(zb + ZC - 1, nz);

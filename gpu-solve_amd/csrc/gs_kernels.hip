@@ -128,7 +128,27 @@ int gs_jacobi_sweep2_norm(const gs_stencil* S, const gs_level* L, int mode, doub
 #define GS_TBX1(M, Z, P, U) hipLaunchKernelGGL((k_tb2y<M, TBY_RY, TBY_WX, true, false, Z, true, 0, P, true, U>), g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr)
 #define GS_TBX(M, Z, P) do { if (k.unit) GS_TBX1(M, Z, P, true); else GS_TBX1(M, Z, P, false); } while (0)
     const bool zv = !v_in;
-    if (xh) {
+    // FX (r06): LINEAR plain pairs over rows of whole 128-point waves (512-point column blocks) take the instance
+    // without per-lane range selects (k_tb2y FX; GS_PAIR_FX=0: the general instance, A/B)
+    if (mode == GS_LINEAR && !zv && k.unit && kKnobs.pairFx &&
+        ((xh && tbx_pfd2() && nx % (2 * WAVE * TBY_WX) == 0) || (y2 && nx % (2 * WAVE) == 0))) {
+        if (xh)
+            hipLaunchKernelGGL((k_tb2y<GS_LINEAR, TBY_RY, TBY_WX, true, false, false, true, 0, 2, true, true, false, 0, true>),
+                               g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0,
+                               zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr);
+        else if (cached)
+            hipLaunchKernelGGL((k_tb2y<GS_LINEAR, TBY_RY, TBY_WX, false, false, false, true, 0, 2, false, true, false, 0, true>),
+                               g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0,
+                               zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr);
+        else
+            hipLaunchKernelGGL((k_tb2y<GS_LINEAR, TBY_RY, TBY_WX, true, false, false, true, 0, 2, false, true, false, 0, true>),
+                               g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0,
+                               zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr);
+    } else if (mode == GS_NEWTON_B && !zv && y2 && !cached && k.unit && kKnobs.pairFx && nx % (2 * WAVE) == 0) {
+        hipLaunchKernelGGL((k_tb2y<GS_NEWTON_B, TBY_RY_NEWTON, TBY_WX, true, false, false, true, 0, 1, false, true, false, 0, true>),
+                           g, b, 0, st, k, v_in, f, w, v_out, partials, nx, ny, nz, L->ldy, L->ldz, zc, zlo ? 1 : 0,
+                           zhi ? 1 : 0, nullptr, nullptr, 0, 0, 0, 0, 0, nullptr);
+    } else if (xh) {
         if (mode == GS_LINEAR) {
             if (zv) GS_TBX(GS_LINEAR, true, 1);
             else if (tbx_pfd2()) GS_TBX(GS_LINEAR, false, 2);
@@ -229,7 +249,17 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
                            dim3(256), 0, st, v_in, coarse_v, nullptr, ws, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy,
                            L->ldz, cl->ldy, cl->ldz, bw, zlo ? 1 : 0, zhi ? 1 : 0);
     }
-#define GS_TBP1(M, P, U, X, WM) hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, 1, X, U>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
+#define GS_TBPF(M, P, U, X, WM, FXV) hipLaunchKernelGGL((k_tb2y<M, newtonish(M) ? TBY_RY_NEWTON : TBY_RY, WM, true, false, false, true, P, 1, X, U, false, 0, FXV>), g, b, 0, st, k, v_in, f, w, v_out, nullptr, (int)L->nx, (int)L->ny, (int)L->nz, L->ldy, L->ldz, zc, zlo ? 1 : 0, zhi ? 1 : 0, coarse_v, coarse_sub, (int)cl->nx, (int)cl->ny, (int)(cl->nz - czoff), cl->ldy, cl->ldz, ws)
+    // FX (r06, as the plain pairs): unit-stencil LINEAR / GS_NEWTON_B prolongation pairs of four x-waves over rows of
+    // whole 128-point waves (512-point column blocks) take the instance without per-lane range selects
+    const bool fx = k.unit && kKnobs.pairFx && b.y == TBY_WX && (xh ? L->nx % (2 * WAVE * TBY_WX) == 0 : L->nx % (2 * WAVE) == 0);
+#define GS_TBP1(M, P, U, X, WM) do { \
+        if constexpr (U && WM == TBY_WX && (M == GS_LINEAR || M == GS_NEWTON_B)) { \
+            if (fx) GS_TBPF(M, P, U, X, WM, true); \
+            else GS_TBPF(M, P, U, X, WM, false); \
+        } else { \
+            GS_TBPF(M, P, U, X, WM, false); \
+        } } while (0)
 #define GS_TBP(M, P, X, WM) do { if (k.unit) GS_TBP1(M, P, true, X, WM); else GS_TBP1(M, P, false, X, WM); } while (0)
     // NEWTON's variant keeps ~37 KB of state per x-wave in LDS (its RECOMP rows): rows of <= 256 points
     // (two x-waves) take the instance sized for two, so that two blocks share a CU (8 waves, the VGPR
@@ -244,6 +274,7 @@ int gs_jacobi_sweep2_prolong_ws(const gs_stencil* S, const gs_level* L, int mode
     else if (xh) GS_TBP(GS_LINEAR, 1, true, TBY_WX);
     else GS_TBP(GS_LINEAR, 1, false, TBY_WX);
 #undef GS_TBP
+#undef GS_TBPF
 #undef GS_TBP1
     return launch_status();
 }

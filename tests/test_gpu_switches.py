@@ -20,7 +20,7 @@ SWITCHES = ["GS_COARSE_POINTS", "GS_NEWTON_PRO_POINTS", "GS_RR_NR", "GS_RR_LDS",
             "GS_NO_PIPELINE", "GS_NO_NEWTON_FUSED_UPDATE", "GS_RR_NTU", "GS_PAIR_ONE_ROUND", "GS_SLAB_ZC", "GS_PAIR_ZC",
             "GS_RR_REVERSE", "GS_HALO_ORDER", "GS_NO_ZERO_Q", "GS_XH_SWIZZLE",
             "GS_MID_ZC", "GS_RR_ZC", "GS_NEWTON_XH", "GS_SPEC_CACHED", "GS_RR_ZC_BIG", "GS_PAIR_ONE_ROUND_MID", "GS_RB_ZC", "GS_RR_NG", "GS_NEWTON_B_FUSED",
-            "GS_NO_NEWTON_G", "GS_RR_DMA"]
+            "GS_NO_NEWTON_G", "GS_RR_DMA", "GS_PAIR_FX"]
 
 # (case, solve args) -> the switches whose paths that problem exercises
 CASES = {
@@ -35,7 +35,8 @@ CASES = {
     "linear2e26": ((0, 512, 512, 256, 2), [("GS_RR_NR", "1"), ("GS_PAIR_BIG_CHUNKS", "0"), ("GS_RR_NTU", "0"),
                                            ("GS_RR_ZC_BIG", "7")]),
     "linear512": ((0, 512, 512, 512, 2), [("GS_PAIR_ONE_ROUND", "0"), ("GS_PAIR_ZC", "96"), ("GS_RR_REVERSE", "0"),
-                                          ("GS_SPEC_CACHED", "1"), ("GS_RR_NG", "2"), ("GS_RR_DMA", "2")]),
+                                          ("GS_SPEC_CACHED", "1"), ("GS_RR_NG", "2"), ("GS_RR_DMA", "2"),
+                                          ("GS_PAIR_FX", "0")]),
     "linear_rows700": ((0, 700, 64, 64, 3), [("GS_PAIR_XH", "0"), ("GS_TBX_PFD", "1"), ("GS_XH_SWIZZLE", "0")]),
     # two loopback slabs of 512^3: the interior launches of the overlapped sweeps (z0 != 0)
     "slabs512": ((0, 512, 512, 1024, 2, 2, 2, 2), [("GS_SLAB_ZC", "16"), ("GS_HALO_ORDER", "1")]),
@@ -45,6 +46,8 @@ CASES = {
     # two loopback slabs in NEWTON mode: GS_NEWTON_G's pairs on slab plane ranges (ghost planes of the factor)
     "newton_slabs": ((2, 130, 66, 128, 2, 2, 2, 2), [("GS_NO_NEWTON_G", "1")]),
     "newton_rows700": ((2, 700, 12, 10, 2), [("GS_NEWTON_XH", "0"), ("GS_NO_NEWTON_G", "1")]),
+    # rows of whole 128-point waves: the NEWTON_B plain and prolongation pairs' FX instances
+    "newton256": ((2, 256, 64, 64, 2), [("GS_PAIR_FX", "0")]),
     "newton255": ((2, 255, 127, 127, 2), [("GS_RB_ZC", "10"), ("GS_RR_NG", "2"), ("GS_NEWTON_B_FUSED", "0"),
                                           ("GS_NO_NEWTON_G", "1"), ("GS_RR_DMA", "2")]),
 }
