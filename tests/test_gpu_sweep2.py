@@ -77,6 +77,36 @@ def test_sweep2_equals_two_sweeps(shape, mode):
     np.testing.assert_array_equal(out.to_xyz(), ref)
 
 
+@pytest.mark.parametrize("nx", [128, 512])
+def test_sweep2_extreme_magnitudes(nx):
+    """Whole-row LINEAR pairs test the fast h^2 division's range with floating-point compares (r06, div_hh_n FPC), the
+    single sweep with the exponent field: fields whose stencil sums straddle both ends of that range (2^-899, 2^601),
+    zeros, denormals and overflow must come out the same — bit for bit, NaNs as NaNs."""
+    rng = np.random.default_rng(nx)
+    shape = (nx, 6, 7)
+    mags = np.array([0.0, 5e-324, 1e-310, 1e-280, 1e-272, 1.3e-271, 1e-270, 1e-200, 1.0, 1e100, 1e180, 4e180, 5e180,
+                     1e200, 1e300])
+
+    def field():
+        a = rand_full(rng, *shape)
+        inner = a[1:nx + 1, 1:7, 1:8]
+        inner[...] = np.sign(inner) * rng.choice(mags, inner.shape) * rng.uniform(0.5, 2.0, inner.shape)
+        return a
+
+    h = 1.0 / 7
+    v0, f0, w0 = field(), field(), rand_full(rng, *shape)
+    with np.errstate(all="ignore"):
+        ref = two_sweeps(v0, f0, w0, 0, h)
+    v, f, w, out = (DevField(*shape).from_xyz(v0), DevField(*shape).from_xyz(f0), DevField(*shape).from_xyz(w0),
+                    DevField(*shape))
+    L = v.level(h)
+    ok(k().gs_jacobi_sweep2(C.byref(stencil()), C.byref(L), 0, 0.8, 1.0, v.ptr, out.ptr, f.ptr, w.ptr, 0, 0, st()))
+    got = out.to_xyz()
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    m = ~np.isnan(ref)
+    assert np.array_equal(got[m].view(np.int64), ref[m].view(np.int64))
+
+
 @pytest.mark.parametrize("nx", [130, 1100])
 @pytest.mark.parametrize("lo,hi", [(1, 9), (5, 14), (12, 22), (3, 3), (10, 11)])
 @pytest.mark.parametrize("mode", [0, 2])
