@@ -2774,11 +2774,14 @@ __global__ __launch_bounds__(WAVE* WXMAX * 2, WPE > 0 ? WPE : 1) void k_tb2y(Coe
             // LDS-only barrier: the outstanding prefetch stays in flight across it
             GS_LDS_BARRIER(); // lgkmcnt(0), s_barrier
             double CL[NE], CR[NE];
-            // VEDGE (LINEAR plain pairs on whole rows, r06): the edge values stay in the VGPRs the LDS broadcast read
-            // fills, and each DPP shift takes its edge as the old value in place — no readfirstlane to SGPRs and no copy
-            // back to a VGPR per shift (20 fewer VALU instructions per plane step, 230 instead of 210 VGPRs); the other
-            // pairs keep them in SGPRs (the extra VGPRs would spill or cost them a wave per SIMD)
-            constexpr bool VEDGE = MODE == GS_LINEAR && PRO == 0 && !XH;
+            // VEDGE (r06: LINEAR plain and prolongation pairs on whole rows, the GS_NEWTON_B FX plain pair): the edge
+            // values stay in the VGPRs the LDS broadcast read fills, and each DPP shift takes its edge as the old value
+            // in place — no readfirstlane to SGPRs and no copy back to a VGPR per shift (20 fewer VALU instructions per
+            // plane step, +20 VGPRs: 230 / 248 / 252, no spill). Pair 0.557-0.568 vs 0.574-0.583 ms, LINEAR prolongation
+            // pair 0.652-0.661 vs 0.665-0.674 ms, Newton iteration 27.54-27.65 vs 27.65-28.04 ms (rotated rounds,
+            // profiles/r06/r06ad_pair_vedge_ab.txt, r06ag_vedge_pro_newton_ab.txt); the other pairs keep them in SGPRs
+            // (the extra VGPRs would spill or cost them a wave per SIMD)
+            constexpr bool VEDGE = !XH && (MODE == GS_LINEAR || (MODE == GS_NEWTON_B && PRO == 0 && FX));
 #pragma unroll
             for (int i = 0; i < NE; i++) { // wave-uniform: kept in SGPRs (VEDGE: VGPRs)
                 if constexpr (VEDGE) {
