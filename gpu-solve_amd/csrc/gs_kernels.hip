@@ -766,10 +766,12 @@ const char* gs_strerror(int code)
 
 const char* gs_build_info(void)
 {
-    return "gpusolve_hip v12: pairs k_tb2y(4x2 waves, 2 rows/wave, one round of z-chunks on large levels, LINEAR 2-step prefetch; +prolong; "
+    return "gpusolve_hip v13: pairs k_tb2y(4x2 waves, 2 rows/wave, one round of z-chunks on large levels, LINEAR 2-step prefetch; +prolong; "
            "512-point column blocks for longer rows in every mode; from 64^3 levels; zero-iterate chunks fitted to "
-           "resident rounds; zero iterates q = +0), sweeps k_rb(ry2 w4 zc<=32 dpp nt), fused residual+restriction "
-           "(2 coarse rows per block from 2^26 points, descending z-chunks, non-temporal unshared rows), NEWTON update + "
+           "resident rounds; zero iterates q = +0; whole-wave rows without range selects (FX); LINEAR loads grouped by "
+           "field; x-edge values in VGPRs for LINEAR and the NEWTON_B whole-row plain pair), sweeps k_rb(ry2 w4 zc<=32 "
+           "dpp nt), fused residual+restriction (2 coarse rows per block from 2^26 points, descending z-chunks, halo rows "
+           "loaded first, non-temporal unshared rows), NEWTON update + "
            "compF (+ level-1 restriction, + the next factor B), NEWTON inner solves on B (GS_NEWTON_B: reciprocal "
            "quotient, shared per pair; GS_NEWTON_G: B = gamma unread), unit-neighbour stencil sums, tiled small levels, "
            "one-workgroup coarse cycle; fp-contract=off";
